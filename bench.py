@@ -1,0 +1,236 @@
+"""bench.py — forward hot path (transform + keep threshold + ordered pack) on MI355X.
+
+Workload (BASELINE.json configs[1]): 1024 synthetic 64^3 fp64 boxes per GPU,
+1 component, keep = 0.999f, inputs resident in HBM before the timed region.
+One step = one wc_forward over the whole batch (cells -> serialized payloads).
+Multi-GPU: one process per GPU; every rank compresses its own 1024 boxes
+(independent AMR units, no data-path collective) -> weak scaling.  The only
+collective is a small all-reduce of kept/byte counts after timing.
+
+Prints ONE JSON line on rank 0 (driver contract).  The CPU baseline is the
+oracle restatement (single thread) on a bounded sample of the same boxes; the
+sample's payload bytes are also compared with the GPU's ("sample_parity").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--boxes", type=int, default=1024)
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--dtype", choices=("f64", "f32"), default="f64")
+    ap.add_argument("--keep", type=float, default=0.999)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="time budget of the CPU-baseline sample (boxes run until it is spent)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_forward_r01.json"),
+                    help="PMC traffic summary (from profiles/collect_pmc.py) merged into roofline.traffic")
+    return ap.parse_args()
+
+
+def synth_device(torch, dev, nboxes, dim, dtype, rank):
+    """v = 300 + 50 sin(0.1 gx) cos(0.07 gy) + 0.01 gz + 0.05 N(0,1)  (SURVEY.md §8(d)),
+    boxes tiled over a 16 x 8 x (n/128) grid of 64^3 patches, generated on device."""
+    td = torch.float64 if dtype == "f64" else torch.float32
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + 7919 * rank)
+    n = dim
+    z = torch.arange(n, device=dev, dtype=torch.float64).view(n, 1, 1)
+    y = torch.arange(n, device=dev, dtype=torch.float64).view(1, n, 1)
+    x = torch.arange(n, device=dev, dtype=torch.float64).view(1, 1, n)
+    out = torch.empty(nboxes * n ** 3, dtype=td, device=dev)
+    for b in range(nboxes):
+        lx, ly, lz = n * (b % 16), n * ((b // 16) % 8), n * (b // 128) + 4096 * rank
+        v = 300.0 + 50.0 * torch.sin(0.1 * (x + lx)) * torch.cos(0.07 * (y + ly)) + 0.01 * (z + lz)
+        v = v + 0.05 * torch.randn((n, n, n), generator=g, device=dev, dtype=torch.float64)
+        out[b * n ** 3:(b + 1) * n ** 3] = v.reshape(-1).to(td)
+    return out
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import wcamd
+    capi = wcamd.capi
+    ctx = capi.Context(local)
+    keep = float(np.float32(args.keep))  # Config::keep is a float (src/argparse.h:13)
+    dims = [(args.dim,) * 3] * args.boxes
+    units, n, extent = capi.make_units(dims)
+    ncells = extent  # dense, 64^3 multiples: no padding
+    dtype_code = capi.WC_F64 if args.dtype == "f64" else capi.WC_F32
+    s_in = 8 if args.dtype == "f64" else 4
+
+    cells = synth_device(torch, dev, args.boxes, args.dim, args.dtype, rank)
+    cap = capi.payload_bound(units, n)
+    payload = torch.empty(cap, dtype=torch.uint8, device=dev)
+    offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    kept = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def step():
+        ctx.forward(cells.data_ptr(), dtype_code, units, n, keep, payload.data_ptr(), cap,
+                    offsets.data_ptr(), kept.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    ctx.profile_enable(True)
+    ctx.profile_read()  # reset
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ctx.profile_enable(False)
+    stages = ctx.profile_read()
+
+    elapsed = t1 - t0
+    kept_total = int(kept.sum().item())
+    payload_bytes = int(offsets[n].item())
+    stats = torch.tensor([elapsed, float(kept_total), float(payload_bytes), float(ncells)],
+                         dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = stats[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats[1:].clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed = float(mx.item())
+        kept_all, bytes_all, cells_all = (float(v) for v in sm.tolist())
+    else:
+        kept_all, bytes_all, cells_all = float(kept_total), float(payload_bytes), float(ncells)
+
+    # ---- roofline of the dominant kernel (per-launch averages from hipEvents) ----
+    per_launch = {k: (ms / cnt, cnt) for k, (ms, cnt) in stages.items()}
+    dominant = max(per_launch, key=lambda k: per_launch[k][0])
+    kept_step = kept_total  # per launch (this rank)
+    alg_bytes_stage = {
+        # algorithmic bytes each kernel owns of B = s_in*N + 8*N_kept + 20*N_units;
+        # the fp32 coefficient staging between K1 and K2 is overhead, not algorithmic traffic.
+        "transform": s_in * ncells,
+        "flat_count": 0,
+        "unit_scan": 0,
+        "unit_offsets": 20 * n,
+        "flat_emit": 8 * kept_step,
+    }
+    dom_ms = per_launch[dominant][0]
+    achieved = alg_bytes_stage.get(dominant, 0) / (dom_ms * 1e-3) / 1e9
+    path_ms = sum(v[0] for v in per_launch.values())
+    path_bytes = s_in * ncells + 8 * kept_step + 20 * n
+    traffic = None
+    pmc_path = Path(args.pmc)
+    if pmc_path.exists():
+        try:
+            pmc = json.loads(pmc_path.read_text())
+            if pmc.get("config", {}).get("boxes") == args.boxes and pmc.get("config", {}).get("dtype") == args.dtype:
+                traffic = pmc.get("per_launch_bytes", {}).get(dominant)
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": f"{'fp64' if args.dtype == 'f64' else 'fp32'} cells/s, fwd transform+threshold+pack, keep={args.keep}",
+        "value": cells_all * args.steps / elapsed,
+        "unit": "cells/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (SURVEY §8(d) field + N(0,0.05) noise, generated on device)",
+        "config": {"workload": f"{args.boxes}x{args.dim}^3 {args.dtype} boxes/GPU, 1 component, "
+                               f"keep={args.keep}f, wc_forward (payload bytes identical to reference)",
+                   "boxes_per_gpu": args.boxes, "box_dim": args.dim, "global_batch": args.boxes * world,
+                   "parallelism": f"box-sharded x{world}"},
+        "compressed_GBps": cells_all * s_in * args.steps / elapsed / 1e9,
+        "kept_fraction": kept_all / cells_all,
+        "payload_bytes_per_step": bytes_all,
+        "stage_ms_per_launch": {k: round(v[0], 4) for k, v in per_launch.items()},
+        "roofline": {
+            "bound": "hbm", "kernel": dominant,
+            "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+            "frac": achieved / PEAK_HBM_GBPS,
+            "traffic": traffic,
+        },
+        "roofline_path": {"achieved": path_bytes / (path_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS,
+                          "unit": "GB/s", "frac": path_bytes / (path_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
+                          "bytes_per_step": path_bytes, "kernel_ms_per_step": path_ms},
+        "cpu_baseline": None,
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, cells, payload, offsets, kept, s_in, keep)
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, cells, payload, offsets, kept, s_in, keep):
+    """Oracle restatement (single thread, gcc -O2) on a bounded sample of the same boxes."""
+    import numpy as np
+    from oracle import oracle as O  # checker / CPU baseline leg only
+
+    nb = args.dim ** 3
+    off = offsets.cpu().numpy()
+    kp = kept.cpu().numpy()
+    done = 0
+    t_cpu = 0.0
+    parity = True
+    scratch = None
+    while done < args.boxes and t_cpu < args.cpu_seconds:
+        box = cells[done * nb:(done + 1) * nb].cpu().numpy().reshape((args.dim,) * 3)
+        t0 = time.perf_counter()
+        b32 = O.narrow(box) if box.dtype == np.float64 else box
+        want, k = O.compress_payload(b32, keep)
+        t_cpu += time.perf_counter() - t0
+        o = int(off[done])
+        got = payload[o:o + 20 + 8 * int(kp[done])].cpu().numpy().tobytes()
+        parity &= (got == want)
+        done += 1
+    return {"value": done * nb / t_cpu, "unit": "cells/s", "cores": 1, "kind": "port",
+            "sample": f"first {done} of {args.boxes} boxes ({done * nb} cells), oracle narrow+transform+"
+                      f"threshold+RLE+serialize (no xz), {t_cpu:.1f} s",
+            "sample_parity": bool(parity)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,136 @@
+/*
+ * wavelet_amd.h — C-ABI of the MI355X (gfx950) wavelet codec.
+ *
+ * This is the drop-in boundary for the reference's per-box hot path
+ * (carsonmw3/wavelet-compression @ 2025-07-04).  The reference calls its codec
+ * through C++ functions; the C++ mirror in include/wavelet_amd/ keeps those
+ * exact signatures and forwards to the entry points below.  Each entry point
+ * names the reference routine(s) it replaces:
+ *
+ *   wc_forward         compress() minus the xz write      src/compressor.h:9-15,
+ *                      = wavelet_decompose + threshold     src/compressor.cpp:192-248
+ *                        + rle_encode + serialize          src/compressor.cpp:24-80
+ *   wc_decompose       wavelet_decompose                   src/compressor.cpp:85-185
+ *   wc_inverse         decompress() minus the xz read      src/decompressor.h:6-10
+ *                      = rle_decode + inverse transform    src/decompressor.cpp:14-30,238-255
+ *   wc_inverse_flat    inverse_wavelet_decompose           src/decompressor.h:18, .cpp:79-159
+ *   wc_rmse            calc_rmse_per_box (one component)   src/calc-loss.h:6-8, .cpp:12-43
+ *
+ * Conventions
+ *   - Plain C types only; every function returns WC_OK (0) or a WC_ERR_* code,
+ *     and wc_last_error() describes the last failure on that context.
+ *   - A "unit" is one Box3D component (one (time, level, box, component) tuple
+ *     of the reference's AMRIterator loop, src/modes.cpp:100-103): W x H x D
+ *     cells, x fastest (src/grid.h:15-19).  Batches of units run in one call.
+ *   - Functions without a _host suffix take DEVICE pointers (HBM-resident data)
+ *     and are asynchronous on the context's stream.  _host variants take host
+ *     pointers, copy through pinned staging, and return when results are ready.
+ *   - One context per device per host thread.  The context owns its stream and
+ *     its scratch memory; the caller owns every buffer it passes.
+ *
+ * Payload layout (device and host): unit u's serialized bytes, IDENTICAL to
+ * the reference's serialize_compressed_wavelet output (src/compressor.cpp:55-80)
+ *     int32 W, H, D; int32 ncoeff = W*H*D; int32 nrle; nrle x {int32 run, float32 value}
+ * start at payload + offsets[u] and are 20 + 8*kept[u] bytes long.  offsets[u]
+ * is chosen ≡ 4 (mod 8) so every pair is 8-byte aligned; the 4-byte gaps
+ * between units carry no data.  offsets[n] is the total buffer extent used.
+ */
+#ifndef WAVELET_AMD_H
+#define WAVELET_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WC_OK 0
+#define WC_ERR_INVALID 1  /* bad argument (null pointer, negative dims, capacity too small) */
+#define WC_ERR_HIP 2      /* a HIP runtime call failed */
+#define WC_ERR_NOMEM 3    /* device or pinned allocation failed */
+#define WC_ERR_FORMAT 4   /* a payload header disagrees with its unit, or a run is negative */
+
+#define WC_F32 0          /* cells are float32 (Box3D, src/box-structs.h:7) */
+#define WC_F64 1          /* cells are float64 (plotfile FAB), narrowed in-kernel (src/preprocess.cpp:78) */
+
+typedef struct wc_unit {
+    uint64_t cell_offset; /* element offset of the unit's first cell in the cell buffer */
+    int32_t nx;           /* Grid3D width  (x, fastest) */
+    int32_t ny;           /* Grid3D height (y) */
+    int32_t nz;           /* Grid3D depth  (z, slowest) */
+    int32_t reserved;     /* must be 0 */
+} wc_unit;
+
+typedef struct wc_ctx wc_ctx;
+
+/* Context lifetime.  `device` is a HIP device ordinal. */
+int wc_ctx_create(int device, wc_ctx** out);
+void wc_ctx_destroy(wc_ctx* ctx);
+const char* wc_last_error(const wc_ctx* ctx);
+
+/* Run on an external hipStream_t (e.g. a torch stream); NULL restores the
+ * context's own stream. */
+int wc_set_stream(wc_ctx* ctx, void* hip_stream);
+int wc_synchronize(wc_ctx* ctx);
+
+/* Host-side helpers (no device work). */
+uint64_t wc_payload_bound(const wc_unit* units, int n);  /* worst case: every coefficient kept */
+uint64_t wc_cell_count(const wc_unit* units, int n);
+
+/* Forward path for a batch: fp64/fp32 cells -> serialized payloads.
+ * keep: the reference's `keep` (a float widened to double, src/argparse.h:13).
+ * d_offsets: n+1 uint64, d_kept: n uint32 (both device).  payload_capacity must
+ * be >= wc_payload_bound(units, n). */
+int wc_forward(wc_ctx* ctx, const void* d_cells, int dtype, const wc_unit* units, int n,
+               double keep, uint8_t* d_payload, uint64_t payload_capacity,
+               uint64_t* d_offsets, uint32_t* d_kept);
+
+int wc_forward_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* units, int n,
+                    double keep, uint8_t* payload, uint64_t payload_capacity,
+                    uint64_t* offsets, uint32_t* kept);
+
+/* Transform only: cells -> flat fp32 coefficients (x-slowest order), written
+ * at the same element offsets as the cells (d_flat has the cell buffer's extent). */
+int wc_decompose(wc_ctx* ctx, const void* d_cells, int dtype, const wc_unit* units, int n,
+                 float* d_flat);
+
+/* Inverse path for a batch: payloads -> fp32 Box3D cells at units[u].cell_offset.
+ * Each payload header must match its unit (W,H,D, ncoeff) or WC_ERR_FORMAT. */
+int wc_inverse(wc_ctx* ctx, const uint8_t* d_payload, const uint64_t* d_offsets,
+               const wc_unit* units, int n, float* d_out);
+
+int wc_inverse_host(wc_ctx* ctx, const uint8_t* payload, const uint64_t* offsets,
+                    const wc_unit* units, int n, float* out);
+
+/* Inverse transform only: flat coefficients -> fp32 Box3D cells. */
+int wc_inverse_flat(wc_ctx* ctx, const float* d_flat, const wc_unit* units, int n, float* d_out);
+
+/* Per-unit RMSE between original cells (fp64 narrowed, or fp32) and fp32
+ * reconstructions; d_rmse: n doubles (device). */
+int wc_rmse(wc_ctx* ctx, const void* d_orig, int dtype, const float* d_regen,
+            const wc_unit* units, int n, double* d_rmse);
+
+/* Per-kernel timing with hipEvents recorded on the context stream around each
+ * launch (used by bench.py for the live roofline figure).  Stage ids below;
+ * wc_profile_read() returns the summed milliseconds and launch counts since
+ * the previous read, then resets. */
+#define WC_STAGE_TRANSFORM 0  /* K1  */
+#define WC_STAGE_COUNT 1      /* K2a */
+#define WC_STAGE_SCAN 2       /* K2b */
+#define WC_STAGE_OFFSETS 3    /* K2c */
+#define WC_STAGE_EMIT 4       /* K2d */
+#define WC_STAGE_DECODE 5     /* K5a-c */
+#define WC_STAGE_INVERSE 6    /* K6  */
+#define WC_STAGE_RMSE 7       /* K7  */
+#define WC_NUM_STAGES 8
+int wc_profile_enable(wc_ctx* ctx, int on);
+int wc_profile_read(wc_ctx* ctx, double* total_ms, uint32_t* launches, int nstages);
+
+/* Version string of the library build (arch, flags). */
+const char* wc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WAVELET_AMD_H */

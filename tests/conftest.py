@@ -1,0 +1,33 @@
+import os
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle as O
+    O.lib()
+    return O
+
+
+@pytest.fixture(scope="session")
+def wc():
+    import wcamd
+    wcamd.capi.load_library()
+    return wcamd
+
+
+@pytest.fixture(scope="session")
+def ctx(wc):
+    c = wc.capi.Context(0)
+    yield c
+    c.close()

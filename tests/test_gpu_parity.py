@@ -1,0 +1,292 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Bar: bit-exact for every integer/byte output (payload bytes => retained index
+set, run lengths and values) and for the fp32 transform / reconstruction (the
+reference's arithmetic is reproduced exactly); RMSE
+within 1e-12 relative (the reference sums sequentially in double, the GPU sums
+in a fixed tree order).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+KEEPS = [float(np.float32(k)) for k in (0.99, 0.999, 0.9999)]  # float widened, src/argparse.h:13
+
+DIMS = [
+    (2, 2, 2), (8, 4, 2), (6, 10, 14), (3, 4, 2), (3, 5, 7), (1, 1, 1), (1, 7, 1), (5, 1, 9),
+    (16, 16, 16), (32, 32, 32), (16, 32, 64), (48, 32, 16), (64, 64, 64), (4, 8, 16),
+    (33, 17, 9), (66, 2, 130), (2, 200, 3), (127, 3, 5), (40, 40, 70),
+]
+
+
+def synth(O, dims, seed0=0, sigma=0.05):
+    return [O.synth_box_f64(O.unit_seed(seed0, 0, i, 0), (3 * i, 5 * i, 7 * i), *d, sigma=sigma)
+            for i, d in enumerate(dims)]
+
+
+def pack(wc, boxes, dtype=np.float64, offsets=None):
+    dims = [(b.shape[2], b.shape[1], b.shape[0]) for b in boxes]
+    units, n, extent = wc.capi.make_units(dims, offsets=offsets)
+    cells = np.zeros(max(extent, 1), dtype)
+    for i, b in enumerate(boxes):
+        o = units[i].cell_offset
+        cells[o:o + b.size] = b.ravel().astype(dtype)
+    return units, n, extent, cells
+
+
+def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None):
+    units, n, extent, cells = pack(wc, boxes, dtype, offsets)
+    payload, offs, kept = ctx.forward_host(cells, units, n, keep)
+    return [wc.capi.unit_payload(payload, offs, kept, i) for i in range(n)], kept
+
+
+def oracle_payload(O, b, keep):
+    b32 = O.narrow(b) if b.dtype == np.float64 else b
+    return O.compress_payload(b32, keep)[0]
+
+
+@pytest.mark.parametrize("keep", KEEPS)
+def test_forward_payload_bit_exact_fp64(wc, ctx, oracle, keep):
+    boxes = synth(oracle, DIMS)
+    got, kept = gpu_payloads(wc, ctx, boxes, keep)
+    for i, b in enumerate(boxes):
+        want = oracle_payload(oracle, b, keep)
+        assert got[i] == want, f"unit {i} dims {DIMS[i]} keep {keep}"
+
+
+def test_forward_payload_bit_exact_fp32_input(wc, ctx, oracle):
+    keep = KEEPS[1]
+    boxes = [oracle.narrow(b) for b in synth(oracle, DIMS, seed0=1)]
+    got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32)
+    for i, b in enumerate(boxes):
+        assert got[i] == oracle.compress_payload(b, keep)[0], f"unit {i} dims {DIMS[i]}"
+
+
+def test_unaligned_offsets(wc, ctx, oracle):
+    """Odd cell offsets disable the vector loads; results must not change."""
+    keep = KEEPS[1]
+    dims = [(8, 8, 8), (6, 4, 2), (16, 2, 4)]
+    boxes = synth(oracle, dims, seed0=2)
+    offs = [1, 1 + 512 + 3, 1 + 512 + 3 + 48 + 5]
+    got, _ = gpu_payloads(wc, ctx, boxes, keep, offsets=offs)
+    for i, b in enumerate(boxes):
+        assert got[i] == oracle_payload(oracle, b, keep)
+
+
+def test_transform_bit_exact(wc, ctx, oracle):
+    import torch
+    boxes = [oracle.narrow(b) for b in synth(oracle, DIMS, seed0=3, sigma=3.0)]
+    units, n, extent, cells = pack(wc, boxes, np.float32)
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(cells).to(dev)
+    d_flat = torch.full((max(extent, 1),), float("nan"), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    ctx.decompose(d_in.data_ptr(), wc.capi.WC_F32, units, n, d_flat.data_ptr())
+    ctx.synchronize()
+    flat = d_flat.cpu().numpy()
+    for i, b in enumerate(boxes):
+        o = units[i].cell_offset
+        want = oracle.wavelet_decompose(b)
+        assert flat[o:o + b.size].tobytes() == want.tobytes(), f"dims {DIMS[i]}"
+
+
+def test_transform_extreme_values(wc, ctx, oracle):
+    """Denormals, huge magnitudes (overflowing float adds), signed zeros."""
+    import torch
+    rng = np.random.default_rng(7)
+    dims = [(8, 6, 4), (5, 3, 7)]
+    boxes = []
+    for (W, H, D) in dims:
+        mant = rng.standard_normal((D, H, W))
+        expo = rng.integers(-149, 128, (D, H, W))
+        b = (mant * np.exp2(expo.astype(np.float64))).astype(np.float32)
+        b[0, 0, :2] = [np.float32(1e-45), np.float32(-1e-45)]
+        b[1, 0, :2] = [np.float32(3.4e38), np.float32(3.4e38)]
+        b[0, 1, :2] = [np.float32(-0.0), np.float32(0.0)]
+        boxes.append(b)
+    units, n, extent, cells = pack(wc, boxes, np.float32)
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(cells).to(dev)
+    d_flat = torch.zeros(max(extent, 1), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    ctx.decompose(d_in.data_ptr(), wc.capi.WC_F32, units, n, d_flat.data_ptr())
+    ctx.synchronize()
+    flat = d_flat.cpu().numpy()
+    for i, b in enumerate(boxes):
+        o = units[i].cell_offset
+        assert flat[o:o + b.size].tobytes() == oracle.wavelet_decompose(b).tobytes()
+
+
+def special_boxes():
+    out = {}
+    b = np.full((4, 4, 4), 5.0, np.float32); b[1, 2, 3] = 7.5
+    out["plus5_spike"] = (b, 15)
+    out["minus5_sign_quirk"] = (np.full((4, 4, 4), -5.0, np.float32), 64)
+    out["plus5"] = (np.full((4, 4, 4), 5.0, np.float32), 8)
+    out["zeros"] = (np.zeros((4, 6, 8), np.float32), 0)
+    b = np.zeros((4, 4, 4), np.float32); b[0, 0, 0] = 3.0; b[0, 0, 1] = -3.0
+    out["tie_pm"] = (b, None)
+    b = np.full((4, 4, 4), 2.0, np.float32); b[0, 0, 0] = np.nan; b[0, 0, 1] = np.nan
+    b[0, 1, 0] = np.nan; b[0, 1, 1] = np.nan; b[1, 0, 0] = np.nan; b[1, 0, 1] = np.nan
+    b[1, 1, 0] = np.nan; b[1, 1, 1] = np.nan
+    out["nan_first"] = (b, 0)
+    b = np.full((4, 4, 4), 2.0, np.float32); b[3, 3, 3] = np.nan
+    out["nan_later"] = (b, None)
+    b = np.full((2, 2, 4), 1.0, np.float32); b[0, 0, 0] = np.inf
+    out["inf"] = (b, None)
+    b = np.full((2, 4, 2), np.float32(1e-40), np.float32); b[1, 1, 1] = np.float32(3e-39)
+    out["denormal"] = (b, None)
+    out["const_3902"] = (np.full((64, 32, 16), np.float32(3902.4), np.float32), 4096)
+    return out
+
+
+def test_special_boxes(wc, ctx, oracle):
+    keep = KEEPS[1]
+    sp = special_boxes()
+    names = list(sp)
+    got, kept = gpu_payloads(wc, ctx, [sp[k][0] for k in names], keep, dtype=np.float32)
+    for i, k in enumerate(names):
+        b, expect_kept = sp[k]
+        want, wk = oracle.compress_payload(b, keep)
+        assert got[i] == want, k
+        if expect_kept is not None:
+            assert wk == expect_kept == int(kept[i]), k
+
+
+def test_empty_and_degenerate_units(wc, ctx, oracle):
+    keep = KEEPS[1]
+    boxes = [np.zeros((0, 3, 3), np.float32), np.ones((1, 1, 1), np.float32) * 4,
+             np.zeros((3, 0, 2), np.float32), np.arange(6, dtype=np.float32).reshape(1, 1, 6)]
+    got, kept = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32)
+    for i, b in enumerate(boxes):
+        if b.size == 0:
+            D, H, W = b.shape
+            assert got[i] == np.array([W, H, D, 0, 0], "<i4").tobytes()
+        else:
+            assert got[i] == oracle.compress_payload(b, keep)[0]
+
+
+@pytest.mark.parametrize("keep", [KEEPS[0], KEEPS[2]])
+def test_inverse_bit_exact(wc, ctx, oracle, keep):
+    boxes = synth(oracle, DIMS, seed0=4)
+    units, n, extent, cells = pack(wc, boxes)
+    payload, offs, kept = ctx.forward_host(cells, units, n, keep)
+    regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
+    for i, b in enumerate(boxes):
+        o = units[i].cell_offset
+        p = wc.capi.unit_payload(payload, offs, kept, i)
+        want = oracle.decompress_payload(p).ravel()
+        assert regen[o:o + b.size].tobytes() == want.tobytes(), f"dims {DIMS[i]}"
+
+
+def test_inverse_flat_random(wc, ctx, oracle):
+    import torch
+    rng = np.random.default_rng(11)
+    dims = [(6, 10, 14), (3, 5, 7), (64, 8, 32), (2, 2, 2), (9, 9, 9)]
+    flats = [(rng.standard_normal(W * H * D) * 100).astype(np.float32) for (W, H, D) in dims]
+    units, n, extent = wc.capi.make_units(dims)
+    f = np.zeros(extent, np.float32)
+    for i, x in enumerate(flats):
+        f[units[i].cell_offset:units[i].cell_offset + x.size] = x
+    dev = torch.device("cuda", 0)
+    d_f = torch.from_numpy(f).to(dev)
+    d_o = torch.full((extent,), 123.0, dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    ctx.inverse_flat(d_f.data_ptr(), units, n, d_o.data_ptr())
+    ctx.synchronize()
+    out = d_o.cpu().numpy()
+    for i, (W, H, D) in enumerate(dims):
+        o = units[i].cell_offset
+        want = oracle.inverse_wavelet_decompose(flats[i], W, H, D).ravel()
+        assert out[o:o + W * H * D].tobytes() == want.tobytes(), dims[i]
+
+
+def test_rmse(wc, ctx, oracle):
+    import torch
+    boxes = synth(oracle, DIMS[:12], seed0=5)
+    keep = KEEPS[0]
+    units, n, extent, cells = pack(wc, boxes)
+    payload, offs, kept = ctx.forward_host(cells, units, n, keep)
+    regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
+    dev = torch.device("cuda", 0)
+    d_a = torch.from_numpy(cells).to(dev)
+    d_r = torch.from_numpy(regen).to(dev)
+    d_out = torch.zeros(n, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    ctx.rmse(d_a.data_ptr(), wc.capi.WC_F64, d_r.data_ptr(), units, n, d_out.data_ptr())
+    ctx.synchronize()
+    got = d_out.cpu().numpy()
+    for i, b in enumerate(boxes):
+        o = units[i].cell_offset
+        want = oracle.rmse(oracle.narrow(b), regen[o:o + b.size].reshape(b.shape))
+        assert got[i] == pytest.approx(want, rel=1e-12, abs=1e-300), DIMS[i]
+
+
+def test_malformed_payload_rejected(wc, ctx, oracle):
+    b = synth(oracle, [(8, 8, 8)], seed0=6)[0]
+    p = bytearray(oracle_payload(oracle, b, KEEPS[1]))
+    units, n, extent = wc.capi.make_units([(8, 8, 8)])
+    offs = np.array([4], np.uint64)
+    bad_dims = bytearray(p); bad_dims[0] = 9
+    bad_run = bytearray(p); bad_run[20:24] = np.array([-5], "<i4").tobytes()
+    for bad in (bad_dims, bad_run):
+        buf = np.zeros(len(bad) + 16, np.uint8)
+        buf[4:4 + len(bad)] = np.frombuffer(bytes(bad), np.uint8)
+        with pytest.raises(wc.WaveletError) as ei:
+            ctx.inverse_host(buf, offs, units, n, extent)
+        assert ei.value.code == wc.capi.WC_ERR_FORMAT
+
+
+def test_rle_decode_out_of_range_pairs_dropped(wc, ctx, oracle):
+    """rle_decode drops pairs whose index reaches total (src/decompressor.cpp:23)."""
+    W, H, D = 4, 2, 2
+    runs = np.array([0, 3, 10, 0], np.int32)
+    vals = np.array([1.5, 2.5, 3.5, 4.5], np.float32)
+    p = oracle.serialize(W, H, D, W * H * D, runs, vals)
+    units, n, extent = wc.capi.make_units([(W, H, D)])
+    buf = np.zeros(len(p) + 16, np.uint8)
+    buf[4:4 + len(p)] = np.frombuffer(p, np.uint8)
+    out = ctx.inverse_host(buf, np.array([4], np.uint64), units, n, extent)
+    flat = oracle.rle_decode(runs, vals, W * H * D)
+    want = oracle.inverse_wavelet_decompose(flat, W, H, D).ravel()
+    assert out.tobytes() == want.tobytes()
+
+
+def test_large_batch_64cubed_fp64(wc, ctx, oracle):
+    """64 boxes of the headline shape (64^3 fp64, keep 0.999f): every payload byte."""
+    keep = KEEPS[1]
+    dims = [(64, 64, 64)] * 64
+    boxes = [oracle.synth_box_f64(oracle.unit_seed(0, 0, i, 0), (64 * (i % 8), 64 * (i // 8), 0), 64, 64, 64)
+             for i in range(64)]
+    got, kept = gpu_payloads(wc, ctx, boxes, keep)
+    frac = kept.sum() / (64 * 64 ** 3)
+    assert 0.05 < frac < 0.95
+    for i, b in enumerate(boxes):
+        assert got[i] == oracle_payload(oracle, b, keep), i
+
+
+def test_reference_wavelet_decomposition_case(wc):
+    """Mirror of src/compressor.cpp:369-384: 4x8x16 box, round trip within 1e-6."""
+    box = np.full((16, 8, 4), 5.0, np.float32)
+    for (x, y, z, v) in [(1, 2, 3, 8.5), (2, 5, 6, 5.44), (1, 1, 1, 3.3999932),
+                         (2, 2, 2, 3.19229), (3, 5, 12, 199.39029)]:
+        box[z, y, x] = np.float32(v)
+    flat = wc.wavelet_decompose(box)
+    back = wc.inverse_wavelet_decompose(flat, 4, 8, 16)
+    assert np.all(np.abs(back - box) <= 1e-6)
+
+
+def test_reference_file_writing_case(wc, tmp_path):
+    """Mirror of src/compressor.cpp:387-406: const 5.0 box, keep 0.999, exact through xz."""
+    box = np.full((16, 8, 4), 5.0, np.float32)
+    wc.compress([box], [0], 0.999, 0, 0, 0, str(tmp_path))
+    back = wc.decompress(str(tmp_path / "compressed-wavelet-0-0-0-0.xz"), 0, 0, 0, 0)
+    assert np.array_equal(back, box)
+
+
+def test_reference_calc_rmse_case(wc):
+    """Mirror of src/calc-loss.cpp:68-86: {3.5, 3.5}."""
+    a = [np.zeros((2, 2, 2), np.float32)] * 2
+    p = [np.full((2, 2, 2), 3.5, np.float32)] * 2
+    assert wc.calc_rmse_per_box(a, p, 2) == [3.5, 3.5]

@@ -1,0 +1,234 @@
+"""ctypes binding of the C-ABI in include/wavelet_amd.h (libwavelet_amd.so).
+
+This module is the only place Python touches the native library.  It has no
+CPU fallback: loading fails loudly if the shared object is missing, and
+creating a context fails loudly if no HIP device is visible.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+from typing import Iterable, Sequence
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_DIR = PKG_DIR / "lib"
+LIB_PATH = LIB_DIR / "libwavelet_amd.so"
+HOST_LIB_PATH = LIB_DIR / "libwavelet_amd_host.so"
+
+WC_OK, WC_ERR_INVALID, WC_ERR_HIP, WC_ERR_NOMEM, WC_ERR_FORMAT = 0, 1, 2, 3, 4
+WC_F32, WC_F64 = 0, 1
+
+# Every symbol include/wavelet_amd.h declares (checked by tests/test_capi.py).
+EXPORTED = (
+    "wc_ctx_create", "wc_ctx_destroy", "wc_last_error", "wc_set_stream", "wc_synchronize",
+    "wc_payload_bound", "wc_cell_count", "wc_forward", "wc_forward_host", "wc_decompose",
+    "wc_inverse", "wc_inverse_host", "wc_inverse_flat", "wc_rmse", "wc_version",
+    "wc_profile_enable", "wc_profile_read",
+)
+
+# Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*), kernel names as rocprof shows them.
+STAGES = ("transform", "flat_count", "unit_scan", "unit_offsets", "flat_emit", "decode", "inverse", "rmse")
+
+
+class WcUnit(ctypes.Structure):
+    """wc_unit: one Box3D component, x fastest (reference src/grid.h:15-19)."""
+    _fields_ = [("cell_offset", ctypes.c_uint64), ("nx", ctypes.c_int32),
+                ("ny", ctypes.c_int32), ("nz", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class WaveletError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"wavelet_amd error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load_library() -> ctypes.CDLL:
+    """Load libwavelet_amd.so (built by __graft_entry__.build()); raise if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise FileNotFoundError(
+            f"{LIB_PATH} is missing: build the HIP extension first "
+            "(python -c 'import __graft_entry__ as g; g.build()')")
+    L = ctypes.CDLL(str(LIB_PATH))
+    vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+    up = ctypes.POINTER(WcUnit)
+    sigs = {
+        "wc_ctx_create": (i32, [i32, ctypes.POINTER(vp)]),
+        "wc_ctx_destroy": (None, [vp]),
+        "wc_last_error": (ctypes.c_char_p, [vp]),
+        "wc_set_stream": (i32, [vp, vp]),
+        "wc_synchronize": (i32, [vp]),
+        "wc_payload_bound": (u64, [up, i32]),
+        "wc_cell_count": (u64, [up, i32]),
+        "wc_forward": (i32, [vp, vp, i32, up, i32, ctypes.c_double, vp, u64, vp, vp]),
+        "wc_forward_host": (i32, [vp, vp, i32, up, i32, ctypes.c_double, vp, u64, vp, vp]),
+        "wc_decompose": (i32, [vp, vp, i32, up, i32, vp]),
+        "wc_inverse": (i32, [vp, vp, vp, up, i32, vp]),
+        "wc_inverse_host": (i32, [vp, vp, vp, up, i32, vp]),
+        "wc_inverse_flat": (i32, [vp, vp, up, i32, vp]),
+        "wc_rmse": (i32, [vp, vp, i32, vp, up, i32, vp]),
+        "wc_version": (ctypes.c_char_p, []),
+        "wc_profile_enable": (i32, [vp, i32]),
+        "wc_profile_read": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32), i32]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def make_units(dims: Sequence[Sequence[int]], offsets: Iterable[int] | None = None,
+               align: int = 4):
+    """Build a wc_unit array for boxes of `dims` = [(W, H, D), ...].
+
+    Without explicit offsets the boxes are packed back to back, each start
+    rounded up to `align` elements (vector loads stay aligned)."""
+    n = len(dims)
+    arr = (WcUnit * max(n, 1))()
+    cur = 0
+    offs = list(offsets) if offsets is not None else None
+    for i, (W, H, D) in enumerate(dims):
+        if offs is None:
+            cur = (cur + align - 1) // align * align
+            off = cur
+            cur += W * H * D
+        else:
+            off = offs[i]
+        arr[i] = WcUnit(off, W, H, D, 0)
+    extent = max((arr[i].cell_offset + arr[i].nx * arr[i].ny * arr[i].nz for i in range(n)), default=0)
+    return arr, n, int(extent)
+
+
+def payload_bound(units, n) -> int:
+    return int(load_library().wc_payload_bound(units, n))
+
+
+def _init_torch_runtime_first():
+    """torch ships its own libamdhip64.so (no SONAME) beside the system ROCm
+    runtime this library links (libamdhip64.so.7), so a process that uses both
+    holds two HIP runtimes.  Device pointers are shared fine (one KFD process),
+    but torch's runtime only finds the GPU if it initialises first — so when
+    torch is importable, initialise it before creating any wc_ctx."""
+    try:
+        import torch
+    except Exception:
+        return
+    try:
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
+
+
+class Context:
+    """One wc_ctx: a HIP device, its stream and its HBM scratch."""
+
+    def __init__(self, device: int = 0):
+        _init_torch_runtime_first()
+        L = load_library()
+        h = ctypes.c_void_p()
+        rc = L.wc_ctx_create(int(device), ctypes.byref(h))
+        if rc != WC_OK:
+            raise WaveletError(rc, f"wc_ctx_create(device={device}) failed: no usable HIP device")
+        self._h = h
+        self.device = device
+        self._L = L
+
+    def close(self):
+        if self._h:
+            self._L.wc_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != WC_OK:
+            raise WaveletError(rc, self._L.wc_last_error(self._h).decode())
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, stream_ptr: int | None):
+        self._check(self._L.wc_set_stream(self._h, ctypes.c_void_p(stream_ptr or 0)))
+
+    def synchronize(self):
+        self._check(self._L.wc_synchronize(self._h))
+
+    def profile_enable(self, on: bool = True):
+        self._check(self._L.wc_profile_enable(self._h, 1 if on else 0))
+
+    def profile_read(self) -> dict:
+        """{stage: (total_ms, launches)} since the previous read (hipEvent timing)."""
+        n = len(STAGES)
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_uint32 * n)()
+        self._check(self._L.wc_profile_read(self._h, ms, cnt, n))
+        return {STAGES[i]: (ms[i], cnt[i]) for i in range(n) if cnt[i]}
+
+    # ---- device-pointer API (torch tensors or raw ints) ------------------
+    def forward(self, d_cells: int, dtype: int, units, n: int, keep: float, d_payload: int,
+                capacity: int, d_offsets: int, d_kept: int):
+        self._check(self._L.wc_forward(self._h, ctypes.c_void_p(d_cells), dtype, units, n,
+                                       float(keep), ctypes.c_void_p(d_payload), capacity,
+                                       ctypes.c_void_p(d_offsets), ctypes.c_void_p(d_kept)))
+
+    def decompose(self, d_cells: int, dtype: int, units, n: int, d_flat: int):
+        self._check(self._L.wc_decompose(self._h, ctypes.c_void_p(d_cells), dtype, units, n,
+                                         ctypes.c_void_p(d_flat)))
+
+    def inverse(self, d_payload: int, d_offsets: int, units, n: int, d_out: int):
+        self._check(self._L.wc_inverse(self._h, ctypes.c_void_p(d_payload), ctypes.c_void_p(d_offsets),
+                                       units, n, ctypes.c_void_p(d_out)))
+
+    def inverse_flat(self, d_flat: int, units, n: int, d_out: int):
+        self._check(self._L.wc_inverse_flat(self._h, ctypes.c_void_p(d_flat), units, n,
+                                            ctypes.c_void_p(d_out)))
+
+    def rmse(self, d_orig: int, dtype: int, d_regen: int, units, n: int, d_rmse: int):
+        self._check(self._L.wc_rmse(self._h, ctypes.c_void_p(d_orig), dtype, ctypes.c_void_p(d_regen),
+                                    units, n, ctypes.c_void_p(d_rmse)))
+
+    # ---- host-array API ---------------------------------------------------
+    def forward_host(self, cells: np.ndarray, units, n: int, keep: float):
+        """cells: flat host array (float32 or float64) -> (payload bytes, offsets, kept)."""
+        c = np.ascontiguousarray(cells)
+        dtype = WC_F64 if c.dtype == np.float64 else WC_F32
+        if c.dtype not in (np.float32, np.float64):
+            raise TypeError("cells must be float32 or float64")
+        cap = payload_bound(units, n)
+        payload = np.empty(cap, np.uint8)
+        offsets = np.zeros(n + 1, np.uint64)
+        kept = np.zeros(max(n, 1), np.uint32)
+        self._check(self._L.wc_forward_host(self._h, c.ctypes.data, dtype, units, n, float(keep),
+                                            payload.ctypes.data, cap, offsets.ctypes.data,
+                                            kept.ctypes.data))
+        return payload, offsets, kept[:n]
+
+    def inverse_host(self, payload: np.ndarray, offsets: np.ndarray, units, n: int, extent: int):
+        p = np.ascontiguousarray(payload, dtype=np.uint8)
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        out = np.zeros(max(extent, 1), np.float32)
+        self._check(self._L.wc_inverse_host(self._h, p.ctypes.data, o.ctypes.data, units, n,
+                                            out.ctypes.data))
+        return out[:extent]
+
+
+def unit_payload(payload: np.ndarray, offsets: np.ndarray, kept: np.ndarray, u: int) -> bytes:
+    """Unit u's serialized bytes (reference src/compressor.cpp:55-80 layout)."""
+    o = int(offsets[u])
+    return payload[o:o + 20 + 8 * int(kept[u])].tobytes()
