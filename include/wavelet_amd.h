@@ -28,12 +28,18 @@
  *   - One context per device per host thread.  The context owns its stream and
  *     its scratch memory; the caller owns every buffer it passes.
  *
- * Payload layout (device and host): unit u's serialized bytes, IDENTICAL to
- * the reference's serialize_compressed_wavelet output (src/compressor.cpp:55-80)
+ * Payload layout: unit u's serialized bytes, IDENTICAL to the reference's
+ * serialize_compressed_wavelet output (src/compressor.cpp:55-80)
  *     int32 W, H, D; int32 ncoeff = W*H*D; int32 nrle; nrle x {int32 run, float32 value}
- * start at payload + offsets[u] and are 20 + 8*kept[u] bytes long.  offsets[u]
- * is chosen ≡ 4 (mod 8) so every pair is 8-byte aligned; the 4-byte gaps
- * between units carry no data.  offsets[n] is the total buffer extent used.
+ * start at payload + offsets[u] and are 20 + 8*kept[u] bytes long.  Every
+ * offsets[u] is == 4 (mod 8), so each pair is 8-byte aligned.
+ *   - wc_forward (device): offsets[u] is unit u's fixed SLOT, the prefix of the
+ *     worst-case sizes 24 + 8*W*H*D of the units before it (starting at 4), so
+ *     no unit waits for another's kept count; offsets[n] = end of the last
+ *     unit's bytes.  The buffer between units is not written.
+ *   - wc_forward_host: the slots are packed densely (each unit 24 + 8*kept[u]
+ *     bytes apart) before the copy back; offsets[] describe the packed buffer.
+ *   - wc_inverse / wc_inverse_host accept any offsets that are multiples of 4.
  */
 #ifndef WAVELET_AMD_H
 #define WAVELET_AMD_H
@@ -72,7 +78,15 @@ const char* wc_last_error(const wc_ctx* ctx);
 /* Run on an external hipStream_t (e.g. a torch stream); NULL restores the
  * context's own stream. */
 int wc_set_stream(wc_ctx* ctx, void* hip_stream);
-int wc_synchronize(wc_ctx* ctx);
+int wc_synchronize(wc_ctx* ctx);  /* also reports kernel-side errors of earlier async calls */
+
+/* Tuning switches.  WC_OPT_FUSED (default 0): 1 runs eligible units (even W,
+ * H, D % 8 == 0, <= 256 tiles, <= 8192 flat-row segments) through the
+ * single-read fused forward kernel; 0 uses the staged path (transform -> HBM
+ * scratch -> threshold/pack) for every unit.  Results are byte-identical
+ * either way; which is faster depends on the box size. */
+#define WC_OPT_FUSED 1
+int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 
 /* Host-side helpers (no device work). */
 uint64_t wc_payload_bound(const wc_unit* units, int n);  /* worst case: every coefficient kept */
@@ -123,7 +137,8 @@ int wc_rmse(wc_ctx* ctx, const void* d_orig, int dtype, const float* d_regen,
 #define WC_STAGE_DECODE 5     /* K5a-c */
 #define WC_STAGE_INVERSE 6    /* K6  */
 #define WC_STAGE_RMSE 7       /* K7  */
-#define WC_NUM_STAGES 8
+#define WC_STAGE_FUSED 8      /* fused single-read forward kernel */
+#define WC_NUM_STAGES 9
 int wc_profile_enable(wc_ctx* ctx, int on);
 int wc_profile_read(wc_ctx* ctx, double* total_ms, uint32_t* launches, int nstages);
 

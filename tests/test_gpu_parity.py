@@ -35,9 +35,13 @@ def pack(wc, boxes, dtype=np.float64, offsets=None):
     return units, n, extent, cells
 
 
-def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None):
+def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None, fused=True):
     units, n, extent, cells = pack(wc, boxes, dtype, offsets)
-    payload, offs, kept = ctx.forward_host(cells, units, n, keep)
+    ctx.set_fused(fused)
+    try:
+        payload, offs, kept = ctx.forward_host(cells, units, n, keep)
+    finally:
+        ctx.set_fused(False)
     return [wc.capi.unit_payload(payload, offs, kept, i) for i in range(n)], kept
 
 
@@ -46,30 +50,36 @@ def oracle_payload(O, b, keep):
     return O.compress_payload(b32, keep)[0]
 
 
+PATHS = [pytest.param(True, id="fused"), pytest.param(False, id="staged")]
+
+
+@pytest.mark.parametrize("fused", PATHS)
 @pytest.mark.parametrize("keep", KEEPS)
-def test_forward_payload_bit_exact_fp64(wc, ctx, oracle, keep):
+def test_forward_payload_bit_exact_fp64(wc, ctx, oracle, keep, fused):
     boxes = synth(oracle, DIMS)
-    got, kept = gpu_payloads(wc, ctx, boxes, keep)
+    got, kept = gpu_payloads(wc, ctx, boxes, keep, fused=fused)
     for i, b in enumerate(boxes):
         want = oracle_payload(oracle, b, keep)
         assert got[i] == want, f"unit {i} dims {DIMS[i]} keep {keep}"
 
 
-def test_forward_payload_bit_exact_fp32_input(wc, ctx, oracle):
+@pytest.mark.parametrize("fused", PATHS)
+def test_forward_payload_bit_exact_fp32_input(wc, ctx, oracle, fused):
     keep = KEEPS[1]
     boxes = [oracle.narrow(b) for b in synth(oracle, DIMS, seed0=1)]
-    got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32)
+    got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, fused=fused)
     for i, b in enumerate(boxes):
         assert got[i] == oracle.compress_payload(b, keep)[0], f"unit {i} dims {DIMS[i]}"
 
 
-def test_unaligned_offsets(wc, ctx, oracle):
+@pytest.mark.parametrize("fused", PATHS)
+def test_unaligned_offsets(wc, ctx, oracle, fused):
     """Odd cell offsets disable the vector loads; results must not change."""
     keep = KEEPS[1]
-    dims = [(8, 8, 8), (6, 4, 2), (16, 2, 4)]
+    dims = [(8, 8, 8), (6, 4, 2), (16, 2, 4), (4, 4, 16)]
     boxes = synth(oracle, dims, seed0=2)
-    offs = [1, 1 + 512 + 3, 1 + 512 + 3 + 48 + 5]
-    got, _ = gpu_payloads(wc, ctx, boxes, keep, offsets=offs)
+    offs = [1, 1 + 512 + 3, 1 + 512 + 3 + 48 + 5, 1 + 512 + 3 + 48 + 5 + 128 + 7]
+    got, _ = gpu_payloads(wc, ctx, boxes, keep, offsets=offs, fused=fused)
     for i, b in enumerate(boxes):
         assert got[i] == oracle_payload(oracle, b, keep)
 
@@ -138,14 +148,32 @@ def special_boxes():
     b = np.full((2, 4, 2), np.float32(1e-40), np.float32); b[1, 1, 1] = np.float32(3e-39)
     out["denormal"] = (b, None)
     out["const_3902"] = (np.full((64, 32, 16), np.float32(3902.4), np.float32), 4096)
+    # the same quirks on fused-eligible shapes (even W, H and D % 8 == 0)
+    b = np.full((8, 4, 4), 5.0, np.float32); b[5, 2, 3] = 7.5
+    out["plus5_spike_f"] = (b, 23)
+    out["minus5_sign_quirk_f"] = (np.full((8, 4, 4), -5.0, np.float32), 128)
+    out["zeros_f"] = (np.zeros((16, 6, 8), np.float32), 0)
+    b = np.zeros((8, 4, 4), np.float32); b[3, 2, 2] = 3.0; b[3, 2, 3] = -3.0; b[7, 3, 1] = -3.0
+    out["tie_pm_f"] = (b, None)
+    b = np.full((8, 4, 4), 2.0, np.float32); b[:2, :2, :2] = np.nan
+    out["nan_first_f"] = (b, 0)
+    b = np.full((8, 4, 4), 2.0, np.float32); b[7, 3, 3] = np.nan
+    out["nan_later_f"] = (b, None)
+    b = np.full((8, 2, 2), 1.0, np.float32); b[4, 0, 0] = -np.inf
+    out["inf_f"] = (b, None)
+    b = np.full((8, 4, 2), np.float32(1e-40), np.float32); b[6, 1, 1] = np.float32(-3e-39)
+    out["denormal_f"] = (b, None)
+    b = np.full((16, 8, 8), 1.0, np.float32); b[9, 7, 6] = -50.0
+    out["neg_max_f"] = (b, None)
     return out
 
 
-def test_special_boxes(wc, ctx, oracle):
+@pytest.mark.parametrize("fused", PATHS)
+def test_special_boxes(wc, ctx, oracle, fused):
     keep = KEEPS[1]
     sp = special_boxes()
     names = list(sp)
-    got, kept = gpu_payloads(wc, ctx, [sp[k][0] for k in names], keep, dtype=np.float32)
+    got, kept = gpu_payloads(wc, ctx, [sp[k][0] for k in names], keep, dtype=np.float32, fused=fused)
     for i, k in enumerate(names):
         b, expect_kept = sp[k]
         want, wk = oracle.compress_payload(b, keep)
@@ -253,17 +281,30 @@ def test_rle_decode_out_of_range_pairs_dropped(wc, ctx, oracle):
     assert out.tobytes() == want.tobytes()
 
 
-def test_large_batch_64cubed_fp64(wc, ctx, oracle):
+@pytest.mark.parametrize("fused", PATHS)
+def test_large_batch_64cubed_fp64(wc, ctx, oracle, fused):
     """64 boxes of the headline shape (64^3 fp64, keep 0.999f): every payload byte."""
     keep = KEEPS[1]
     dims = [(64, 64, 64)] * 64
     boxes = [oracle.synth_box_f64(oracle.unit_seed(0, 0, i, 0), (64 * (i % 8), 64 * (i // 8), 0), 64, 64, 64)
              for i in range(64)]
-    got, kept = gpu_payloads(wc, ctx, boxes, keep)
+    got, kept = gpu_payloads(wc, ctx, boxes, keep, fused=fused)
     frac = kept.sum() / (64 * 64 ** 3)
     assert 0.05 < frac < 0.95
     for i, b in enumerate(boxes):
         assert got[i] == oracle_payload(oracle, b, keep), i
+
+
+@pytest.mark.parametrize("fused", PATHS)
+def test_128cubed_fp32_and_mixed_sizes(wc, ctx, oracle, fused):
+    """C5 shape (128^3 fp32, keep 0.9999f: 256 fused tiles per unit) beside
+    AMR-style mixed boxes in one batch."""
+    keep = KEEPS[2]
+    dims = [(128, 128, 128), (32, 32, 32), (16, 16, 16), (48, 32, 16), (64, 64, 64), (128, 64, 32)]
+    boxes = [oracle.narrow(b) for b in synth(oracle, dims, seed0=8)]
+    got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, fused=fused)
+    for i, b in enumerate(boxes):
+        assert got[i] == oracle.compress_payload(b, keep)[0], dims[i]
 
 
 def test_reference_wavelet_decomposition_case(wc):

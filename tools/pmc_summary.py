@@ -1,0 +1,79 @@
+"""Summarise rocprofv3 CSV output for profiles/.
+
+usage: python tools/pmc_summary.py <kernel_stats.csv> [--fetch fetch_counter_collection.csv]
+                                   [--write write_counter_collection.csv] [--out profiles/x.json]
+                                   [--boxes N --dtype f64]
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  Per MI355X_MICROARCH.md §HBM,
+on gfx950 FETCH_SIZE reads exactly 1/2 of a wide coalesced stream's bytes, so
+read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE reads the bytes exactly for
+16-B-per-lane stores.  Both are averaged per launch of each kernel.
+"""
+import argparse
+import csv
+import json
+import re
+from collections import defaultdict
+
+STAGE_OF = [("k_transform", "transform"), ("k_flat_count", "flat_count"), ("k_unit_scan", "unit_scan"),
+            ("k_unit_offsets", "unit_offsets"), ("k_flat_emit", "flat_emit"),
+            ("k_decode", "decode"), ("k_inverse", "inverse"), ("k_rmse", "rmse"),
+            ("k_fwd", "transform")]
+
+
+def stage(name):
+    for pat, st in STAGE_OF:
+        if pat in name:
+            return st
+    return None
+
+
+def counters(path, counter):
+    acc = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row.get("Counter_Name") != counter:
+                continue
+            st = stage(row.get("Kernel_Name", ""))
+            if st:
+                acc[st].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("stats")
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--out")
+    ap.add_argument("--boxes", type=int, default=1024)
+    ap.add_argument("--dtype", default="f64")
+    a = ap.parse_args()
+    kern = {}
+    with open(a.stats) as f:
+        for row in csv.DictReader(f):
+            st = stage(row["Name"])
+            if st:
+                kern[st] = {"name": row["Name"][:80], "calls": int(row["Calls"]),
+                            "avg_us": float(row["AverageNs"]) / 1e3, "pct": float(row["Percentage"])}
+    out = {"config": {"boxes": a.boxes, "dtype": a.dtype}, "kernels": kern}
+    per = {}
+    if a.fetch:
+        fk = counters(a.fetch, "FETCH_SIZE")
+        for k, v in fk.items():
+            per.setdefault(k, {})["read_bytes"] = 2 * v * 1024
+    if a.write:
+        wk = counters(a.write, "WRITE_SIZE")
+        for k, v in wk.items():
+            per.setdefault(k, {})["write_bytes"] = v * 1024
+    if per:
+        out["pmc_per_launch"] = per
+        out["per_launch_bytes"] = {k: v.get("read_bytes", 0) + v.get("write_bytes", 0) for k, v in per.items()}
+    s = json.dumps(out, indent=1)
+    if a.out:
+        open(a.out, "w").write(s + "\n")
+    print(s)
+
+
+if __name__ == "__main__":
+    main()

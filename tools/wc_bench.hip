@@ -1,0 +1,195 @@
+// wc_bench — torch-free C++ driver of the C-ABI, for rocprofv3 (--pmc) runs.
+//
+// Same workload as bench.py (N boxes of D^3, fp64 or fp32, keep 0.999f): the
+// synthetic field of SURVEY.md §8(d) is generated on the device (hash-based
+// Box-Muller noise), then wc_forward runs `steps` times.  Prints one JSON line.
+//
+// usage: wc_bench [boxes=1024] [dim=64] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1]
+//                 [fused=0|1] [check=0|1]
+// check=1: also run the staged path once and compare every unit's payload
+// bytes with the fused path's ("paths_identical" in the JSON line).
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "wavelet_amd.h"
+
+#define CK(x)                                                                                \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) {                                                              \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            std::exit(2);                                                                    \
+        }                                                                                    \
+    } while (0)
+
+__device__ inline unsigned long long mix64(unsigned long long z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+template <typename T>
+__global__ void synth(T* out, int dim, long long nboxes, unsigned long long seed) {
+    const long long per = (long long)dim * dim * dim;
+    const long long total = per * nboxes;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long b = i / per, r = i % per;
+        const int x = (int)(r % dim), y = (int)((r / dim) % dim), z = (int)(r / ((long long)dim * dim));
+        const double gx = dim * (b % 16) + x, gy = dim * ((b / 16) % 8) + y, gz = dim * (b / 128) + z;
+        const unsigned long long h1 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * i + 1));
+        const unsigned long long h2 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * i + 2));
+        const double u1 = ((double)(h1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);
+        const double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
+        const double g = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+        out[i] = (T)(300.0 + 50.0 * sin(0.1 * gx) * cos(0.07 * gy) + 0.01 * gz + 0.05 * g);
+    }
+}
+
+int main(int argc, char** argv) {
+    const int boxes = argc > 1 ? std::atoi(argv[1]) : 1024;
+    const int dim = argc > 2 ? std::atoi(argv[2]) : 64;
+    const bool f64 = argc > 3 ? std::strcmp(argv[3], "f32") != 0 : true;
+    const double keep = (double)(float)(argc > 4 ? std::atof(argv[4]) : 0.999);
+    const int steps = argc > 5 ? std::atoi(argv[5]) : 10;
+    const int warmup = argc > 6 ? std::atoi(argv[6]) : 2;
+    const bool inverse = argc > 7 ? std::atoi(argv[7]) != 0 : false;
+    const bool fused = argc > 8 ? std::atoi(argv[8]) != 0 : false;
+    const bool check = argc > 9 ? std::atoi(argv[9]) != 0 : false;
+
+    std::vector<wc_unit> units(boxes);
+    const unsigned long long per = (unsigned long long)dim * dim * dim;
+    for (int i = 0; i < boxes; ++i) units[i] = wc_unit{per * i, dim, dim, dim, 0};
+    const size_t esz = f64 ? 8 : 4;
+    void* cells = nullptr;
+    CK(hipMalloc(&cells, esz * per * boxes));
+    if (f64)
+        synth<double><<<4096, 256>>>((double*)cells, dim, boxes, 1234);
+    else
+        synth<float><<<4096, 256>>>((float*)cells, dim, boxes, 1234);
+    CK(hipDeviceSynchronize());
+
+    const uint64_t cap = wc_payload_bound(units.data(), boxes);
+    uint8_t* payload = nullptr;
+    uint64_t* offsets = nullptr;
+    uint32_t* kept = nullptr;
+    float* regen = nullptr;
+    CK(hipMalloc(&payload, cap));
+    CK(hipMalloc(&offsets, 8 * (boxes + 1)));
+    CK(hipMalloc(&kept, 4 * boxes));
+    if (inverse) CK(hipMalloc(&regen, 4 * per * boxes));
+
+    wc_ctx* ctx = nullptr;
+    if (wc_ctx_create(0, &ctx) != WC_OK) {
+        std::fprintf(stderr, "wc_ctx_create failed\n");
+        return 2;
+    }
+    wc_set_option(ctx, WC_OPT_FUSED, fused ? 1 : 0);
+    auto fwd = [&]() {
+        int rc = wc_forward(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, keep, payload, cap, offsets, kept);
+        if (rc != WC_OK) {
+            std::fprintf(stderr, "wc_forward: %s\n", wc_last_error(ctx));
+            std::exit(2);
+        }
+    };
+    auto inv = [&]() {
+        int rc = wc_inverse(ctx, payload, offsets, units.data(), boxes, regen);
+        if (rc != WC_OK) {
+            std::fprintf(stderr, "wc_inverse: %s\n", wc_last_error(ctx));
+            std::exit(2);
+        }
+    };
+    for (int i = 0; i < warmup; ++i) {
+        fwd();
+        if (inverse) inv();
+    }
+    wc_synchronize(ctx);
+    wc_profile_enable(ctx, 1);
+    double ms[WC_NUM_STAGES];
+    uint32_t cnt[WC_NUM_STAGES];
+    wc_profile_read(ctx, ms, cnt, WC_NUM_STAGES);
+    auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < steps; ++i) fwd();
+    wc_synchronize(ctx);
+    auto t1 = std::chrono::steady_clock::now();
+    wc_profile_read(ctx, ms, cnt, WC_NUM_STAGES);
+    double inv_ms = 0;
+    double ims[WC_NUM_STAGES];
+    uint32_t icnt[WC_NUM_STAGES];
+    if (inverse) {
+        auto a = std::chrono::steady_clock::now();
+        for (int i = 0; i < steps; ++i) inv();
+        auto b = std::chrono::steady_clock::now();
+        inv_ms = std::chrono::duration<double, std::milli>(b - a).count() / steps;
+        wc_profile_read(ctx, ims, icnt, WC_NUM_STAGES);
+    }
+    const double step_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() / steps;
+    int identical = -1;
+    if (check) {
+        // Fused vs staged: every unit's serialized bytes must match.
+        std::vector<uint64_t> off_a(boxes + 1), off_b(boxes + 1);
+        std::vector<uint32_t> k_a(boxes), k_b(boxes);
+        std::vector<uint8_t> pa(cap), pb(cap);
+        wc_set_option(ctx, WC_OPT_FUSED, 1);
+        fwd();
+        wc_synchronize(ctx);
+        CK(hipMemcpy(off_a.data(), offsets, 8 * (boxes + 1), hipMemcpyDeviceToHost));
+        CK(hipMemcpy(k_a.data(), kept, 4 * boxes, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(pa.data(), payload, cap, hipMemcpyDeviceToHost));
+        CK(hipMemset(payload, 0xA5, cap));
+        wc_set_option(ctx, WC_OPT_FUSED, 0);
+        fwd();
+        wc_synchronize(ctx);
+        CK(hipMemcpy(off_b.data(), offsets, 8 * (boxes + 1), hipMemcpyDeviceToHost));
+        CK(hipMemcpy(k_b.data(), kept, 4 * boxes, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(pb.data(), payload, cap, hipMemcpyDeviceToHost));
+        identical = 1;
+        for (int i = 0; i < boxes && identical; ++i) {
+            if (k_a[i] != k_b[i] || off_a[i] != off_b[i]) identical = 0;
+            else if (std::memcmp(pa.data() + off_a[i], pb.data() + off_b[i], 20 + 8ull * k_a[i]) != 0) identical = 0;
+        }
+        wc_set_option(ctx, WC_OPT_FUSED, fused ? 1 : 0);
+    }
+    uint64_t total = 0;
+    CK(hipMemcpy(&total, offsets + boxes, 8, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> hk(boxes);
+    CK(hipMemcpy(hk.data(), kept, 4 * boxes, hipMemcpyDeviceToHost));
+    double ksum = 0;
+    for (uint32_t k : hk) ksum += k;
+    const char* names[WC_NUM_STAGES] = {"transform", "flat_count", "unit_scan", "unit_offsets",
+                                        "flat_emit", "decode", "inverse", "rmse", "fused"};
+    std::printf("{\"boxes\": %d, \"dim\": %d, \"dtype\": \"%s\", \"keep\": %.17g, \"steps\": %d, "
+                "\"ms_per_step\": %.4f, \"cells_per_s\": %.6e, \"kept_fraction\": %.6f, \"payload_bytes\": %llu, "
+                "\"fused\": %d, \"paths_identical\": %d, \"stage_ms\": {",
+                boxes, dim, f64 ? "f64" : "f32", keep, steps, step_ms, per * boxes / (step_ms * 1e-3),
+                ksum / (double)(per * boxes), (unsigned long long)total, fused ? 1 : 0, identical);
+    bool first = true;
+    for (int s = 0; s < WC_NUM_STAGES; ++s)
+        if (cnt[s]) {
+            std::printf("%s\"%s\": %.4f", first ? "" : ", ", names[s], ms[s] / cnt[s]);
+            first = false;
+        }
+    if (inverse) {
+        std::printf("}, \"inverse_ms_per_step\": %.4f, \"inverse_stage_ms\": {", inv_ms);
+        first = true;
+        for (int s = 0; s < WC_NUM_STAGES; ++s)
+            if (icnt[s]) {
+                std::printf("%s\"%s\": %.4f", first ? "" : ", ", names[s], ims[s] / icnt[s]);
+                first = false;
+            }
+    }
+    std::printf("}}\n");
+    wc_ctx_destroy(ctx);
+    (void)hipFree(cells);
+    (void)hipFree(payload);
+    (void)hipFree(offsets);
+    (void)hipFree(kept);
+    if (regen) (void)hipFree(regen);
+    return 0;
+}

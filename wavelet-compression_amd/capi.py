@@ -26,11 +26,13 @@ EXPORTED = (
     "wc_ctx_create", "wc_ctx_destroy", "wc_last_error", "wc_set_stream", "wc_synchronize",
     "wc_payload_bound", "wc_cell_count", "wc_forward", "wc_forward_host", "wc_decompose",
     "wc_inverse", "wc_inverse_host", "wc_inverse_flat", "wc_rmse", "wc_version",
-    "wc_profile_enable", "wc_profile_read",
+    "wc_profile_enable", "wc_profile_read", "wc_set_option",
 )
+WC_OPT_FUSED = 1
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*), kernel names as rocprof shows them.
-STAGES = ("transform", "flat_count", "unit_scan", "unit_offsets", "flat_emit", "decode", "inverse", "rmse")
+STAGES = ("transform", "flat_count", "unit_scan", "unit_offsets", "flat_emit", "decode", "inverse", "rmse",
+          "fused")
 
 
 class WcUnit(ctypes.Structure):
@@ -57,6 +59,7 @@ def load_library() -> ctypes.CDLL:
         raise FileNotFoundError(
             f"{LIB_PATH} is missing: build the HIP extension first "
             "(python -c 'import __graft_entry__ as g; g.build()')")
+    _share_torch_runtime()
     L = ctypes.CDLL(str(LIB_PATH))
     vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
     up = ctypes.POINTER(WcUnit)
@@ -77,6 +80,7 @@ def load_library() -> ctypes.CDLL:
         "wc_rmse": (i32, [vp, vp, i32, vp, up, i32, vp]),
         "wc_version": (ctypes.c_char_p, []),
         "wc_profile_enable": (i32, [vp, i32]),
+        "wc_set_option": (i32, [vp, i32, ctypes.c_int64]),
         "wc_profile_read": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32), i32]),
     }
     for name, (res, args) in sigs.items():
@@ -113,19 +117,19 @@ def payload_bound(units, n) -> int:
     return int(load_library().wc_payload_bound(units, n))
 
 
-def _init_torch_runtime_first():
-    """torch ships its own libamdhip64.so (no SONAME) beside the system ROCm
-    runtime this library links (libamdhip64.so.7), so a process that uses both
-    holds two HIP runtimes.  Device pointers are shared fine (one KFD process),
-    but torch's runtime only finds the GPU if it initialises first — so when
-    torch is importable, initialise it before creating any wc_ctx."""
-    try:
-        import torch
-    except Exception:
+def _share_torch_runtime():
+    """torch ships its own HIP runtime (torch/lib/libamdhip64.so, SONAME
+    libamdhip64.so.7, ROCm 7.0) beside the system one this library links
+    (/opt/rocm/lib/libamdhip64.so.7).  If torch is loaded first, the dynamic
+    loader resolves our NEEDED libamdhip64.so.7 to torch's copy and the process
+    has ONE HIP runtime; loaded the other way round there would be two, and
+    only the first to initialise gets the GPU.  So import torch (if present)
+    before dlopen-ing the library.  Set WCAMD_NO_TORCH=1 to skip (torch-free
+    processes then use the system ROCm runtime)."""
+    if os.environ.get("WCAMD_NO_TORCH") == "1":
         return
     try:
-        if torch.cuda.is_available():
-            torch.cuda.init()
+        import torch  # noqa: F401
     except Exception:
         pass
 
@@ -134,7 +138,6 @@ class Context:
     """One wc_ctx: a HIP device, its stream and its HBM scratch."""
 
     def __init__(self, device: int = 0):
-        _init_torch_runtime_first()
         L = load_library()
         h = ctypes.c_void_p()
         rc = L.wc_ctx_create(int(device), ctypes.byref(h))
@@ -168,6 +171,13 @@ class Context:
 
     def synchronize(self):
         self._check(self._L.wc_synchronize(self._h))
+
+    def set_option(self, option: int, value: int):
+        self._check(self._L.wc_set_option(self._h, int(option), int(value)))
+
+    def set_fused(self, on: bool):
+        """Route eligible units through the fused single-read kernel (default off)."""
+        self.set_option(WC_OPT_FUSED, 1 if on else 0)
 
     def profile_enable(self, on: bool = True):
         self._check(self._L.wc_profile_enable(self._h, 1 if on else 0))

@@ -28,7 +28,12 @@ struct UnitDev {
     int32_t lbx, lby, lbz;  // log2 of the transform tile shape in blocks
     uint32_t ftile_begin;   // first flat (threshold/compaction) tile of this unit
     uint32_t nftiles;       // number of flat tiles = ceil(ncells / kFlatTile)
-    int32_t pad0, pad1;
+    uint64_t pay_off;       // payload slot: prefix of worst-case sizes, == 4 (mod 8)
+    uint64_t seg_off;       // fused units: first segment record
+    uint32_t xt_begin;      // fused units: first tile in the fused tile list
+    uint32_t ntile_u;       // fused units: tiles G of this unit
+    int32_t ntz;            // z tiles per unit (segments per flat row half)
+    int32_t fused;          // 1: handled by k_forward_fused, 0: staged path
 };
 
 // A transform tile: a (1<<lbx) x (1<<lby) x (1<<lbz) box of 2x2x2 blocks.
@@ -51,5 +56,33 @@ constexpr unsigned long long kKeyNaNFirst = ~0ull;
 constexpr uint32_t kErrHeader = 1u;      // payload header disagrees with the unit
 constexpr uint32_t kErrNegativeRun = 2u; // a run length < 0 (reference: UB)
 constexpr uint32_t kErrTooManyPairs = 4u;// nrle > ncoeff
+constexpr uint32_t kErrTimeout = 8u;     // a fused-kernel hand-off wait hit its bound
+
+// The fused forward kernel keeps a unit's G tiles co-resident; cap G well
+// below the resident grid (>= 1024 tiles of 256 threads on 256 CUs).
+constexpr uint32_t kMaxFusedTiles = 256;
+// ... and its segment count (flat-row pieces) to what one workgroup scans with
+// 32 records in flight per thread.
+constexpr uint64_t kMaxFusedSegments = 256 * 32;
+
+// Parameter block of k_forward_fused (wc_fused.hip), filled by wc_capi.cpp.
+struct FusedParams {
+    const void* cells;
+    const UnitDev* units;
+    const XTile* tiles;           // fused tiles, unit-major
+    uint32_t ntiles;
+    int n;
+    uint32_t* ticket;             // zeroed per call
+    uint32_t* arrive;             // [n], zeroed per call
+    uint32_t* ready;              // [n], zeroed per call
+    unsigned long long* keyslot;  // [ntiles], zeroed per call
+    uint32_t* segrec;             // segment records: count | (last + 1) << 8
+    uint2* segoff;                // per segment: (pair offset, previous kept flat index + 1)
+    uint8_t* payload;
+    uint64_t* offsets;            // [n + 1]
+    uint32_t* kept;               // [n]
+    uint32_t* err;
+    double keep;
+};
 
 }  // namespace wc
