@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="time budget of the CPU-baseline sample (boxes run until it is spent)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_forward_r01.json"),
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r01" / "pmc_forward_staged.json"),
                     help="PMC traffic summary (from profiles/collect_pmc.py) merged into roofline.traffic")
     return ap.parse_args()
 
@@ -121,18 +121,14 @@ def main():
 
     elapsed = t1 - t0
     kept_total = int(kept.sum().item())
-    payload_bytes = int(offsets[n].item())
-    stats = torch.tensor([elapsed, float(kept_total), float(payload_bytes), float(ncells)],
-                         dtype=torch.float64, device=dev)
+    payload_bytes = int(kept.to(torch.int64).sum().item()) * 8 + 20 * n  # serialized bytes (slots excluded)
+    local = {"seconds": elapsed, "kept": kept_total, "payload_bytes": payload_bytes, "cells": ncells}
     if world > 1:
-        mx = stats[:1].clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = stats[1:].clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed = float(mx.item())
-        kept_all, bytes_all, cells_all = (float(v) for v in sm.tolist())
-    else:
-        kept_all, bytes_all, cells_all = float(kept_total), float(payload_bytes), float(ncells)
+        # the one collective: run metrics (a few bytes) over RCCL, after timing
+        from wavelet_compression_amd.shard import reduce_metrics
+        local = reduce_metrics(local, device=dev)
+    elapsed = local["seconds"]
+    kept_all, bytes_all, cells_all = local["kept"], local["payload_bytes"], local["cells"]
 
     # ---- roofline of the dominant kernel (per-launch averages from hipEvents) ----
     per_launch = {k: (ms / cnt, cnt) for k, (ms, cnt) in stages.items()}

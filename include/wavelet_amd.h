@@ -119,11 +119,18 @@ int wc_inverse_host(wc_ctx* ctx, const uint8_t* payload, const uint64_t* offsets
 
 /* Inverse transform only: flat coefficients -> fp32 Box3D cells. */
 int wc_inverse_flat(wc_ctx* ctx, const float* d_flat, const wc_unit* units, int n, float* d_out);
+int wc_inverse_flat_host(wc_ctx* ctx, const float* flat, const wc_unit* units, int n, float* out);
 
 /* Per-unit RMSE between original cells (fp64 narrowed, or fp32) and fp32
  * reconstructions; d_rmse: n doubles (device). */
 int wc_rmse(wc_ctx* ctx, const void* d_orig, int dtype, const float* d_regen,
             const wc_unit* units, int n, double* d_rmse);
+int wc_rmse_host(wc_ctx* ctx, const void* orig, int dtype, const float* regen,
+                 const wc_unit* units, int n, double* rmse);
+
+/* Transform only, host pointers (the reference's static wavelet_decompose). */
+int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* units, int n,
+                      float* flat);
 
 /* Per-kernel timing with hipEvents recorded on the context stream around each
  * launch (used by bench.py for the live roofline figure).  Stage ids below;

@@ -1,0 +1,78 @@
+"""The C-ABI library loads on a CPU-only host and exports every entry point
+include/wavelet_amd.h declares; host-only helpers and argument checks work
+without a GPU.  No compute call is made here (those are the -m gpu tests)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def declared_functions():
+    text = (ROOT / "include" / "wavelet_amd.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(wc_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_declares_expected_entry_points(wc):
+    decl = declared_functions()
+    assert "wc_forward" in decl and "wc_inverse" in decl and "wc_rmse" in decl
+    assert set(decl) == set(wc.capi.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol(wc):
+    lib = wc.capi.load_library()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+
+
+def test_shared_object_dynamic_symbols(wc):
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", str(wc.capi.LIB_PATH)], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (wc_\w+)", out))
+    assert set(declared_functions()) <= exported
+    # only the boundary is exported with C linkage: no stray unmangled wc_ symbols
+    assert exported == set(declared_functions())
+
+
+def test_library_is_built_for_gfx950(wc):
+    blob = wc.capi.LIB_PATH.read_bytes()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_host_helpers(wc):
+    units, n, extent = wc.capi.make_units([(64, 64, 64), (8, 4, 2), (3, 5, 7)])
+    L = wc.capi.load_library()
+    assert L.wc_cell_count(units, n) == 64 ** 3 + 64 + 105
+    assert L.wc_payload_bound(units, n) == 4 + sum(24 + 8 * c for c in (64 ** 3, 64, 105))
+    assert units[1].cell_offset % 4 == 0 and units[2].cell_offset % 4 == 0
+    assert L.wc_version().startswith(b"wavelet_amd")
+
+
+def test_null_context_is_rejected(wc):
+    L = wc.capi.load_library()
+    units, n, _ = wc.capi.make_units([(4, 4, 4)])
+    assert L.wc_forward(None, None, 0, units, n, 0.999, None, 0, None, None) == wc.capi.WC_ERR_INVALID
+    assert L.wc_inverse(None, None, None, units, n, None) == wc.capi.WC_ERR_INVALID
+    assert L.wc_set_option(None, 1, 0) == wc.capi.WC_ERR_INVALID
+    assert L.wc_last_error(None) == b"null context"
+
+
+def test_context_creation_without_gpu_fails_loudly(wc):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(wc.WaveletError):
+        wc.capi.Context(0)
+
+
+def test_package_has_no_cpu_fallback():
+    """The product never imports the oracle (test infrastructure only)."""
+    pkg = ROOT / "wavelet-compression_amd"
+    for f in list(pkg.glob("*.py")) + list((pkg / "csrc").rglob("*")):
+        if f.is_file() and f.suffix in (".py", ".cpp", ".hip", ".h"):
+            text = f.read_text()
+            assert "oracle" not in text.replace("oracle/", "").lower() or f.name == "__init__.py", f

@@ -1,0 +1,90 @@
+"""Multi-rank sharding on CPU (gloo, world_size 2): the unit partition, the
+metrics all-reduce and that a sharded run reproduces the single-process
+payloads.  The per-unit compute here is the CPU oracle (these ranks have no
+GPU); the GPU ranks of bench.py use the same plan_shards / reduce_metrics."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+def test_plan_shards_contiguous_and_balanced(wc):
+    from wavelet_compression_amd.shard import plan_shards
+    counts = [64 ** 3] * 64 + [32 ** 3] * 96 + [16 ** 3] * 256
+    for world in (1, 2, 4, 8):
+        sh = plan_shards(counts, world)
+        assert sh[0][0] == 0 and sh[-1][1] == len(counts)
+        assert all(a[1] == b[0] for a, b in zip(sh, sh[1:]))
+        loads = [sum(counts[a:b]) for a, b in sh]
+        assert max(loads) - sum(counts) / world <= max(counts)
+    assert plan_shards([5], 4) == [(0, 0), (0, 0), (0, 1), (1, 1)] or \
+        sum(b - a for a, b in plan_shards([5], 4)) == 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, dims, keep, out_q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(root))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WCAMD_NO_TORCH="1")
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import wcamd
+    from wavelet_compression_amd.shard import plan_shards, reduce_metrics
+    from oracle import oracle as O
+    counts = [w * h * d for (w, h, d) in dims]
+    a, b = plan_shards(counts, world)[rank]
+    payloads, kept = {}, 0
+    for u in range(a, b):
+        cells = O.synth_box_f64(O.unit_seed(0, 0, u, 0), (0, 0, 0), *dims[u])
+        p, k = O.compress_payload(O.narrow(cells), keep)
+        payloads[u] = p
+        kept += k
+    m = reduce_metrics({"cells": sum(counts[a:b]), "kept": kept, "boxes": b - a,
+                        "payload_bytes": sum(len(p) for p in payloads.values()),
+                        "seconds": 0.1 * (rank + 1), "min_value": float(rank), "max_value": float(rank)})
+    gathered = [None] * world
+    dist.all_gather_object(gathered, payloads)
+    if rank == 0:
+        merged = {}
+        for g in gathered:
+            merged.update(g)
+        out_q.put((m, merged))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_reproduce_single_process(wc, oracle):
+    import torch.multiprocessing as mp
+    dims = [(16, 16, 16), (8, 4, 2), (32, 16, 8), (6, 10, 14), (16, 32, 64), (3, 5, 7)]
+    keep = float(np.float32(0.999))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, dims, keep, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    m, merged = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single = {}
+    kept = 0
+    for u, d in enumerate(dims):
+        cells = oracle.synth_box_f64(oracle.unit_seed(0, 0, u, 0), (0, 0, 0), *d)
+        p, k = oracle.compress_payload(oracle.narrow(cells), keep)
+        single[u] = p
+        kept += k
+    assert merged == single
+    assert m["kept"] == kept and m["boxes"] == len(dims)
+    assert m["cells"] == sum(w * h * d for (w, h, d) in dims)
+    assert m["seconds"] == pytest.approx(0.2) and m["min_value"] == 0.0 and m["max_value"] == 1.0

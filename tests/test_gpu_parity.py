@@ -331,3 +331,25 @@ def test_reference_calc_rmse_case(wc):
     a = [np.zeros((2, 2, 2), np.float32)] * 2
     p = [np.full((2, 2, 2), 3.5, np.float32)] * 2
     assert wc.calc_rmse_per_box(a, p, 2) == [3.5, 3.5]
+
+
+@pytest.mark.parametrize("fused", PATHS)
+def test_gpu_matches_committed_golden_fixtures(wc, ctx, fused):
+    """Stored vectors (tests/golden/codec_golden.npz): payload bytes and reconstructions."""
+    import json
+    from pathlib import Path
+    g = Path(__file__).parent / "golden"
+    z = np.load(g / "codec_golden.npz")
+    meta = json.loads((g / "codec_golden.json").read_text())
+    by_keep = {}
+    for case in meta["cases"]:
+        by_keep.setdefault(case["keep"], []).append(case)
+    for keep, cases in by_keep.items():
+        boxes = [z[c["box"]] for c in cases]
+        got, kept = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, fused=fused)
+        for i, c in enumerate(cases):
+            assert got[i] == z[c["name"] + "/payload"].tobytes(), c["name"]
+            assert int(kept[i]) == c["kept"], c["name"]
+        regen = wc.decompress_payloads(got)
+        for i, c in enumerate(cases):
+            assert regen[i].tobytes() == z[c["name"] + "/regen"].tobytes(), c["name"]

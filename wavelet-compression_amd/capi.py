@@ -26,7 +26,8 @@ EXPORTED = (
     "wc_ctx_create", "wc_ctx_destroy", "wc_last_error", "wc_set_stream", "wc_synchronize",
     "wc_payload_bound", "wc_cell_count", "wc_forward", "wc_forward_host", "wc_decompose",
     "wc_inverse", "wc_inverse_host", "wc_inverse_flat", "wc_rmse", "wc_version",
-    "wc_profile_enable", "wc_profile_read", "wc_set_option",
+    "wc_profile_enable", "wc_profile_read", "wc_set_option", "wc_inverse_flat_host", "wc_rmse_host",
+    "wc_decompose_host",
 )
 WC_OPT_FUSED = 1
 
@@ -81,6 +82,9 @@ def load_library() -> ctypes.CDLL:
         "wc_version": (ctypes.c_char_p, []),
         "wc_profile_enable": (i32, [vp, i32]),
         "wc_set_option": (i32, [vp, i32, ctypes.c_int64]),
+        "wc_inverse_flat_host": (i32, [vp, vp, up, i32, vp]),
+        "wc_rmse_host": (i32, [vp, vp, i32, vp, up, i32, vp]),
+        "wc_decompose_host": (i32, [vp, vp, i32, up, i32, vp]),
         "wc_profile_read": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32), i32]),
     }
     for name, (res, args) in sigs.items():
@@ -228,6 +232,27 @@ class Context:
                                             payload.ctypes.data, cap, offsets.ctypes.data,
                                             kept.ctypes.data))
         return payload, offsets, kept[:n]
+
+    def decompose_host(self, cells: np.ndarray, units, n: int, extent: int) -> np.ndarray:
+        c = np.ascontiguousarray(cells)
+        dtype = WC_F64 if c.dtype == np.float64 else WC_F32
+        out = np.zeros(max(extent, 1), np.float32)
+        self._check(self._L.wc_decompose_host(self._h, c.ctypes.data, dtype, units, n, out.ctypes.data))
+        return out[:extent]
+
+    def inverse_flat_host(self, flat: np.ndarray, units, n: int, extent: int) -> np.ndarray:
+        f = np.ascontiguousarray(flat, np.float32)
+        out = np.zeros(max(extent, 1), np.float32)
+        self._check(self._L.wc_inverse_flat_host(self._h, f.ctypes.data, units, n, out.ctypes.data))
+        return out[:extent]
+
+    def rmse_host(self, orig: np.ndarray, regen: np.ndarray, units, n: int) -> np.ndarray:
+        o = np.ascontiguousarray(orig)
+        dtype = WC_F64 if o.dtype == np.float64 else WC_F32
+        r = np.ascontiguousarray(regen, np.float32)
+        out = np.zeros(max(n, 1), np.float64)
+        self._check(self._L.wc_rmse_host(self._h, o.ctypes.data, dtype, r.ctypes.data, units, n, out.ctypes.data))
+        return out[:n]
 
     def inverse_host(self, payload: np.ndarray, offsets: np.ndarray, units, n: int, extent: int):
         p = np.ascontiguousarray(payload, dtype=np.uint8)

@@ -185,39 +185,24 @@ def decompress(file_path, time: int = 0, level: int = 0, component: int = 0, box
 
 def inverse_wavelet_decompose(flat, x: int, y: int, z: int) -> np.ndarray:
     """src/decompressor.cpp:79-159 on the GPU: flat coefficients -> Box3D (z, y, x)."""
-    import torch  # device buffers only
     f = np.ascontiguousarray(flat, np.float32)
     if f.size != x * y * z:
         raise ValueError("flat length != x*y*z")
     units, n, extent = capi.make_units([(x, y, z)])
-    ctx = context(0)
-    dev = torch.device("cuda", ctx.device)
-    d_flat = torch.from_numpy(f).to(dev)
-    d_out = torch.empty(max(extent, 1), dtype=torch.float32, device=dev)
-    ctx.inverse_flat(d_flat.data_ptr(), units, n, d_out.data_ptr())
-    ctx.synchronize()
-    return d_out[:extent].cpu().numpy().reshape(z, y, x)
+    return context(0).inverse_flat_host(f, units, n, extent).reshape(z, y, x)
 
 
 def wavelet_decompose(box: np.ndarray) -> np.ndarray:
     """src/compressor.cpp:85-185 (static there) on the GPU: Box3D -> flat coefficients."""
-    import torch
     W, H, D = _box_dims(box)
     units, n, extent = capi.make_units([(W, H, D)])
-    ctx = context(0)
-    dev = torch.device("cuda", ctx.device)
-    d_in = torch.from_numpy(np.ascontiguousarray(box, np.float32).ravel()).to(dev)
-    d_flat = torch.empty(max(extent, 1), dtype=torch.float32, device=dev)
-    ctx.decompose(d_in.data_ptr(), capi.WC_F32, units, n, d_flat.data_ptr())
-    ctx.synchronize()
-    return d_flat[:extent].cpu().numpy()
+    return context(0).decompose_host(np.ascontiguousarray(box, np.float32).ravel(), units, n, extent)
 
 
 def calc_rmse_per_box(actual: Sequence[np.ndarray], pred: Sequence[np.ndarray],
                       num_components: int) -> List[float]:
     """src/calc-loss.cpp:12-43 on the GPU (one K7 launch for all components).
-    Note: like the reference, every component uses actual[0]'s dimensions."""
-    import torch
+    Like the reference, every component uses actual[0]'s dimensions."""
     W, H, D = _box_dims(actual[0])
     units, n, extent = capi.make_units([(W, H, D)] * num_components)
     a = np.zeros(max(extent, 1), np.float32)
@@ -226,13 +211,7 @@ def calc_rmse_per_box(actual: Sequence[np.ndarray], pred: Sequence[np.ndarray],
         o = units[c].cell_offset
         a[o:o + W * H * D] = np.ascontiguousarray(actual[c], np.float32).ravel()
         p[o:o + W * H * D] = np.ascontiguousarray(pred[c], np.float32).ravel()
-    ctx = context(0)
-    dev = torch.device("cuda", ctx.device)
-    da, dp = torch.from_numpy(a).to(dev), torch.from_numpy(p).to(dev)
-    dr = torch.empty(num_components, dtype=torch.float64, device=dev)
-    ctx.rmse(da.data_ptr(), capi.WC_F32, dp.data_ptr(), units, n, dr.data_ptr())
-    ctx.synchronize()
-    return dr.cpu().tolist()
+    return context(0).rmse_host(a, p, units, n).tolist()
 
 
 def calc_adj_loss(rmse: float, value_range: float) -> float:

@@ -1,0 +1,142 @@
+// compressor.cpp — C++ mirror of the reference's compress() (src/compressor.cpp:192-297).
+//
+// All components of the box go to the GPU in ONE wc_forward_host call (the
+// reference loops per component, :203); the serialized payloads come back
+// byte-identical to serialize_compressed_wavelet, and the host only does the
+// xz stage and the file write.
+#include <lzma.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
+#include <mutex>
+#include <vector>
+
+#include "host_ctx.h"
+#include "wavelet_amd/codec_extras.h"
+#include "wavelet_amd/compressor.h"
+#include "wavelet_amd/decompressor.h"
+
+namespace wavelet_amd {
+
+wc_ctx* thread_ctx() {
+    thread_local struct Holder {
+        wc_ctx* c = nullptr;
+        ~Holder() {
+            if (c) wc_ctx_destroy(c);
+        }
+    } h;
+    if (!h.c) {
+        const char* dev = std::getenv("WCAMD_DEVICE");
+        const int d = dev ? std::atoi(dev) : 0;
+        if (wc_ctx_create(d, &h.c) != WC_OK) fatal("wc_ctx_create failed: no usable HIP device");
+    }
+    return h.c;
+}
+
+std::vector<std::pair<int, float>> rle_encode(const std::vector<bool>& mask, const std::vector<float>& values) {
+    std::vector<std::pair<int, float>> out;
+    int gap = 0;
+    size_t vi = 0;
+    for (bool m : mask) {
+        if (!m) {
+            ++gap;
+            continue;
+        }
+        out.emplace_back(gap, values[vi++]);
+        gap = 0;
+    }
+    return out;
+}
+
+std::string serialize_compressed_wavelet(const CompressedWavelet& cw) {
+    std::string buf;
+    auto put = [&buf](const void* p, size_t n) { buf.append(static_cast<const char*>(p), n); };
+    for (int d : cw.shape) put(&d, 4);
+    for (int d : cw.coeff_shape) put(&d, 4);
+    const int n = static_cast<int>(cw.rle_encoded.size());
+    put(&n, 4);
+    for (const auto& pr : cw.rle_encoded) {
+        put(&pr.first, 4);
+        put(&pr.second, 4);
+    }
+    return buf;
+}
+
+std::vector<float> wavelet_decompose(const Box3D& box) {
+    wc_ctx* c = thread_ctx();
+    wc_unit u{0, (int32_t)box.width(), (int32_t)box.height(), (int32_t)box.depth(), 0};
+    std::vector<float> flat(box.data_size());
+    if (flat.empty()) return flat;
+    check(c, wc_decompose_host(c, box.data(), WC_F32, &u, 1, flat.data()), "wavelet_decompose");
+    return flat;
+}
+
+std::string xz_compress(const std::string& payload) {
+    // lzma_easy_encoder(preset 6, CRC64) + one lzma_code(LZMA_FINISH) into a
+    // buffer of 1.1 x input + 128 (src/compressor.cpp:260-285).
+    lzma_stream strm = LZMA_STREAM_INIT;
+    if (lzma_easy_encoder(&strm, 6, LZMA_CHECK_CRC64) != LZMA_OK) fatal("Failed to initialize LZMA encoder");
+    std::vector<uint8_t> out(static_cast<size_t>(payload.size() * 1.1) + 128);
+    strm.next_in = reinterpret_cast<const uint8_t*>(payload.data());
+    strm.avail_in = payload.size();
+    strm.next_out = out.data();
+    strm.avail_out = out.size();
+    if (lzma_code(&strm, LZMA_FINISH) != LZMA_STREAM_END) {
+        lzma_end(&strm);
+        fatal("LZMA compression failed");
+    }
+    const size_t used = out.size() - strm.avail_out;
+    lzma_end(&strm);
+    return std::string(reinterpret_cast<const char*>(out.data()), used);
+}
+
+}  // namespace wavelet_amd
+
+using namespace wavelet_amd;
+
+std::vector<CompressedWavelet> compress(multiBox3D& box, std::vector<int> components, double keep, int time,
+                                        int level, int box_index, std::string compressed_dir) {
+    const int n = static_cast<int>(components.size());
+    std::vector<CompressedWavelet> out;
+    if (n == 0) return out;
+    // Pack box[0..n) (positional, src/compressor.cpp:203-206) into one buffer.
+    std::vector<wc_unit> units(n);
+    uint64_t cursor = 0;
+    for (int c = 0; c < n; ++c) {
+        const Box3D& b = box.at(c);
+        cursor = (cursor + 3) & ~uint64_t(3);
+        units[c] = wc_unit{cursor, (int32_t)b.width(), (int32_t)b.height(), (int32_t)b.depth(), 0};
+        cursor += b.data_size();
+    }
+    std::vector<float> cells(cursor ? cursor : 1);
+    for (int c = 0; c < n; ++c)
+        if (box[c].data_size()) std::memcpy(cells.data() + units[c].cell_offset, box[c].data(), 4 * box[c].data_size());
+    const uint64_t cap = wc_payload_bound(units.data(), n);
+    std::vector<uint8_t> payload(cap);
+    std::vector<uint64_t> offsets(n + 1);
+    std::vector<uint32_t> kept(n);
+    wc_ctx* ctx = thread_ctx();
+    check(ctx, wc_forward_host(ctx, cells.data(), WC_F32, units.data(), n, keep, payload.data(), cap, offsets.data(),
+                               kept.data()),
+          "GPU forward");
+    for (int c = 0; c < n; ++c) {
+        const std::string serialized(reinterpret_cast<const char*>(payload.data() + offsets[c]), 20 + 8ull * kept[c]);
+        CompressedWavelet cw = deserialize_compressed_wavelet(serialized);
+        for (const auto& pr : cw.rle_encoded)
+            if (std::fabs((double)pr.second) > INT16_MAX) cw.need32 = true;  // src/compressor.cpp:229
+        const std::filesystem::path fname =
+            std::filesystem::path(compressed_dir) / ("compressed-wavelet-" + std::to_string(time) + "-" +
+                                                     std::to_string(level) + "-" + std::to_string(components[c]) +
+                                                     "-" + std::to_string(box_index) + ".xz");
+        std::ofstream file(fname, std::ios::binary);
+        if (file.is_open()) {  // a failed open silently skips the file, as the reference does (:256-257)
+            const std::string xz = xz_compress(serialized);
+            file.write(xz.data(), (std::streamsize)xz.size());
+        }
+        out.push_back(std::move(cw));
+    }
+    return out;
+}

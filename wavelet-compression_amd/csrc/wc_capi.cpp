@@ -726,4 +726,70 @@ int wc_inverse_host(wc_ctx* c, const uint8_t* payload, const uint64_t* offsets, 
     return WC_OK;
 }
 
+// Stage host arrays through the context's staging buffers for the
+// transform-only, inverse-only and RMSE entry points.
+int wc_decompose_host(wc_ctx* c, const void* cells, int dtype, const wc_unit* units, int n, float* flat) {
+    if (!c) return WC_ERR_INVALID;
+    int rc;
+    if ((rc = validate_units(c, units, n))) return rc;
+    if (dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
+    if (n == 0) return WC_OK;
+    if (!cells || !flat) return fail(c, WC_ERR_INVALID, "null buffer");
+    if ((rc = set_device(c))) return rc;
+    const size_t esz = dtype == WC_F64 ? 8 : 4;
+    const uint64_t ext = cells_extent(units, n);
+    if ((rc = ensure(c, c->h_cells, esz * ext)) || (rc = ensure(c, c->h_out, sizeof(float) * ext))) return rc;
+    hipError_t e = hipMemcpyAsync(c->h_cells.p, cells, esz * ext, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "cells upload");
+    if ((rc = wc_decompose(c, c->h_cells.p, dtype, units, n, (float*)c->h_out.p))) return rc;
+    if ((e = hipMemcpyAsync(flat, c->h_out.p, sizeof(float) * ext, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return hip_fail(c, e, "flat readback");
+    return WC_OK;
+}
+
+int wc_inverse_flat_host(wc_ctx* c, const float* flat, const wc_unit* units, int n, float* out) {
+    if (!c) return WC_ERR_INVALID;
+    int rc;
+    if ((rc = validate_units(c, units, n))) return rc;
+    if (n == 0) return WC_OK;
+    if (!flat || !out) return fail(c, WC_ERR_INVALID, "null buffer");
+    if ((rc = set_device(c))) return rc;
+    const uint64_t ext = cells_extent(units, n);
+    if ((rc = ensure(c, c->h_cells, sizeof(float) * ext)) || (rc = ensure(c, c->h_out, sizeof(float) * ext)))
+        return rc;
+    hipError_t e = hipMemcpyAsync(c->h_cells.p, flat, sizeof(float) * ext, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "flat upload");
+    if ((rc = wc_inverse_flat(c, (const float*)c->h_cells.p, units, n, (float*)c->h_out.p))) return rc;
+    if ((e = hipMemcpyAsync(out, c->h_out.p, sizeof(float) * ext, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return hip_fail(c, e, "box readback");
+    return WC_OK;
+}
+
+int wc_rmse_host(wc_ctx* c, const void* orig, int dtype, const float* regen, const wc_unit* units, int n,
+                 double* rmse) {
+    if (!c) return WC_ERR_INVALID;
+    int rc;
+    if ((rc = validate_units(c, units, n))) return rc;
+    if (dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
+    if (n == 0) return WC_OK;
+    if (!orig || !regen || !rmse) return fail(c, WC_ERR_INVALID, "null buffer");
+    if ((rc = set_device(c))) return rc;
+    const size_t esz = dtype == WC_F64 ? 8 : 4;
+    const uint64_t ext = cells_extent(units, n);
+    if ((rc = ensure(c, c->h_cells, esz * ext)) || (rc = ensure(c, c->h_out, sizeof(float) * ext)) ||
+        (rc = ensure(c, c->h_offsets, sizeof(double) * n)))
+        return rc;
+    hipError_t e;
+    if ((e = hipMemcpyAsync(c->h_cells.p, orig, esz * ext, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(c->h_out.p, regen, sizeof(float) * ext, hipMemcpyHostToDevice, c->stream)) != hipSuccess)
+        return hip_fail(c, e, "rmse upload");
+    if ((rc = wc_rmse(c, c->h_cells.p, dtype, (const float*)c->h_out.p, units, n, (double*)c->h_offsets.p))) return rc;
+    if ((e = hipMemcpyAsync(rmse, c->h_offsets.p, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
+        return hip_fail(c, e, "rmse readback");
+    return WC_OK;
+}
+
 }  // extern "C"
