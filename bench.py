@@ -142,6 +142,8 @@ def main():
         "unit_scan": 0,
         "unit_offsets": 20 * n,
         "flat_emit": 8 * kept_step,
+        # the fused kernel owns the whole path: cells in, pairs + headers out
+        "fused": s_in * ncells + 8 * kept_step + 20 * n,
     }
     dom_ms = per_launch[dominant][0]
     achieved = alg_bytes_stage.get(dominant, 0) / (dom_ms * 1e-3) / 1e9

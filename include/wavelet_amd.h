@@ -80,11 +80,11 @@ const char* wc_last_error(const wc_ctx* ctx);
 int wc_set_stream(wc_ctx* ctx, void* hip_stream);
 int wc_synchronize(wc_ctx* ctx);  /* also reports kernel-side errors of earlier async calls */
 
-/* Tuning switches.  WC_OPT_FUSED (default 0): 1 runs eligible units (even W,
- * H, D % 8 == 0, <= 256 tiles, <= 8192 flat-row segments) through the
+/* Tuning switches.  WC_OPT_FUSED (default 1): 1 runs eligible units (even W
+ * <= 64, even H, D % 8 == 0, D <= 64, W*H <= 4096 flat rows) through the
  * single-read fused forward kernel; 0 uses the staged path (transform -> HBM
  * scratch -> threshold/pack) for every unit.  Results are byte-identical
- * either way; which is faster depends on the box size. */
+ * either way (DESIGN.md has the timings of both). */
 #define WC_OPT_FUSED 1
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 

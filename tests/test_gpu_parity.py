@@ -41,7 +41,7 @@ def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None, fused=Tru
     try:
         payload, offs, kept = ctx.forward_host(cells, units, n, keep)
     finally:
-        ctx.set_fused(False)
+        ctx.set_fused(True)  # library default
     return [wc.capi.unit_payload(payload, offs, kept, i) for i in range(n)], kept
 
 
@@ -297,8 +297,8 @@ def test_large_batch_64cubed_fp64(wc, ctx, oracle, fused):
 
 @pytest.mark.parametrize("fused", PATHS)
 def test_128cubed_fp32_and_mixed_sizes(wc, ctx, oracle, fused):
-    """C5 shape (128^3 fp32, keep 0.9999f: 256 fused tiles per unit) beside
-    AMR-style mixed boxes in one batch."""
+    """C5 shape (128^3 fp32, keep 0.9999f: staged, W > 64) beside fused-eligible and
+    other AMR-style mixed boxes in one batch."""
     keep = KEEPS[2]
     dims = [(128, 128, 128), (32, 32, 32), (16, 16, 16), (48, 32, 16), (64, 64, 64), (128, 64, 32)]
     boxes = [oracle.narrow(b) for b in synth(oracle, dims, seed0=8)]

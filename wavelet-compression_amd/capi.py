@@ -180,7 +180,7 @@ class Context:
         self._check(self._L.wc_set_option(self._h, int(option), int(value)))
 
     def set_fused(self, on: bool):
-        """Route eligible units through the fused single-read kernel (default off)."""
+        """Route eligible units through the fused single-read kernel (default on)."""
         self.set_option(WC_OPT_FUSED, 1 if on else 0)
 
     def profile_enable(self, on: bool = True):

@@ -6,7 +6,7 @@
 // WC_ERR_HIP if the device or code object is absent.
 //
 // Forward path per batch (wc_forward):
-//   fused units  (even dims, D % 8 == 0, <= kMaxFusedTiles tiles)
+//   fused units  (even dims, D % 8 == 0, W <= 64, D <= 64, <= kMaxFusedTiles tiles)
 //       -> k_forward_fused: one read of the cells, pairs written in place
 //   staged units (everything else: odd dims, short z, huge boxes)
 //       -> k_transform{,_fast} -> flat coefficients in HBM scratch
@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -24,7 +25,7 @@
 namespace wc {
 size_t transform_lds_bytes(int lbx, int lby, int lbz);
 size_t transform_fast_lds_bytes(int lbx, int lby, int lbz);
-size_t fused_lds_bytes(int lbx, int lby, int lbz);
+size_t fused_lds_bytes(int lbx, int lby, int lbz, uint32_t ntile);
 hipError_t launch_transform(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
                             float*, int, unsigned long long*);
 hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
@@ -71,9 +72,9 @@ struct Plan {
     uint32_t nft_staged = 0;
     uint32_t nstaged_units = 0;  // units (including empty ones) the staged kernels finish
     uint64_t coef_extent = 0;  // floats of staged coefficient scratch
-    uint64_t nseg = 0;         // fused segment records
+    uint64_t ntab = 0;         // fused row-table granules
     size_t lds_gen = 0, lds_fast = 0, lds_fused = 0, lds_inverse = 0;
-    size_t flags_bytes = 0;    // ticket + arrive[n] + ready[n] + keyslot[nfused]
+    size_t flags_bytes = 0;    // ticket + keyslot[nfused]
     DevBuf d_units, d_xtiles, d_ftiles;
 };
 
@@ -92,10 +93,10 @@ struct wc_ctx {
     std::string err;
     Plan plan;
     bool plan_valid = false;
-    bool opt_fused = false;  // WC_OPT_FUSED default (see include/wavelet_amd.h)
+    bool opt_fused = true;   // WC_OPT_FUSED default (see include/wavelet_amd.h)
     bool err_check_pending = false;
     // scratch (grow-only)
-    DevBuf coef, keys, tcount, tlast, toff, tprev, tsum, tbase, part, errflag, flags, segrec, segoff;
+    DevBuf coef, keys, tcount, tlast, toff, tprev, tsum, tbase, part, errflag, flags, table;
     // host-path staging
     DevBuf h_cells, h_payload, h_packed, h_offsets, h_poff, h_kept, h_out;
     // per-kernel event timing (wc_profile_enable / wc_profile_read)
@@ -220,7 +221,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     P.ngen = P.nfast = P.nfused = P.nft_staged = P.nstaged_units = 0;
     P.lds_gen = P.lds_fast = P.lds_fused = P.lds_inverse = 0;
     std::vector<XTile> gen, fast, fused;
-    uint64_t coef_cursor = 0, pay_cursor = 4, seg_cursor = 0;
+    uint64_t coef_cursor = 0, pay_cursor = 4, tab_cursor = 0;
     for (int i = 0; i < n; ++i) {
         const wc_unit& u = units[i];
         UnitDev& d = P.units[i];
@@ -246,15 +247,19 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         const bool fast_ok = (u.nx % 2 == 0) && (u.ny % 2 == 0) && (u.nz % 8 == 0);
         const uint64_t ntile = (uint64_t)((d.nbx + (1 << d.lbx) - 1) >> d.lbx) *
                                ((d.nby + (1 << d.lby) - 1) >> d.lby) * d.ntz;
-        const uint64_t nseg_u = (uint64_t)u.nx * u.ny * 2 * d.ntz;
-        if (fast_ok && c->opt_fused && ntile <= kMaxFusedTiles && nseg_u <= kMaxFusedSegments) {
+        // fused: tiles span the whole x and z extent (one tile row per y block
+        // range), G <= kMaxFusedTiles, the row table fits kMaxFusedRows.
+        const uint64_t nrows_tile = (uint64_t)4 << (d.lbx + d.lby);
+        const bool fused_ok = fast_ok && d.nbx <= (1 << d.lbx) && d.ntz == 1 && ntile <= kMaxFusedTiles &&
+                              ntile * nrows_tile <= kMaxFusedRows;
+        if (fused_ok && c->opt_fused) {
             d.fused = 1;
             d.xt_begin = (uint32_t)fused.size();
             d.ntile_u = (uint32_t)ntile;
-            d.seg_off = seg_cursor;
-            seg_cursor += nseg_u;
+            d.tab_off = tab_cursor;
+            tab_cursor += ntile * nrows_tile / 4;
             push_tiles(fused, d, (uint32_t)i);
-            P.lds_fused = std::max(P.lds_fused, fused_lds_bytes(d.lbx, d.lby, d.lbz));
+            P.lds_fused = std::max(P.lds_fused, fused_lds_bytes(d.lbx, d.lby, d.lbz, (uint32_t)ntile));
         } else {
             ++P.nstaged_units;
             d.coef_off = (coef_cursor + 3) & ~uint64_t(3);
@@ -287,8 +292,8 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     P.xtiles.insert(P.xtiles.end(), fast.begin(), fast.end());
     P.xtiles.insert(P.xtiles.end(), fused.begin(), fused.end());
     P.coef_extent = coef_cursor ? coef_cursor + kFlatTile : 0;  // slack: flat tiles read whole float4 groups
-    P.nseg = seg_cursor;
-    P.flags_bytes = 16 + 8 * (size_t)n + 8 * (size_t)P.nfused + 16;
+    P.ntab = tab_cursor;
+    P.flags_bytes = 16 + 8 * (size_t)P.nfused;
     int rc;
     if ((rc = upload(c, P.d_units, P.units.data(), sizeof(UnitDev) * P.units.size(), "upload units")) ||
         (rc = upload(c, P.d_xtiles, P.xtiles.data(), sizeof(XTile) * P.xtiles.size(), "upload xtiles")) ||
@@ -311,8 +316,7 @@ int ensure_scratch(wc_ctx* c) {
         (rc = ensure(c, c->toff, sizeof(uint32_t) * nft)) || (rc = ensure(c, c->tprev, sizeof(uint32_t) * nft)) ||
         (rc = ensure(c, c->tsum, sizeof(uint64_t) * nft)) || (rc = ensure(c, c->tbase, sizeof(uint64_t) * nft)) ||
         (rc = ensure(c, c->part, sizeof(double) * nft)) || (rc = ensure(c, c->errflag, 16)) ||
-        (rc = ensure(c, c->flags, P.flags_bytes)) || (rc = ensure(c, c->segrec, sizeof(uint32_t) * P.nseg)) ||
-        (rc = ensure(c, c->segoff, 8 * P.nseg)))
+        (rc = ensure(c, c->flags, P.flags_bytes)) || (rc = ensure(c, c->table, 8 * P.ntab)))
         return rc;
     return WC_OK;
 }
@@ -345,6 +349,7 @@ int forward_impl(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, 
     if (P.nfused) {
         uint8_t* fl = (uint8_t*)c->flags.p;
         if ((e = hipMemsetAsync(fl, 0, P.flags_bytes, c->stream)) != hipSuccess ||
+            (e = hipMemsetAsync(c->table.p, 0, 8 * P.ntab, c->stream)) != hipSuccess ||
             (e = hipMemsetAsync(c->errflag.p, 0, 4, c->stream)) != hipSuccess)
             return hip_fail(c, e, "memset fused flags");
         FusedParams fp{};
@@ -354,16 +359,14 @@ int forward_impl(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, 
         fp.ntiles = P.nfused;
         fp.n = n;
         fp.ticket = (uint32_t*)fl;
-        fp.arrive = (uint32_t*)(fl + 16);
-        fp.ready = fp.arrive + n;
-        fp.keyslot = (unsigned long long*)(fl + 16 + 8 * (size_t)n);
-        fp.segrec = (uint32_t*)c->segrec.p;
-        fp.segoff = (uint2*)c->segoff.p;
+        fp.keyslot = (unsigned long long*)(fl + 16);
+        fp.table = (unsigned long long*)c->table.p;
         fp.payload = d_payload;
         fp.offsets = d_offsets;
         fp.kept = d_kept;
         fp.err = (uint32_t*)c->errflag.p;
         fp.keep = keep;
+        if (const char* dg = std::getenv("WCAMD_FUSED_DIAG")) fp.diag = (uint32_t)std::atoi(dg);
         {
             StageTimer t(c, WC_STAGE_FUSED);
             e = launch_forward_fused(c->stream, dtype, P.lds_fused, fp);
@@ -460,7 +463,7 @@ void wc_ctx_destroy(wc_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->coef,      &c->keys,      &c->tcount,    &c->tlast,      &c->toff,
                       &c->tprev,     &c->tsum,      &c->tbase,     &c->part,       &c->errflag,
-                      &c->flags,     &c->segrec,    &c->segoff,    &c->h_cells,    &c->h_payload,
+                      &c->flags,     &c->table,     &c->h_cells,    &c->h_payload,
                       &c->h_packed,  &c->h_offsets, &c->h_poff,    &c->h_kept,     &c->h_out,
                       &c->plan.d_units, &c->plan.d_xtiles, &c->plan.d_ftiles};
     for (DevBuf* b : bufs)

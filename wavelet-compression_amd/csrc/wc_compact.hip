@@ -27,7 +27,7 @@ __global__ __launch_bounds__(kThreads) void k_flat_count(
     __shared__ uint32_t s_cnt[4], s_last[4];
     const FTile ft = tiles[blockIdx.x];
     const UnitDev& U = units[ft.unit];
-    const double thresh = unit_thresh(U, unit_key[ft.unit], coef, keep);
+    const float tf = thresh_as_float(unit_thresh(U, unit_key[ft.unit], coef, keep));
     const int64_t start = (int64_t)ft.index * kFlatTile;
     const int len = (int)min((int64_t)kFlatTile, (int64_t)U.ncells - start);
     const float4* __restrict__ p4 = reinterpret_cast<const float4*>(coef + U.coef_off + start);
@@ -44,7 +44,7 @@ __global__ __launch_bounds__(kThreads) void k_flat_count(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int idx = w * 1024 + it * 256 + l * 4 + j;
-            const bool k = idx < len && (double)fabsf(e[j]) > thresh;
+            const bool k = idx < len && fabsf(e[j]) > tf;
             cnt += k;
             if (k) last = (uint32_t)(start + idx + 1);
         }
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kThreads) void k_flat_emit(
     __shared__ uint32_t s_cnt[4], s_last[4];
     const FTile ft = tiles[blockIdx.x];
     const UnitDev& U = units[ft.unit];
-    const double thresh = unit_thresh(U, unit_key[ft.unit], coef, keep);
+    const float tf = thresh_as_float(unit_thresh(U, unit_key[ft.unit], coef, keep));
     const int64_t start = (int64_t)ft.index * kFlatTile;
     const int len = (int)min((int64_t)kFlatTile, (int64_t)U.ncells - start);
     const float4* __restrict__ p4 = reinterpret_cast<const float4*>(coef + U.coef_off + start);
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kThreads) void k_flat_emit(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int idx = w * 1024 + it * 256 + l * 4 + j;
-            const bool k = idx < len && (double)fabsf(e[j]) > thresh;
+            const bool k = idx < len && fabsf(e[j]) > tf;
             kb |= (uint32_t)k << (it * 4 + j);
         }
     }

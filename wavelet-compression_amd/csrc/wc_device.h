@@ -9,6 +9,12 @@ namespace wc {
 __device__ __forceinline__ float haar_lo(float a, float b) { return (a + b) * 0.5f; }
 __device__ __forceinline__ float haar_hi(float a, float b) { return (a - b) * 0.5f; }
 
+// The reference keeps |c| iff (double)|c| > thresh (src/compressor.cpp:225-226).
+// With tf = thresh rounded toward -inf to float, that is exactly |c| > tf for
+// every float |c|: no float lies strictly between tf and thresh; NaN and
+// +-inf thresholds map to themselves.
+__device__ __forceinline__ float thresh_as_float(double thresh) { return __double2float_rd(thresh); }
+
 __device__ __forceinline__ int lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0));
 }

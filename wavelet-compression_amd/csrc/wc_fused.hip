@@ -1,41 +1,38 @@
 // wc_fused.hip — single-read forward path: transform + keep threshold + ordered
-// pack in ONE kernel, for units with even W, H and D % 8 == 0 whose tile count
-// G fits comfortably in the resident grid.
+// pack in ONE kernel, for units whose transform tiles span the full x and z
+// extent (even W, H, D % 8 == 0, W <= 64, D <= 64, <= kMaxFusedTiles tiles).
 //
 //   src/compressor.cpp:85-185  wavelet_decompose  -> phase 1 (coefficients stay in LDS)
-//   src/compressor.cpp:212-216 signed max, thresh -> phase 2 (box-wide max exchange)
-//   src/compressor.cpp:222-238 mask + rle_encode  -> phases 3-5 (segment scan, emit)
+//   src/compressor.cpp:212-216 signed max, thresh -> phase 2 (unit-wide max exchange)
+//   src/compressor.cpp:222-238 mask + rle_encode  -> phases 3-5 (row table, scan, emit)
 //   src/compressor.cpp:55-80   serialize          -> header + pairs written in place
 //
-// A unit (one Box3D component) is cut into G transform tiles (the fast K1 tile:
-// up to 32 x-blocks x 32 z-blocks, 4 z-blocks per thread).  Every tile:
-//   1. takes a ticket (atomic counter) -> tile index.  Tiles of one unit have
-//      consecutive tickets, so a tile only ever waits for tiles that have
-//      already started; with >= G resident slots the grid cannot deadlock.
-//   2. loads its cells once, transforms them into LDS rows keyed by flat row
-//      (I, J) and reduces its max-|c| key (|c| bits, first flat index, sign).
-//   3. publishes the key as one self-validating 8-byte granule and waits for
-//      all G granules of its unit -> thresh = signed max * (1 - keep).
-//   4. thresholds its rows (wave ballots) and publishes one record per
-//      segment (a TZ-long piece of a flat row: kept count, last kept).
-//   5. the last tile of the unit to arrive scans the unit's records in flat
-//      order (exclusive count -> pair offset, exclusive max -> previous kept
-//      flat index) and publishes them; the others wait for its ready flag.
-//   6. every tile emits its kept coefficients as (run, value) pairs straight
-//      into the unit's payload slot.
-// Hand-offs follow MI355X_MICROARCH.md "Valid forms": sc1 (agent-scope relaxed
-// atomic) stores drained by s_waitcnt vmcnt(0) before a workgroup barrier and
-// the signalling atomic; sc1 loads after the poll/ticket.  Every spin is
-// bounded and raises kErrTimeout instead of hanging.
+// A unit (one Box3D component) is cut along y into G tiles; each tile owns
+// complete flat rows (I, J) (x-slowest / z-fastest, :178-181).  Every tile:
+//   0. takes a ticket (atomic counter) -> tile index.  Tiles of one unit hold
+//      consecutive tickets, so a tile only waits for tiles that have started;
+//      with >= G resident slots the grid cannot deadlock.
+//   1. loads its cells once and transforms them into LDS rows; reduces its
+//      max-|c| key (|c| bits, first flat index, sign).
+//   2. publishes the key as one self-validating 8-byte granule and waits for
+//      the unit's G granules -> thresh = signed max * (1 - keep).
+//   3. thresholds its rows (wave ballots) and publishes one 14-bit record per
+//      row (kept count, last kept + 1), four per self-validating granule.
+//   4. reads the whole unit's row table (every tile does: no serial scan, no
+//      ready flag) and block-scans it in flat order -> for its own rows the
+//      pair offset and the previous kept flat index.
+//   5. emits its kept coefficients as (run, value) pairs into the unit's slot;
+//      tile 0 writes the 20-byte header, kept[u] and offsets[u].
+// Two hand-offs per tile, both "data is the flag" granules (MI355X_MICROARCH.md
+// Valid forms, R2): one 8-byte sc1 store per granule, relaxed agent-scope
+// (sc1) loads to poll.  Every spin is bounded and raises kErrTimeout.
 #include "wc_device.h"
 
 namespace wc {
 
 constexpr unsigned long long kValid = 1ull << 63;
 constexpr uint32_t kSpinLimit = 1u << 22;
-// Segment records the last arriver scans per thread (plan caps a fused unit at
-// kThreads * kScanPer segments).
-constexpr int kScanPer = 32;
+
 
 __device__ __forceinline__ void st_rlx(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -69,20 +66,13 @@ __device__ __forceinline__ double key_thresh(unsigned long long key, double keep
 }
 
 
-// Segment id of (flat row (I, J), z half sz, z tile tz): flat order.
-__device__ __forceinline__ uint32_t seg_id(int I, int J, int H, int sz, int tz, int ntz) {
-    return (uint32_t)((((int64_t)I * H + J) * 2 + sz) * ntz + tz);
-}
 
 template <typename T>
-__global__ __launch_bounds__(kThreads, 4) void k_forward_fused(FusedParams P) {
+__global__ __launch_bounds__(kThreads, 3) void k_forward_fused(FusedParams P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-
-    // Carve the tail of the dynamic LDS: misc words first (fixed), the tile after.
-    unsigned long long* misc = reinterpret_cast<unsigned long long*>(lds);  // 16 words
-    // misc[0]: ticket   misc[1]: thresh (double bits)   misc[2]: last-arriver flag
-    // misc[4..7]: per-wave key maxima   misc[8..11]: per-wave scan totals
+    // misc[0] ticket, misc[1] thresh bits, misc[4..7] wave key maxima, misc[8..11] scan scratch
+    unsigned long long* misc = reinterpret_cast<unsigned long long*>(lds);
     if (tid == 0) misc[0] = atomicAdd(P.ticket, 1u);
     __syncthreads();
     const uint32_t t = (uint32_t)misc[0];
@@ -93,13 +83,17 @@ __global__ __launch_bounds__(kThreads, 4) void k_forward_fused(FusedParams P) {
     const int hx = U.hx, hy = U.hy, hz = U.hz;
     const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
     const int TX = 1 << lbx, TY = 1 << lby, TZ = 1 << lbz;
-    const int rowlen = 2 * TZ, rstride = rowlen + 4;
+    const int rowlen = 2 * TZ, rstride = rowlen + 4;   // rowlen == D: the tile spans all of z
     const int nrows = 4 * TX * TY;
-    const int nelem = nrows * rowlen;
-    const int nchunk = (nelem + 63) >> 6;
-    const int tz = td.bz0 >> lbz;
-    float* rows = lds + 32;                                                  // after misc (128 B)
-    unsigned long long* masks = reinterpret_cast<unsigned long long*>(rows + nrows * rstride);
+    const uint32_t G = U.ntile_u;
+    const uint32_t gme = t - U.xt_begin;               // my tile index within the unit (along y)
+    // LDS carve (16-B aligned pieces)
+    uint32_t* slab = reinterpret_cast<uint32_t*>(lds + 32);  // [0,64) slab totals/bases, [64,128) slab last
+    float* rows = lds + 32 + 128;
+    unsigned long long* masks = reinterpret_cast<unsigned long long*>(rows + nrows * rstride);  // per row
+    uint32_t* own_off = reinterpret_cast<uint32_t*>(masks + nrows);
+    uint32_t* own_prev = own_off + nrows;
+    uint16_t* tab = reinterpret_cast<uint16_t*>(own_prev + nrows + 2 * kThreads);  // 4096 records; rec[] aliases
 
     // ---- phase 1: load + transform into LDS rows, local max key ----------
     const int64_t sy = W, sz = (int64_t)W * H;
@@ -169,20 +163,21 @@ __global__ __launch_bounds__(kThreads, 4) void k_forward_fused(FusedParams P) {
     __syncthreads();
 
     // ---- phase 2: publish the key granule, wait for the unit's G granules --
-    const uint32_t G = U.ntile_u, gbase = U.xt_begin;
     if (tid == 0) {
         unsigned long long k = misc[4];
         for (int i = 1; i < 4; ++i) k = misc[4 + i] > k ? misc[4 + i] : k;
         st_rlx(P.keyslot + t, k | kValid);
     }
-    if (w == 0) {
+    if (w == 0 && (P.diag & 1u)) {
+        if (lane == 0) misc[1] = (unsigned long long)__double_as_longlong(key_thresh(misc[4], P.keep));
+    } else if (w == 0) {
         unsigned long long best = 0;
         for (uint32_t g0 = 0; g0 < G; g0 += 64) {
             const uint32_t gi = g0 + lane;
             const bool need = gi < G;
             unsigned long long v = 0;
             for (uint32_t spin = 0;; ++spin) {
-                if (need) v = ld_rlx(P.keyslot + gbase + gi);
+                if (need) v = ld_rlx(P.keyslot + U.xt_begin + gi);
                 if (__all(!need || (v & kValid))) break;
                 if (spin > kSpinLimit) {
                     if (lane == 0) atomicOr(P.err, kErrTimeout);
@@ -198,147 +193,185 @@ __global__ __launch_bounds__(kThreads, 4) void k_forward_fused(FusedParams P) {
     __syncthreads();
     const double thresh = __longlong_as_double((long long)misc[1]);
 
-    // ---- phase 3: threshold rows -> ballot masks + segment records ---------
-    const int lrow = lbz + 1;
-    for (int ch = w; ch < nchunk; ch += 4) {
-        const int e = (ch << 6) + lane;
-        const int row = e >> lrow, col = e & (rowlen - 1);
+    // ---- phase 3: threshold rows -> per-row keep masks + records ----------
+    // 4 consecutive columns per lane (one 16-B LDS read), lpr lanes per row.
+    // Column c holds K = (c mod TZ) + (c / TZ) * hz; hz % 4 == 0, so a lane's
+    // four columns are all valid or all padding and map to 4 consecutive K.
+    const int lpr = rowlen >> 2, llpr = lbz - 1;  // lanes per row, log2
+    const int rpw = 64 >> llpr;                    // rows per wave-iteration
+    const float tf = thresh_as_float(thresh);
+    uint16_t* rec = tab;  // my records, published below, then overwritten by the table
+    for (int rb = w * rpw; rb < ((P.diag & 16u) ? 0 : nrows); rb += 4 * rpw) {
+        const int row = rb + (lane >> llpr), q = lane & (lpr - 1);
         const int bxl = row & (TX - 1);
-        int r2 = row >> lbx;
-        const int ssx = r2 & 1;
-        r2 >>= 1;
-        const int byl = r2 & (TY - 1), ssy = r2 >> lby;
-        const int ssz = col >> lbz, bzl = col & (TZ - 1);
-        const int bx = td.bx0 + bxl, by = td.by0 + byl;
-        const bool rv = e < nelem && bx < hx && by < hy;
-        const bool ev = rv && (td.bz0 + bzl) < hz;
-        const float cv = e < nelem ? rows[row * rstride + col] : 0.0f;
-        const bool keepv = ev && (double)fabsf(cv) > thresh;
-        const unsigned long long m = __ballot(keepv);
-        if (lane == 0) masks[ch] = m;
-        if (rv && bzl == 0) {
-            const unsigned long long segm = TZ >= 64 ? ~0ull : ((1ull << TZ) - 1ull);
-            const unsigned long long sb = (m >> lane) & segm;
-            const uint32_t cnt = (uint32_t)__popcll(sb);
-            const uint32_t last1 = sb ? (uint32_t)(64 - __clzll(sb)) : 0u;  // last local index + 1
-            const int I = bx + ssx * hx, J = by + ssy * hy;
-            st_rlx(P.segrec + U.seg_off + seg_id(I, J, H, ssz, tz, U.ntz), cnt | (last1 << 8));
+        const int byl = ((row >> lbx) >> 1) & (TY - 1);
+        const int zc = (4 * q) & (TZ - 1), kb = zc + ((4 * q) >> lbz) * hz;  // column -> K offset
+        const bool rv = row < nrows && td.bx0 + bxl < hx && td.by0 + byl < hy && zc < hz;
+        unsigned long long m = 0;
+        if (rv) {
+            const float4 v4 = *reinterpret_cast<const float4*>(rows + row * rstride + 4 * q);
+            const uint32_t nib = (uint32_t)(fabsf(v4.x) > tf) | ((uint32_t)(fabsf(v4.y) > tf) << 1) |
+                                 ((uint32_t)(fabsf(v4.z) > tf) << 2) | ((uint32_t)(fabsf(v4.w) > tf) << 3);
+            m = (unsigned long long)nib << kb;  // masks are in flat K order (bit K of row (I, J))
+        }
+        for (int o = 1; o < lpr; o <<= 1) m |= __shfl_xor(m, o);
+        if (q == 0 && row < nrows) {
+            masks[row] = m;
+            const uint32_t last1 = m ? (uint32_t)(64 - __clzll(m)) : 0u;
+            rec[row] = (uint16_t)((uint32_t)__popcll(m) | (last1 << 7));
         }
     }
-    drain_stores();
     __syncthreads();
-    if (tid == 0) misc[2] = (atomicAdd(P.arrive + td.unit, 1u) == G - 1) ? 1ull : 0ull;
+    unsigned long long* mytab = P.table + U.tab_off + (uint64_t)gme * (nrows >> 2);
+    for (int i = tid; i < (nrows >> 2); i += kThreads) {
+        const unsigned long long g = kValid | (unsigned long long)rec[4 * i] |
+                                     ((unsigned long long)rec[4 * i + 1] << 14) |
+                                     ((unsigned long long)rec[4 * i + 2] << 28) |
+                                     ((unsigned long long)rec[4 * i + 3] << 42);
+        st_rlx(mytab + i, g);
+    }
+    __syncthreads();  // rec[] is read before the table overwrites it
+
+    // ---- phase 4: read the unit's row table into LDS, in flat (I, J) order -
+    // Granule i of tile g holds local rows 4*(i mod nrows/4) .. +3; local row
+    // r = (((h*TY + jj) * 2 + sx) << lbx) + bxl is flat row
+    // (I, J) = (bxl + sx*hx, g*TY + jj + h*hy).  Every valid (I, J) has exactly
+    // one writer, so ft[0 .. W*H) ends up fully defined.
+    uint16_t* ft = tab;
+    const uint32_t ngr = (P.diag & 2u) ? 0u : G * (uint32_t)(nrows >> 2);
+    const unsigned long long* utab = P.table + U.tab_off;
+    const int lgq = lbx + lby;  // log2(nrows / 4)
+    for (uint32_t i = tid; i < ngr; i += kThreads) {
+        unsigned long long v = 0;
+        for (uint32_t spin = 0;; ++spin) {
+            v = ld_rlx(utab + i);
+            if (v & kValid) break;
+            if (spin > kSpinLimit) {
+                atomicOr(P.err, kErrTimeout);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const uint32_t g = i >> lgq;
+        const uint32_t r0 = (i & ((1u << lgq) - 1u)) << 2;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint32_t r = r0 + e;
+            const uint32_t bxl = r & (TX - 1), sxv = (r >> lbx) & 1u;
+            const uint32_t jj = (r >> (lbx + 1)) & (TY - 1), h = r >> (lbx + 1 + lby);
+            const uint32_t jy = (g << lby) + jj;
+            if (bxl < (uint32_t)hx && jy < (uint32_t)hy)
+                ft[(bxl + sxv * hx) * (uint32_t)H + jy + h * hy] = (uint16_t)((v >> (14 * e)) & 0x3fffu);
+        }
+    }
     __syncthreads();
 
-    // ---- phase 4: last arriver scans the unit's segments in flat order -----
-    // Thread t owns records [t*per, t*per + per): all its loads are issued
-    // before any is used (kScanPer in flight), then a local scan, one block
-    // scan, and the (offset, prev) stores.
-    if (misc[2]) {
-        const uint32_t nseg = (uint32_t)W * (uint32_t)H * 2u * (uint32_t)U.ntz;
-        const uint32_t per = (nseg + kThreads - 1) / kThreads;  // <= kScanPer (plan guarantees)
-        const uint32_t s0 = min(nseg, (uint32_t)tid * per), s1 = min(nseg, s0 + per);
-        const uint32_t* rec = P.segrec + U.seg_off;
-        const int ntz = U.ntz;
-        uint32_t r[kScanPer];
+    // ---- phase 5: pair offsets of my rows ----------------------------------
+    // Block scan over the W*H flat rows, 16 per thread (two 16-B LDS reads):
+    // chunk prefix = pairs before the chunk, and last kept flat index + 1
+    // before it.  Then each own row adds the (< 16) rows of its chunk before it.
+    const uint32_t nflat = (uint32_t)W * (uint32_t)H;  // <= kMaxFusedRows
+    uint32_t* cp_sum = own_prev + nrows;                // [256] chunk prefixes
+    uint32_t* cp_last = cp_sum + kThreads;
+    auto chunk_scan = [&](uint32_t c, uint32_t lim, uint32_t& sum, uint32_t& last) {
+        // sum / last over flat rows [16c, min(16c + lim, nflat))
+        const uint4* q = reinterpret_cast<const uint4*>(ft + 16 * c);
+        const uint4 a = q[0], b = q[1];
+        const uint32_t wd[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        sum = 0;
+        last = 0;
 #pragma unroll
-        for (int k = 0; k < kScanPer; ++k) r[k] = (s0 + k < s1) ? ld_rlx(rec + s0 + k) : 0u;
-        // segment flat start: s = ((I*H + J) * 2 + sz) * ntz + tz
-        auto seg_start = [&](uint32_t s) -> uint32_t {
-            const uint32_t rowi = s / (2u * ntz), rem = s - rowi * 2u * ntz;
-            const uint32_t ssz = rem / ntz, ttz = rem - ssz * ntz;
-            return (uint32_t)((uint64_t)rowi * D + ttz * TZ + ssz * hz);
-        };
-        uint32_t cnt = 0, mx = 0;  // mx: last kept flat index + 1 in my range
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            cnt += r[k] & 0xffu;
-            if (r[k] >> 8) mx = seg_start(s0 + k) + (r[k] >> 8);
-        }
-        uint32_t* s_sum = reinterpret_cast<uint32_t*>(misc + 8);   // misc[8..9]
-        uint32_t* s_max = reinterpret_cast<uint32_t*>(misc + 10);  // misc[10..11]
-        ScanOut sc = block_scan_sum_max<uint32_t>(cnt, mx, s_sum, s_max);
-        uint32_t off = (uint32_t)sc.excl_sum, prev = sc.excl_max;
-        unsigned long long* so = reinterpret_cast<unsigned long long*>(P.segoff + U.seg_off);
-#pragma unroll
-        for (int k = 0; k < kScanPer; ++k) {
-            if (s0 + k < s1) {
-                st_rlx(so + s0 + k, (unsigned long long)off | ((unsigned long long)prev << 32));
-                off += r[k] & 0xffu;
-                if (r[k] >> 8) prev = seg_start(s0 + k) + (r[k] >> 8);
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t fr = 16 * c + k;
+            const uint32_t rc = (k & 1) ? (wd[k >> 1] >> 16) : (wd[k >> 1] & 0xffffu);
+            if ((uint32_t)k < lim && fr < nflat) {
+                sum += rc & 0x7fu;
+                if (rc >> 7) last = fr * (uint32_t)D + (rc >> 7);
             }
         }
-        if (tid == 0) {
-            const uint32_t total = (uint32_t)sc.total_sum;
-            int32_t* h = reinterpret_cast<int32_t*>(P.payload + U.pay_off);
-            h[0] = W;
-            h[1] = H;
-            h[2] = D;
-            h[3] = (int32_t)U.ncells;
-            h[4] = (int32_t)total;
+    };
+    if (!(P.diag & 4u)) {
+        uint32_t csum, clast;
+        chunk_scan(tid, 16, csum, clast);
+        const ScanOut so = block_scan_sum_max<uint32_t>(csum, clast, slab, slab + 64);
+        cp_sum[tid] = (uint32_t)so.excl_sum;
+        cp_last[tid] = so.excl_max;
+        if (gme == 0 && tid == 0) {
+            const uint32_t total = (uint32_t)so.total_sum;
+            int32_t* hd = reinterpret_cast<int32_t*>(P.payload + U.pay_off);
+            hd[0] = W;
+            hd[1] = H;
+            hd[2] = D;
+            hd[3] = (int32_t)U.ncells;
+            hd[4] = (int32_t)total;
             P.kept[td.unit] = total;
             P.offsets[td.unit] = U.pay_off;
             if ((int)td.unit == P.n - 1) P.offsets[P.n] = U.pay_off + 20 + 8ull * total;
         }
-        drain_stores();
         __syncthreads();
-        if (tid == 0) st_rlx(P.ready + td.unit, 1u);
-    } else {
-        if (tid == 0) {
-            for (uint32_t spin = 0; ld_rlx(P.ready + td.unit) == 0u; ++spin) {
-                if (spin > kSpinLimit) {
-                    atomicOr(P.err, kErrTimeout);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
+        for (int r = tid; r < nrows; r += kThreads) {
+            const uint32_t bxl = r & (TX - 1), sxv = (r >> lbx) & 1u;
+            const uint32_t jj = (r >> (lbx + 1)) & (TY - 1), h = r >> (lbx + 1 + lby);
+            const uint32_t bx = td.bx0 + bxl, byv = td.by0 + jj;
+            uint32_t off = 0, prev = 0;
+            if (bx < (uint32_t)hx && byv < (uint32_t)hy) {
+                const uint32_t fr = (bx + sxv * hx) * (uint32_t)H + byv + h * hy;
+                uint32_t ps, pl;
+                chunk_scan(fr >> 4, fr & 15u, ps, pl);
+                off = cp_sum[fr >> 4] + ps;
+                prev = pl ? pl : cp_last[fr >> 4];
             }
+            own_off[r] = off;
+            own_prev[r] = prev;
         }
-        __syncthreads();
     }
+    __syncthreads();
 
-    // ---- phase 5: emit (run, value) pairs from LDS --------------------------
+    // ---- phase 6: emit (run, value) pairs, 4 columns per lane ---------------
     uint8_t* __restrict__ pairs = P.payload + U.pay_off + 20;
-    for (int ch = w; ch < nchunk; ch += 4) {
-        const unsigned long long m = masks[ch];
-        if (m == 0ull) continue;  // wave-uniform; lanes past nelem never have a mask bit
-        const int e = (ch << 6) + lane;
-        const int row = e >> lrow, col = e & (rowlen - 1);
-        const int bxl = row & (TX - 1);
-        int r2 = row >> lbx;
-        const int ssx = r2 & 1;
-        r2 >>= 1;
-        const int byl = r2 & (TY - 1), ssy = r2 >> lby;
-        const int ssz = col >> lbz, bzl = col & (TZ - 1);
-        const int bx = td.bx0 + bxl, by = td.by0 + byl;
-        const int I = bx + ssx * hx, J = by + ssy * hy, K = td.bz0 + bzl + ssz * hz;
-        const int sl = lane & ~(TZ - 1);  // first lane of my segment
-        unsigned long long so = 0;
-        if (lane == sl && ((m >> lane) & (TZ >= 64 ? ~0ull : ((1ull << TZ) - 1ull))))
-            so = ld_rlx(reinterpret_cast<const unsigned long long*>(P.segoff + U.seg_off +
-                                                                    seg_id(I, J, H, ssz, tz, U.ntz)));
-        so = __shfl(so, sl);
-        if ((m >> lane) & 1ull) {
-            const unsigned long long below = m & ((1ull << lane) - 1ull) & ~((1ull << sl) - 1ull);
-            const uint32_t rank = (uint32_t)so + (uint32_t)__popcll(below);
-            const uint32_t f = (uint32_t)(((int64_t)I * H + J) * D + K);
-            int32_t run;
-            if (below)
-                run = lane - (63 - __clzll(below)) - 1;
-            else
-                run = (int32_t)(f - (uint32_t)(so >> 32));  // f - prev - 1, with so.y = prev + 1
-            uint2 pr;
-            pr.x = (uint32_t)run;
-            pr.y = __float_as_uint(rows[row * rstride + col]);
-            *reinterpret_cast<uint2*>(pairs + 8ull * rank) = pr;
+    for (int rb = w * rpw; rb < ((P.diag & 8u) ? 0 : nrows); rb += 4 * rpw) {
+        const int row = rb + (lane >> llpr), q = lane & (lpr - 1);
+        const int zc = (4 * q) & (TZ - 1), kb = zc + ((4 * q) >> lbz) * hz;
+        const unsigned long long m = row < nrows ? masks[row] : 0ull;
+        const uint32_t nib = zc < hz ? (uint32_t)(m >> kb) & 0xfu : 0u;
+        if (nib) {
+            const int bxl = row & (TX - 1);
+            int r2 = row >> lbx;
+            const int ssx = r2 & 1;
+            r2 >>= 1;
+            const int byl = r2 & (TY - 1), ssy = r2 >> lby;
+            const uint32_t I = td.bx0 + bxl + ssx * hx, J = td.by0 + byl + ssy * hy;
+            const uint32_t fbase = (I * (uint32_t)H + J) * (uint32_t)D;
+            const unsigned long long below = m & ((1ull << kb) - 1ull);
+            uint32_t rank = own_off[row] + (uint32_t)__popcll(below);
+            // previous kept flat index + 1
+            uint32_t prev1 = below ? fbase + (uint32_t)(64 - __clzll(below)) : own_prev[row];
+            const float4 v4 = *reinterpret_cast<const float4*>(rows + row * rstride + 4 * q);
+            const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (nib & (1u << j)) {
+                    const uint32_t f = fbase + kb + j;
+                    uint2 pr;
+                    pr.x = f - prev1;  // run = f - prev - 1
+                    pr.y = __float_as_uint(vv[j]);
+                    *reinterpret_cast<uint2*>(pairs + 8ull * rank) = pr;
+                    ++rank;
+                    prev1 = f + 1;
+                }
+            }
         }
     }
 }
 
-size_t fused_lds_bytes(int lbx, int lby, int lbz) {
+size_t fused_lds_bytes(int lbx, int lby, int lbz, uint32_t ntile) {
     const size_t nrows = (size_t)4 << (lbx + lby);
     const size_t rowlen = (size_t)2 << lbz;
-    const size_t nchunk = (nrows * rowlen + 63) / 64;
-    return 128 + nrows * (rowlen + 4) * sizeof(float) + nchunk * 8;
+    // misc 128 | slab 512 | rows | masks, own_off, own_prev (16 B/row) | chunk prefixes 2 KB |
+    // flat row table (kThreads * 16 records, read as 32-B chunks)
+    (void)ntile;
+    return 128 + 512 + nrows * (rowlen + 4) * sizeof(float) + nrows * 16 + 2 * kThreads * 4 +
+           16 * kThreads * 2;
 }
 
 hipError_t launch_forward_fused(hipStream_t st, int dtype, size_t lds, const FusedParams& p) {

@@ -29,7 +29,7 @@ struct UnitDev {
     uint32_t ftile_begin;   // first flat (threshold/compaction) tile of this unit
     uint32_t nftiles;       // number of flat tiles = ceil(ncells / kFlatTile)
     uint64_t pay_off;       // payload slot: prefix of worst-case sizes, == 4 (mod 8)
-    uint64_t seg_off;       // fused units: first segment record
+    uint64_t tab_off;       // fused units: first row-table granule (4 rows per granule)
     uint32_t xt_begin;      // fused units: first tile in the fused tile list
     uint32_t ntile_u;       // fused units: tiles G of this unit
     int32_t ntz;            // z tiles per unit (segments per flat row half)
@@ -61,9 +61,8 @@ constexpr uint32_t kErrTimeout = 8u;     // a fused-kernel hand-off wait hit its
 // The fused forward kernel keeps a unit's G tiles co-resident; cap G well
 // below the resident grid (>= 1024 tiles of 256 threads on 256 CUs).
 constexpr uint32_t kMaxFusedTiles = 256;
-// ... and its segment count (flat-row pieces) to what one workgroup scans with
-// 32 records in flight per thread.
-constexpr uint64_t kMaxFusedSegments = 256 * 32;
+// ... and the unit's row table (one 14-bit record per flat row, kept in LDS).
+constexpr uint64_t kMaxFusedRows = 4096;
 
 // Parameter block of k_forward_fused (wc_fused.hip), filled by wc_capi.cpp.
 struct FusedParams {
@@ -73,16 +72,14 @@ struct FusedParams {
     uint32_t ntiles;
     int n;
     uint32_t* ticket;             // zeroed per call
-    uint32_t* arrive;             // [n], zeroed per call
-    uint32_t* ready;              // [n], zeroed per call
     unsigned long long* keyslot;  // [ntiles], zeroed per call
-    uint32_t* segrec;             // segment records: count | (last + 1) << 8
-    uint2* segoff;                // per segment: (pair offset, previous kept flat index + 1)
+    unsigned long long* table;    // row-table granules, zeroed per call
     uint8_t* payload;
     uint64_t* offsets;            // [n + 1]
     uint32_t* kept;               // [n]
     uint32_t* err;
     double keep;
+    uint32_t diag;  // diagnostics only ($WCAMD_FUSED_DIAG): skip 1 key wait, 2 table wait, 4 scan, 8 emit, 16 threshold
 };
 
 }  // namespace wc
