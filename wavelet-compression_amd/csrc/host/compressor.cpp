@@ -74,25 +74,6 @@ std::vector<float> wavelet_decompose(const Box3D& box) {
     return flat;
 }
 
-std::string xz_compress(const std::string& payload) {
-    // lzma_easy_encoder(preset 6, CRC64) + one lzma_code(LZMA_FINISH) into a
-    // buffer of 1.1 x input + 128 (src/compressor.cpp:260-285).
-    lzma_stream strm = LZMA_STREAM_INIT;
-    if (lzma_easy_encoder(&strm, 6, LZMA_CHECK_CRC64) != LZMA_OK) fatal("Failed to initialize LZMA encoder");
-    std::vector<uint8_t> out(static_cast<size_t>(payload.size() * 1.1) + 128);
-    strm.next_in = reinterpret_cast<const uint8_t*>(payload.data());
-    strm.avail_in = payload.size();
-    strm.next_out = out.data();
-    strm.avail_out = out.size();
-    if (lzma_code(&strm, LZMA_FINISH) != LZMA_STREAM_END) {
-        lzma_end(&strm);
-        fatal("LZMA compression failed");
-    }
-    const size_t used = out.size() - strm.avail_out;
-    lzma_end(&strm);
-    return std::string(reinterpret_cast<const char*>(out.data()), used);
-}
-
 }  // namespace wavelet_amd
 
 using namespace wavelet_amd;

@@ -1,0 +1,392 @@
+// modes.cpp — the reference's -c / -d / -estimate drivers (src/modes.cpp:24-327),
+// batched for the GPU.
+//
+// The reference walks (t, lev, box) with AMRIterator and calls the per-box
+// codec, one component and one unit at a time, after loading the whole run
+// into memory.  Here the same work list is cut into chunks of whole boxes
+// (about $WCAMD_CHUNK_CELLS cells, default 2^28 = 2 GiB of fp64): a chunk's
+// FAB data is read straight into one fp64 buffer (the kernel narrows to fp32,
+// as src/preprocess.cpp:78 does on load), all its units go through ONE
+// wc_forward_host call, and the payloads are xz-encoded and written by the
+// host thread pool while the next chunk is read and transformed.  Output
+// files, names and bytes are the reference's.
+#include <algorithm>
+#include <charconv>
+#include <chrono>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <filesystem>
+#include <fstream>
+#include <future>
+#include <numeric>
+
+#include "host_ctx.h"
+#include "log.h"
+#include "wavelet_amd/calc-loss.h"
+#include "wavelet_amd/iterator.h"
+#include "wavelet_amd/modes.h"
+#include "wavelet_amd/preprocess.h"
+#include "wavelet_amd/readandwrite.h"
+#include "wavelet_amd/tmpdir.h"
+#include "wavelet_amd/writeplotfile.h"
+#include "wavelet_amd/xz_pool.h"
+
+using namespace wavelet_amd;
+
+namespace {
+
+using Clock = std::chrono::high_resolution_clock;
+double since(Clock::time_point t0) { return std::chrono::duration<double>(Clock::now() - t0).count(); }
+
+// fmt's "{}" for a double: shortest representation that round-trips.
+std::string fmt_double(double v) {
+    char b[64];
+    auto r = std::to_chars(b, b + sizeof b, v);
+    return std::string(b, r.ptr);
+}
+
+uint64_t chunk_cells() {
+    if (const char* v = std::getenv("WCAMD_CHUNK_CELLS")) {
+        const long long n = std::atoll(v);
+        if (n > 0) return (uint64_t)n;
+    }
+    return 1ull << 28;
+}
+
+// The run's layout without its cell data: plotfile headers + FAB index.
+struct RunIndex {
+    std::vector<std::string> files;
+    std::vector<int> levels;
+    std::vector<int> comp_idxs;
+    std::vector<std::vector<std::vector<FabRef>>> fabs;  // [t][lev][box]
+    LocDimData locations, dimensions;
+    std::vector<std::vector<int>> box_counts;
+    AMReXInfo amrexinfo;
+    bool ok = false;
+};
+
+RunIndex index_run(const std::vector<std::string>& files, const std::vector<std::string>& components,
+                   const std::vector<int>& levels) {
+    RunIndex r;
+    r.files = files;
+    r.levels = levels;
+    for (size_t i = 0; i < files.size(); ++i) {
+        const PlotHeader h = read_plot_header(files[i]);
+        if (i == 0) {
+            r.comp_idxs = match_components(h, components);
+            if (r.comp_idxs.empty() && !components.empty()) {
+                log_error("Some components you entered were not found. Check that the names you entered match "
+                          "their names exactly in the AMReX Header files.");
+                return r;
+            }
+            r.amrexinfo.ref_ratios = h.ref_ratios;
+        }
+        if (h.dim != 3) log_error("Error: you are using a 3D build to open a " + std::to_string(h.dim) + "D plotfile");
+        r.amrexinfo.true_times.push_back(h.true_time);
+        r.amrexinfo.geomcellinfo.push_back(h.geomcell);
+        r.amrexinfo.xDim = h.xDim;
+        r.amrexinfo.yDim = h.yDim;
+        r.amrexinfo.zDim = h.zDim;
+        std::vector<int> steps(levels.size(), 0);
+        for (size_t l = 0; l < levels.size() && l < h.steps.size(); ++l) steps[l] = h.steps[l];
+        r.amrexinfo.level_steps.push_back(steps);
+        r.fabs.emplace_back();
+        r.locations.emplace_back();
+        r.dimensions.emplace_back();
+        r.box_counts.emplace_back();
+        for (int level : levels) {
+            std::vector<FabRef> fl = read_level_index(files[i], level);
+            std::vector<std::vector<int>> locs, dims;
+            for (const FabRef& f : fl) {
+                locs.push_back({f.lo[0], f.lo[1], f.lo[2]});
+                dims.push_back({f.hi[0] - f.lo[0] + 1, f.hi[1] - f.lo[1] + 1, f.hi[2] - f.lo[2] + 1});
+            }
+            r.box_counts.back().push_back((int)fl.size());
+            r.fabs.back().push_back(std::move(fl));
+            r.locations.back().push_back(std::move(locs));
+            r.dimensions.back().push_back(std::move(dims));
+        }
+    }
+    r.ok = true;
+    return r;
+}
+
+// A chunk of whole boxes, in iterator order.
+struct BoxRef {
+    int t, lev, box;
+};
+
+struct Chunk {
+    std::vector<BoxRef> boxes;
+    std::vector<wc_unit> units;     // nc units per box, comp-major within the box
+    std::vector<double> cells;      // fp64 FAB data of the selected components
+    uint64_t ncells = 0;
+};
+
+// Cut the run into chunks of about `budget` cells (at least one box each).
+std::vector<Chunk> plan_chunks(const RunIndex& r, size_t nc, uint64_t budget) {
+    std::vector<Chunk> out(1);
+    AMRIterator it(r.files.size(), r.levels.size(), r.box_counts, nc);
+    it.iterate([&](int t, int l, int b) {
+        const FabRef& f = r.fabs[t][l][b];
+        const uint64_t npts = (uint64_t)(f.hi[0] - f.lo[0] + 1) * (f.hi[1] - f.lo[1] + 1) * (f.hi[2] - f.lo[2] + 1);
+        if (!out.back().boxes.empty() && out.back().ncells + npts * nc > budget) out.emplace_back();
+        Chunk& c = out.back();
+        c.boxes.push_back({t, l, b});
+        for (size_t k = 0; k < nc; ++k) {
+            c.units.push_back(wc_unit{c.ncells + k * npts, f.hi[0] - f.lo[0] + 1, f.hi[1] - f.lo[1] + 1,
+                                      f.hi[2] - f.lo[2] + 1, 0});
+        }
+        c.ncells += npts * nc;
+    });
+    if (out.back().boxes.empty()) out.pop_back();
+    return out;
+}
+
+void load_chunk(const RunIndex& r, Chunk& c, int threads) {
+    c.cells.resize(std::max<uint64_t>(c.ncells, 1));
+    const size_t nc = r.comp_idxs.size();
+    parallel_for(c.boxes.size(), threads, [&](size_t i) {
+        const BoxRef& b = c.boxes[i];
+        read_fab(r.fabs[b.t][b.lev][b.box], r.comp_idxs, c.cells.data() + c.units[i * nc].cell_offset);
+    });
+}
+
+struct Packed {
+    std::vector<uint8_t> payload;
+    std::vector<uint64_t> offsets;
+    std::vector<uint32_t> kept;
+};
+
+Packed forward_chunk(const Chunk& c, double keep) {
+    Packed p;
+    const int n = (int)c.units.size();
+    p.payload.resize(wc_payload_bound(c.units.data(), n));
+    p.offsets.resize(n + 1);
+    p.kept.resize(n);
+    wc_ctx* ctx = thread_ctx();
+    check(ctx, wc_forward_host(ctx, c.cells.data(), WC_F64, c.units.data(), n, keep, p.payload.data(),
+                               p.payload.size(), p.offsets.data(), p.kept.data()),
+          "GPU forward");
+    return p;
+}
+
+std::string unit_name(int t, int lev, int comp, int box) {
+    return "compressed-wavelet-" + std::to_string(t) + "-" + std::to_string(lev) + "-" + std::to_string(comp) + "-" +
+           std::to_string(box) + ".xz";
+}
+
+// Payloads -> one buffer for wc_inverse_host (offsets = 4 mod 8: pairs 8-B aligned).
+void inverse_batch(const std::vector<std::string>& payloads, const std::vector<wc_unit>& units, float* out) {
+    std::vector<uint64_t> offs(payloads.size());
+    uint64_t cur = 4;
+    for (size_t i = 0; i < payloads.size(); ++i) {
+        if (payloads[i].size() < 20) fatal("Deserialization failed: payload shorter than its header");
+        offs[i] = cur;
+        cur += (payloads[i].size() + 4 + 7) / 8 * 8;
+    }
+    std::vector<uint8_t> buf(cur + 8, 0);
+    for (size_t i = 0; i < payloads.size(); ++i) std::memcpy(buf.data() + offs[i], payloads[i].data(), payloads[i].size());
+    wc_ctx* ctx = thread_ctx();
+    check(ctx, wc_inverse_host(ctx, buf.data(), offs.data(), units.data(), (int)units.size(), out), "GPU decompress");
+}
+
+// Compress every unit of `r` into `dir` (file names joined as std::filesystem
+// paths, src/compressor.cpp:250-254).  `on_chunk` sees each chunk after its
+// forward pass (estimate mode keeps the cells for the RMSE).
+template <class OnChunk>
+void compress_run(const RunIndex& r, double keep, const std::filesystem::path& dir, OnChunk on_chunk) {
+    const size_t nc = r.comp_idxs.size();
+    const int threads = host_threads();
+    std::vector<Chunk> chunks = plan_chunks(r, nc, chunk_cells());
+    std::future<void> xz_done;  // xz of the previous chunk, overlapped with this one's read + GPU pass
+    std::shared_ptr<Packed> prev;
+    for (Chunk& c : chunks) {
+        load_chunk(r, c, threads);
+        auto p = std::make_shared<Packed>(forward_chunk(c, keep));
+        std::vector<XzJob> jobs;
+        for (size_t i = 0; i < c.boxes.size(); ++i)
+            for (size_t k = 0; k < nc; ++k) {
+                const size_t u = i * nc + k;
+                const BoxRef& b = c.boxes[i];
+                jobs.push_back(XzJob{p->payload.data() + p->offsets[u], 20 + 8ull * p->kept[u],
+                                     (dir / unit_name(b.t, b.lev, r.comp_idxs[k], b.box)).string()});
+            }
+        if (xz_done.valid()) xz_done.get();
+        prev = p;
+        xz_done = std::async(std::launch::async, [jobs = std::move(jobs), p, threads]() { xz_write_files(jobs, threads); });
+        on_chunk(c);
+        c.cells.clear();
+        c.cells.shrink_to_fit();
+    }
+    if (xz_done.valid()) xz_done.get();
+}
+
+}  // namespace
+
+int compress(const Config& cfg) {
+    const std::vector<std::string> files = format_files(cfg.data_dir, cfg.min_time, cfg.max_time);
+    const std::vector<int> levels = format_levels(cfg.min_level, cfg.max_level);
+    const int num_times = (int)files.size(), num_levels = (int)levels.size();
+    const int num_components = (int)cfg.components.size();
+    log_info("Processing data...");
+    const auto t0 = Clock::now();
+    RunIndex r = index_run(files, cfg.components, levels);
+    if (!r.ok) return 1;
+    RunInfo runinfo{files, cfg.min_level, cfg.max_level, cfg.components, r.comp_idxs};
+    AMRIterator iterator(num_times, num_levels, r.box_counts, num_components);
+    if (!cfg.compressed_dir.empty() && !std::filesystem::exists(cfg.compressed_dir)) {
+        std::error_code ec;
+        std::filesystem::create_directories(cfg.compressed_dir, ec);
+        if (ec) log_error("Failed to create compressed directory " + cfg.compressed_dir + ": " + ec.message());
+    }
+    write_runinfo(runinfo, cfg.compressed_dir, "runinfo.raw");
+    write_loc_dim_to_bin(r.locations, cfg.compressed_dir, "locations.raw", iterator);
+    write_loc_dim_to_bin(r.dimensions, cfg.compressed_dir, "dimensions.raw", iterator);
+    write_box_counts(r.box_counts, cfg.compressed_dir, "boxcounts.raw", num_times, num_levels);
+    write_amrexinfo(r.amrexinfo, cfg.compressed_dir, "amrexinfo.raw");
+    log_info("Successfully processed data in " + fmt_double(since(t0)) + " seconds. Beginning compression...");
+    const auto t1 = Clock::now();
+    compress_run(r, (double)cfg.keep, std::filesystem::path(cfg.compressed_dir), [](const Chunk&) {});
+    log_info("Compression completed in " + fmt_double(since(t1)) + " seconds.");
+    return 0;
+}
+
+int decompress(const Config& cfg) {
+    RunInfo runinfo = read_runinfo(cfg.compressed_dir, "runinfo.raw");
+    const std::vector<int> levels = format_levels(runinfo.min_level, runinfo.max_level);
+    const int num_times = (int)runinfo.files.size(), num_levels = (int)levels.size();
+    const int num_components = (int)runinfo.components.size();
+    if (num_times > 0)
+        log_info("Decompressing data between timestep " + runinfo.files.front() + " and " + runinfo.files.back() +
+                 ", level " + std::to_string(runinfo.min_level) + " and " + std::to_string(runinfo.max_level) +
+                 ", for " + std::to_string(num_components) + " components");
+    log_info("Beginning decompression...");
+    const auto t0 = Clock::now();
+    const std::vector<std::vector<int>> counts = read_box_counts(cfg.compressed_dir, "boxcounts.raw", num_times, num_levels);
+    AMRIterator iterator(num_times, num_levels, counts, num_components);
+    const AMReXInfo info = read_amrex_info(cfg.compressed_dir, "amrexinfo.raw");
+    const LocDimData locs = read_loc_dim_from_bin(cfg.compressed_dir, "locations.raw", counts, iterator, num_times, num_levels);
+    const LocDimData dims = read_loc_dim_from_bin(cfg.compressed_dir, "dimensions.raw", counts, iterator, num_times, num_levels);
+    const int threads = host_threads();
+    double t_decode = 0;
+    // One timestep at a time: decode its files on the pool, one GPU inverse
+    // for all its units, then write its plotfile.
+    for (int t = 0; t < num_times; ++t) {
+        const auto ts = Clock::now();
+        std::vector<std::string> paths;
+        std::vector<wc_unit> units;
+        uint64_t cursor = 0;
+        for (int l = 0; l < num_levels; ++l)
+            for (int b = 0; b < counts[t][l]; ++b)
+                for (int comp : runinfo.comp_idxs) {
+                    paths.push_back(cfg.compressed_dir + unit_name(t, l, comp, b));  // string concatenation (src/modes.cpp:157)
+                    (void)comp;
+                }
+        std::vector<std::string> payloads = xz_read_files(paths, threads);
+        for (const std::string& p : payloads) {
+            if (p.size() < 20) fatal("Deserialization failed: payload shorter than its header");
+            int32_t h[3];
+            std::memcpy(h, p.data(), sizeof h);
+            wc_unit u{cursor, std::max(h[0], 0), std::max(h[1], 0), std::max(h[2], 0), 0};
+            cursor += (uint64_t)u.nx * u.ny * u.nz;
+            cursor = (cursor + 3) & ~uint64_t(3);
+            units.push_back(u);
+        }
+        std::vector<float> cells(std::max<uint64_t>(cursor, 1));
+        inverse_batch(payloads, units, cells.data());
+        payloads.clear();
+        std::vector<std::vector<std::vector<multiBox3D>>> regen(1);
+        regen[0].resize(num_levels);
+        size_t u = 0;
+        for (int l = 0; l < num_levels; ++l)
+            for (int b = 0; b < counts[t][l]; ++b) {
+                multiBox3D mb;
+                for (int c = 0; c < num_components; ++c, ++u) {
+                    Box3D box(units[u].nx, units[u].ny, units[u].nz);
+                    if (box.data_size()) std::memcpy(box.data(), cells.data() + units[u].cell_offset, 4 * box.data_size());
+                    mb.push_back(std::move(box));
+                }
+                regen[0][l].push_back(std::move(mb));
+            }
+        t_decode += since(ts);
+        AMReXInfo one = info;
+        one.true_times = {info.true_times[t]};
+        one.geomcellinfo = {info.geomcellinfo[t]};
+        one.level_steps = {info.level_steps[t]};
+        write_plotfiles(std::move(regen), {locs[t]}, {dims[t]}, {runinfo.files[t]}, num_levels, num_components,
+                        runinfo.components, one, cfg.out_dir);
+    }
+    log_info("Decompression completed in " + fmt_double(t_decode) + " seconds.");
+    log_info("Sucessfully wrote plotfiles.");
+    (void)t0;
+    return 0;
+}
+
+int estimate(Config& cfg) {
+    const int num_components = (int)cfg.components.size();
+    TempDir scratch;
+    const std::vector<std::string> files = format_files(cfg.data_dir, cfg.min_time, cfg.min_time);
+    const std::vector<int> levels{cfg.min_level};
+    RunIndex r = index_run(files, cfg.components, levels);
+    if (!r.ok || files.empty()) return 1;
+    const size_t nc = r.comp_idxs.size();
+    // Keep each chunk's cells for the RMSE; min/max over the narrowed values.
+    std::vector<Chunk> kept_chunks;
+    std::vector<float> minv(nc, FLT_MAX), maxv(nc, FLT_MIN);  // src/preprocess.cpp:30-31 quirk
+    compress_run(r, (double)cfg.keep, scratch.path(), [&](Chunk& c) {
+        for (size_t u = 0; u < c.units.size(); ++u) {
+            const size_t k = u % nc;
+            const uint64_t n = (uint64_t)c.units[u].nx * c.units[u].ny * c.units[u].nz;
+            const double* s = c.cells.data() + c.units[u].cell_offset;
+            for (uint64_t i = 0; i < n; ++i) {
+                const float v = (float)s[i];
+                if (v < minv[k]) minv[k] = v;
+                if (v > maxv[k]) maxv[k] = v;
+            }
+        }
+        Chunk keep;
+        keep.boxes = c.boxes;
+        keep.units = c.units;
+        keep.ncells = c.ncells;
+        keep.cells.swap(c.cells);
+        kept_chunks.push_back(std::move(keep));
+    });
+    log_info("Compression complete.");
+    // Decompress from the written files, then per-box RMSE on the GPU.
+    std::vector<std::vector<double>> all_rmses(nc);
+    const int threads = host_threads();
+    for (Chunk& c : kept_chunks) {
+        std::vector<std::string> paths;
+        for (const BoxRef& b : c.boxes)
+            for (size_t k = 0; k < nc; ++k) paths.push_back((scratch.path() / unit_name(b.t, b.lev, r.comp_idxs[k], b.box)).string());
+        std::vector<std::string> payloads = xz_read_files(paths, threads);
+        std::vector<float> regen(std::max<uint64_t>(c.ncells, 1));
+        inverse_batch(payloads, c.units, regen.data());
+        std::vector<double> rmse(c.units.size());
+        wc_ctx* ctx = thread_ctx();
+        check(ctx, wc_rmse_host(ctx, c.cells.data(), WC_F64, regen.data(), c.units.data(), (int)c.units.size(), rmse.data()),
+              "GPU RMSE");
+        for (size_t u = 0; u < rmse.size(); ++u) all_rmses[u % nc].push_back(rmse[u]);
+    }
+    log_info("Decompression complete.");
+    for (int c = 0; c < num_components && c < (int)nc; ++c) {
+        const double mean = std::accumulate(all_rmses[c].begin(), all_rmses[c].end(), 0.0) / all_rmses[c].size();
+        log_info("Predicted RMSE, " + cfg.components[c] + " = " + fmt_double(mean));
+        const double loss = calc_adj_loss(mean, maxv[c] - minv[c]);
+        log_info("Predicted Adjusted loss, " + cfg.components[c] + " = " + fmt_double(loss));
+    }
+    // compressed size vs the level's raw size scaled to the compressed components (src/modes.cpp:294-324)
+    std::ifstream x(files[0] + "/Header");
+    if (!x.is_open()) log_error("Failed to open header file: " + files[0]);
+    std::string str;
+    int ncomp_file = 1;
+    x >> str >> ncomp_file;
+    double raw_size = calc_size(files[0] + "/Level_" + std::to_string(levels[0]) + "/");
+    raw_size /= ncomp_file;
+    raw_size *= num_components;
+    const double compressed_size = calc_size(scratch.path().string());
+    log_info("Predicted compressed size: " + fmt_double(compressed_size / raw_size * 100) + "%");
+    return 0;
+}

@@ -250,7 +250,8 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         // fused: tiles span the whole x and z extent (one tile row per y block
         // range), G <= kMaxFusedTiles, the row table fits kMaxFusedRows.
         const uint64_t nrows_tile = (uint64_t)4 << (d.lbx + d.lby);
-        const bool fused_ok = fast_ok && d.nbx <= (1 << d.lbx) && d.ntz == 1 && ntile <= kMaxFusedTiles &&
+        const bool fused_ok = fast_ok && (u.cell_offset % 2 == 0) && d.nbx <= (1 << d.lbx) && d.ntz == 1 &&
+                              ntile <= kMaxFusedTiles &&
                               ntile * nrows_tile <= kMaxFusedRows;
         if (fused_ok && c->opt_fused) {
             d.fused = 1;
@@ -366,7 +367,6 @@ int forward_impl(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, 
         fp.kept = d_kept;
         fp.err = (uint32_t*)c->errflag.p;
         fp.keep = keep;
-        if (const char* dg = std::getenv("WCAMD_FUSED_DIAG")) fp.diag = (uint32_t)std::atoi(dg);
         {
             StageTimer t(c, WC_STAGE_FUSED);
             e = launch_forward_fused(c->stream, dtype, P.lds_fused, fp);

@@ -67,52 +67,178 @@ __device__ __forceinline__ double key_thresh(unsigned long long key, double keep
 
 
 
+// Per-tile descriptors are read-only for the whole launch: read them through
+// the constant address space so uniform indices become scalar (SMEM) loads
+// into SGPRs instead of per-lane copies in VGPRs.
+#define WC_CONST __attribute__((address_space(4)))
+__device__ __forceinline__ XTile tile_at(const FusedParams& P, uint32_t t) {
+    const WC_CONST XTile* p = (const WC_CONST XTile*)(uintptr_t)P.tiles + t;
+    XTile r;
+    r.unit = p->unit;
+    r.bx0 = p->bx0;
+    r.by0 = p->by0;
+    r.bz0 = p->bz0;
+    return r;
+}
+__device__ __forceinline__ const WC_CONST UnitDev& unit_at(const FusedParams& P, uint32_t u) {
+    return ((const WC_CONST UnitDev*)(uintptr_t)P.units)[u];
+}
+
+// Lane-explicit wave64 shuffles (ds_bpermute from a caller-supplied lane):
+// inside the persistent loop `lane` is opaque, so the compiler cannot hoist
+// the per-lane shuffle addresses out of the loop and keep them live.
+__device__ __forceinline__ uint32_t bperm(uint32_t v, int src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
+}
+__device__ __forceinline__ unsigned long long bperm64(unsigned long long v, int src) {
+    return (unsigned long long)bperm((uint32_t)v, src) | ((unsigned long long)bperm((uint32_t)(v >> 32), src) << 32);
+}
+__device__ __forceinline__ unsigned long long wmax64(unsigned long long v, int lane) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long x = bperm64(v, lane ^ o);
+        v = x > v ? x : v;
+    }
+    return v;
+}
+// Block-wide (kThreads) exclusive sum + exclusive max; scratch s[0..3], s[64..67].
+__device__ __forceinline__ void block_scan2(uint32_t v, uint32_t m, int tid, uint32_t* s, uint32_t& esum,
+                                            uint32_t& emax, uint32_t& tsum) {
+    const int l = tid & 63, w = tid >> 6;
+    uint32_t incl = v, im = m;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int src = l >= o ? l - o : l;
+        const uint32_t a = bperm(incl, src), b = bperm(im, src);
+        if (l >= o) {
+            incl += a;
+            im = b > im ? b : im;
+        }
+    }
+    if (l == 63) {
+        s[w] = incl;
+        s[64 + w] = im;
+    }
+    __syncthreads();
+    uint32_t wbase = 0, wmax = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kThreads / 64; ++i) {
+        if (i < w) {
+            wbase += s[i];
+            wmax = s[64 + i] > wmax ? s[64 + i] : wmax;
+        }
+        tot += s[i];
+    }
+    __syncthreads();
+    uint32_t em = bperm(im, l > 0 ? l - 1 : 0);
+    if (l == 0) em = 0;
+    esum = wbase + incl - v;
+    emax = em > wmax ? em : wmax;
+    tsum = tot;
+}
+
+template <typename T>
+struct Pair2;
+template <>
+struct Pair2<double> {
+    using type = double2;
+};
+template <>
+struct Pair2<float> {
+    using type = float2;
+};
+
+// One transform column of a tile: x-pair x y-pair x 8 z-planes of raw cells
+// (4 z-blocks), held in registers from issue to use so the loads of the
+// next tile stay in flight while the current tile waits on its unit.
+template <typename T>
+struct RawCol {
+    typename Pair2<T>::type r[8][2];
+    bool act;
+};
+
+template <typename T>
+__device__ __forceinline__ void issue_col(const FusedParams& P, const XTile& td, const WC_CONST UnitDev& U, int ci,
+                                          RawCol<T>& c) {
+    const int lbx = U.lbx, lby = U.lby;
+    const int TX = 1 << lbx, TY = 1 << lby, TZ = 1 << U.lbz;
+    const int bxl = ci & (TX - 1), byl = (ci >> lbx) & (TY - 1), bzq = ci >> (lbx + lby);
+    const int bx = td.bx0 + bxl, by = td.by0 + byl, bzb = td.bz0 + 4 * bzq;
+    c.act = ci < ((TX * TY * TZ) >> 2) && bx < U.hx && by < U.hy && bzb < U.hz;
+    // fused units have an even cell offset (host check): x-pairs are aligned vectors
+    const uint32_t sy = (uint32_t)U.nx, sz = (uint32_t)U.nx * (uint32_t)U.ny;
+    const uint32_t o0 = c.act ? 2u * bx + sy * (2u * by) + sz * (2u * bzb) : 0u;
+    const T* __restrict__ base = static_cast<const T*>(P.cells) + U.cell_off;
+    using V = typename Pair2<T>::type;
+#pragma unroll
+    for (int zp = 0; zp < 8; ++zp)
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) {
+            if (c.act)
+                c.r[zp][dy] = *reinterpret_cast<const V*>(base + (o0 + sz * zp + sy * dy));
+            else
+                c.r[zp][dy] = V{0, 0};
+        }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kThreads, 3) void k_forward_fused(FusedParams P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    // misc[0] ticket, misc[1] thresh bits, misc[4..7] wave key maxima, misc[8..11] scan scratch
+    const int tid0 = threadIdx.x;
+    // misc[0] current tile, misc[1] thresh bits, misc[2] prefetched tile, misc[4..7] wave key maxima
     unsigned long long* misc = reinterpret_cast<unsigned long long*>(lds);
-    if (tid == 0) misc[0] = atomicAdd(P.ticket, 1u);
+    if (tid0 == 0) misc[0] = atomicAdd(P.ticket, 1u);
     __syncthreads();
-    const uint32_t t = (uint32_t)misc[0];
+    uint32_t t = __builtin_amdgcn_readfirstlane((uint32_t)misc[0]);
     if (t >= P.ntiles) return;
-    const XTile td = P.tiles[t];
-    const UnitDev& U = P.units[td.unit];
+    RawCol<T> raw;
+    {
+        const XTile tt = tile_at(P, t);
+        issue_col<T>(P, tt, unit_at(P, tt.unit), tid0, raw);
+    }
+
+    // Persistent loop.  Tickets are claimed in order, so a unit's tiles hold
+    // consecutive tickets; a workgroup waits only on its current tile's unit
+    // and prefetches only a ticket of a LATER unit, so every waited-on tile is
+    // either running or unclaimed (claimable by a finishing workgroup).
+    for (;;) {
+    int tid;  // opaque per iteration: keeps lane-derived values from being hoisted and held live
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"(tid0));
+    const int w = tid >> 6, lane = tid & 63;
+    const XTile td = tile_at(P, t);
+    const WC_CONST UnitDev& U = unit_at(P, td.unit);
     const int W = U.nx, H = U.ny, D = U.nz;
     const int hx = U.hx, hy = U.hy, hz = U.hz;
     const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
     const int TX = 1 << lbx, TY = 1 << lby, TZ = 1 << lbz;
-    const int rowlen = 2 * TZ, rstride = rowlen + 4;   // rowlen == D: the tile spans all of z
+    const int rowlen = 2 * TZ, rstride = rowlen + 4;   // the tile spans all of z
     const int nrows = 4 * TX * TY;
     const uint32_t G = U.ntile_u;
     const uint32_t gme = t - U.xt_begin;               // my tile index within the unit (along y)
     // LDS carve (16-B aligned pieces)
-    uint32_t* slab = reinterpret_cast<uint32_t*>(lds + 32);  // [0,64) slab totals/bases, [64,128) slab last
+    uint32_t* slab = reinterpret_cast<uint32_t*>(lds + 32);  // block-scan scratch
     float* rows = lds + 32 + 128;
     unsigned long long* masks = reinterpret_cast<unsigned long long*>(rows + nrows * rstride);  // per row
     uint32_t* own_off = reinterpret_cast<uint32_t*>(masks + nrows);
     uint32_t* own_prev = own_off + nrows;
     uint16_t* tab = reinterpret_cast<uint16_t*>(own_prev + nrows + 2 * kThreads);  // 4096 records; rec[] aliases
 
-    // ---- phase 1: load + transform into LDS rows, local max key ----------
-    const int64_t sy = W, sz = (int64_t)W * H;
-    const T* __restrict__ src = static_cast<const T*>(P.cells) + U.cell_off;
-    const bool vec = (U.cell_off & 1) == 0;
-    const int ncol = (TX * TY * TZ) >> 2;
+    // ---- phase 1: transform the landed column into LDS rows, local max key -
     unsigned long long kmax = 0;
-    for (int ci = tid; ci < ncol; ci += kThreads) {
+    if (raw.act) {
+        const int ci = tid;
         const int bxl = ci & (TX - 1);
         const int byl = (ci >> lbx) & (TY - 1);
         const int bzq = ci >> (lbx + lby);
         const int bx = td.bx0 + bxl, by = td.by0 + byl, bzb = td.bz0 + 4 * bzq;
-        if (bx >= hx || by >= hy || bzb >= hz) continue;
         float v[8][2][2];
-        const T* p0 = src + 2 * (int64_t)bx + sy * (2 * by) + sz * (2 * (int64_t)bzb);
 #pragma unroll
         for (int zp = 0; zp < 8; ++zp)
 #pragma unroll
-            for (int dy = 0; dy < 2; ++dy) load_xpair<T>(p0 + sz * zp + sy * dy, true, vec, v[zp][dy][0], v[zp][dy][1]);
+            for (int dy = 0; dy < 2; ++dy) {
+                v[zp][dy][0] = (float)raw.r[zp][dy].x;  // fp64 -> fp32 RNE, src/preprocess.cpp:78
+                v[zp][dy][1] = (float)raw.r[zp][dy].y;
+            }
         float c[4][2][2][2];  // [q][sz][sy][sx]
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -158,9 +284,24 @@ __global__ __launch_bounds__(kThreads, 3) void k_forward_fused(FusedParams P) {
                     }
                 }
     }
-    kmax = wave_max_u64(kmax);
+    kmax = wmax64(kmax, lane);
     if (lane == 0) misc[4 + w] = kmax;
+    // claim the next tile now, so its loads overlap this tile's hand-offs --
+    // only when the counter has already passed my unit: it never decreases,
+    // so the ticket the add returns is then of a later unit too.
+    if (tid == 0) {
+        const uint32_t later = U.xt_begin + G;  // first ticket of a later unit
+        const uint32_t cur = __hip_atomic_load(P.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t nxt = 0xffffffffu;
+        if (cur >= later && cur < P.ntiles) nxt = atomicAdd(P.ticket, 1u);
+        misc[2] = nxt;
+    }
     __syncthreads();
+    const uint32_t tnext = __builtin_amdgcn_readfirstlane((uint32_t)misc[2]);
+    if (tnext < P.ntiles) {
+        const XTile tt = tile_at(P, tnext);
+        issue_col<T>(P, tt, unit_at(P, tt.unit), tid, raw);
+    }
 
     // ---- phase 2: publish the key granule, wait for the unit's G granules --
     if (tid == 0) {
@@ -168,9 +309,7 @@ __global__ __launch_bounds__(kThreads, 3) void k_forward_fused(FusedParams P) {
         for (int i = 1; i < 4; ++i) k = misc[4 + i] > k ? misc[4 + i] : k;
         st_rlx(P.keyslot + t, k | kValid);
     }
-    if (w == 0 && (P.diag & 1u)) {
-        if (lane == 0) misc[1] = (unsigned long long)__double_as_longlong(key_thresh(misc[4], P.keep));
-    } else if (w == 0) {
+    if (w == 0) {
         unsigned long long best = 0;
         for (uint32_t g0 = 0; g0 < G; g0 += 64) {
             const uint32_t gi = g0 + lane;
@@ -187,7 +326,7 @@ __global__ __launch_bounds__(kThreads, 3) void k_forward_fused(FusedParams P) {
             }
             best = v > best ? v : best;
         }
-        best = wave_max_u64(best);
+        best = wmax64(best, lane);
         if (lane == 0) misc[1] = (unsigned long long)__double_as_longlong(key_thresh(best, P.keep));
     }
     __syncthreads();
@@ -201,7 +340,7 @@ __global__ __launch_bounds__(kThreads, 3) void k_forward_fused(FusedParams P) {
     const int rpw = 64 >> llpr;                    // rows per wave-iteration
     const float tf = thresh_as_float(thresh);
     uint16_t* rec = tab;  // my records, published below, then overwritten by the table
-    for (int rb = w * rpw; rb < ((P.diag & 16u) ? 0 : nrows); rb += 4 * rpw) {
+    for (int rb = w * rpw; rb < nrows; rb += 4 * rpw) {
         const int row = rb + (lane >> llpr), q = lane & (lpr - 1);
         const int bxl = row & (TX - 1);
         const int byl = ((row >> lbx) >> 1) & (TY - 1);
@@ -214,7 +353,7 @@ __global__ __launch_bounds__(kThreads, 3) void k_forward_fused(FusedParams P) {
                                  ((uint32_t)(fabsf(v4.z) > tf) << 2) | ((uint32_t)(fabsf(v4.w) > tf) << 3);
             m = (unsigned long long)nib << kb;  // masks are in flat K order (bit K of row (I, J))
         }
-        for (int o = 1; o < lpr; o <<= 1) m |= __shfl_xor(m, o);
+        for (int o = 1; o < lpr; o <<= 1) m |= bperm64(m, lane ^ o);
         if (q == 0 && row < nrows) {
             masks[row] = m;
             const uint32_t last1 = m ? (uint32_t)(64 - __clzll(m)) : 0u;
@@ -238,7 +377,7 @@ __global__ __launch_bounds__(kThreads, 3) void k_forward_fused(FusedParams P) {
     // (I, J) = (bxl + sx*hx, g*TY + jj + h*hy).  Every valid (I, J) has exactly
     // one writer, so ft[0 .. W*H) ends up fully defined.
     uint16_t* ft = tab;
-    const uint32_t ngr = (P.diag & 2u) ? 0u : G * (uint32_t)(nrows >> 2);
+    const uint32_t ngr = G * (uint32_t)(nrows >> 2);
     const unsigned long long* utab = P.table + U.tab_off;
     const int lgq = lbx + lby;  // log2(nrows / 4)
     for (uint32_t i = tid; i < ngr; i += kThreads) {
@@ -290,14 +429,13 @@ __global__ __launch_bounds__(kThreads, 3) void k_forward_fused(FusedParams P) {
             }
         }
     };
-    if (!(P.diag & 4u)) {
-        uint32_t csum, clast;
+    {
+        uint32_t csum, clast, esum, emax, total;
         chunk_scan(tid, 16, csum, clast);
-        const ScanOut so = block_scan_sum_max<uint32_t>(csum, clast, slab, slab + 64);
-        cp_sum[tid] = (uint32_t)so.excl_sum;
-        cp_last[tid] = so.excl_max;
+        block_scan2(csum, clast, tid, slab, esum, emax, total);
+        cp_sum[tid] = esum;
+        cp_last[tid] = emax;
         if (gme == 0 && tid == 0) {
-            const uint32_t total = (uint32_t)so.total_sum;
             int32_t* hd = reinterpret_cast<int32_t*>(P.payload + U.pay_off);
             hd[0] = W;
             hd[1] = H;
@@ -329,7 +467,7 @@ __global__ __launch_bounds__(kThreads, 3) void k_forward_fused(FusedParams P) {
 
     // ---- phase 6: emit (run, value) pairs, 4 columns per lane ---------------
     uint8_t* __restrict__ pairs = P.payload + U.pay_off + 20;
-    for (int rb = w * rpw; rb < ((P.diag & 8u) ? 0 : nrows); rb += 4 * rpw) {
+    for (int rb = w * rpw; rb < nrows; rb += 4 * rpw) {
         const int row = rb + (lane >> llpr), q = lane & (lpr - 1);
         const int zc = (4 * q) & (TZ - 1), kb = zc + ((4 * q) >> lbz) * hz;
         const unsigned long long m = row < nrows ? masks[row] : 0ull;
@@ -362,6 +500,21 @@ __global__ __launch_bounds__(kThreads, 3) void k_forward_fused(FusedParams P) {
             }
         }
     }
+
+    __syncthreads();  // this tile's LDS is free
+    if (tnext < P.ntiles) {
+        t = tnext;
+        continue;
+    }
+    if (tid0 == 0) misc[0] = atomicAdd(P.ticket, 1u);
+    __syncthreads();
+    t = __builtin_amdgcn_readfirstlane((uint32_t)misc[0]);
+    if (t >= P.ntiles) return;
+    {
+        const XTile tt = tile_at(P, t);
+        issue_col<T>(P, tt, unit_at(P, tt.unit), tid, raw);
+    }
+    }
 }
 
 size_t fused_lds_bytes(int lbx, int lby, int lbz, uint32_t ntile) {
@@ -374,12 +527,35 @@ size_t fused_lds_bytes(int lbx, int lby, int lbz, uint32_t ntile) {
            16 * kThreads * 2;
 }
 
+// Persistent grid: one workgroup per resident slot (never more than the tiles).
+// Residency is not needed for correctness (tickets order the work), only for
+// not launching workgroups that would find the ticket counter exhausted.
+template <typename T>
+static uint32_t fused_grid(size_t lds, uint32_t ntiles) {
+    static thread_local size_t c_lds = 0;
+    static thread_local uint32_t c_slots = 0;
+    static thread_local int c_dev = -1;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (c_lds != lds || c_dev != dev) {
+        int per_cu = 0, ncu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_forward_fused<T>, kThreads, lds) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 ||
+            ncu < 1)
+            return ntiles;
+        c_lds = lds;
+        c_dev = dev;
+        c_slots = (uint32_t)per_cu * (uint32_t)ncu;
+    }
+    return ntiles < c_slots ? ntiles : c_slots;
+}
+
 hipError_t launch_forward_fused(hipStream_t st, int dtype, size_t lds, const FusedParams& p) {
     if (p.ntiles == 0) return hipSuccess;
     if (dtype == 1)
-        k_forward_fused<double><<<p.ntiles, kThreads, lds, st>>>(p);
+        k_forward_fused<double><<<fused_grid<double>(lds, p.ntiles), kThreads, lds, st>>>(p);
     else
-        k_forward_fused<float><<<p.ntiles, kThreads, lds, st>>>(p);
+        k_forward_fused<float><<<fused_grid<float>(lds, p.ntiles), kThreads, lds, st>>>(p);
     return hipGetLastError();
 }
 

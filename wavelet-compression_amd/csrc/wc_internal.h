@@ -79,7 +79,6 @@ struct FusedParams {
     uint32_t* kept;               // [n]
     uint32_t* err;
     double keep;
-    uint32_t diag;  // diagnostics only ($WCAMD_FUSED_DIAG): skip 1 key wait, 2 table wait, 4 scan, 8 emit, 16 threshold
 };
 
 }  // namespace wc

@@ -214,3 +214,69 @@ def format_files(data_dir: str, min_time: str, max_time: str) -> List[str]:
 def format_levels(min_level: int, max_level: int) -> List[int]:
     """src/argparse.cpp:164-172."""
     return list(range(min_level, max_level + 1))
+
+
+def _r17(v: float) -> str:
+    return "%.17g" % v
+
+
+def _box(lo, hi) -> str:
+    return "((%d,%d,%d) (%d,%d,%d) (0,0,0))" % (lo[0], lo[1], lo[2], hi[0], hi[1], hi[2])
+
+
+_FAB_REAL = "FAB ((8, (64 11 52 0 1 12 0 1023)),(8, (8 7 6 5 4 3 2 1)))"
+
+
+def write_plotfile(path, names: Sequence[str], time: float, geomcell: Sequence[float], ref_ratio: int,
+                   base_dims: Tuple[int, int, int], level_steps: Sequence[int], levels) -> None:
+    """Single-rank amrex::WriteMultiLevelPlotfile output, as the C++ writer
+    (csrc/host/writeplotfile.cpp) produces it.  levels[l] = list of
+    (lo (x, y, z), data float64 (ncomp, D, H, W)).  Used by the tests to build
+    plotfile inputs on machines without the reference's fixtures."""
+    pdir = Path(path)
+    nlev = len(levels)
+    ncell = [[int(base_dims[k] * ref_ratio ** l) for k in range(3)] for l in range(nlev)]
+    dx = [[(geomcell[3 + k] - geomcell[k]) / ncell[l][k] for k in range(3)] for l in range(nlev)]
+    out = ["HyperCLaw-V1.1\n", f"{len(names)}\n"] + [f"{n}\n" for n in names]
+    out += ["3\n", _r17(time) + "\n", f"{nlev - 1}\n"]
+    out.append("".join(_r17(geomcell[k]) + " " for k in range(3)) + "\n")
+    out.append("".join(_r17(geomcell[3 + k]) + " " for k in range(3)) + "\n")
+    out.append("".join(f"{ref_ratio} " for _ in range(1, nlev)) + "\n")
+    out.append("".join(_box((0, 0, 0), [n - 1 for n in ncell[l]]) + " " for l in range(nlev)) + "\n")
+    out.append("".join(f"{s} " for s in level_steps[:nlev]) + "\n")
+    for l in range(nlev):
+        out.append("".join(_r17(d) + " " for d in dx[l]) + "\n")
+    out.append("0\n0\n")
+    for l, fabs in enumerate(levels):
+        out.append(f"{l} {len(fabs)} {_r17(time)}\n{level_steps[l]}\n")
+        for lo, data in fabs:
+            D, H, W = data.shape[1:]
+            for k, n in enumerate((W, H, D)):
+                out.append(_r17(geomcell[k] + dx[l][k] * lo[k]) + " " + _r17(geomcell[k] + dx[l][k] * (lo[k] + n)) + "\n")
+        out.append(f"Level_{l}/Cell\n")
+        ldir = pdir / f"Level_{l}"
+        ldir.mkdir(parents=True, exist_ok=True)
+        offs, mins, maxs, boxes = [], [], [], []
+        pos = 0
+        with open(ldir / "Cell_D_00000", "wb") as f:
+            for lo, data in fabs:
+                D, H, W = data.shape[1:]
+                hi = (lo[0] + W - 1, lo[1] + H - 1, lo[2] + D - 1)
+                boxes.append(_box(lo, hi))
+                hdr = (_FAB_REAL + _box(lo, hi) + f" {data.shape[0]}\n").encode()
+                offs.append(pos)
+                f.write(hdr)
+                arr = np.ascontiguousarray(data, dtype="<f8")
+                f.write(arr.tobytes())
+                pos += len(hdr) + arr.nbytes
+                mins.append([float(arr[c].min()) for c in range(arr.shape[0])])
+                maxs.append([float(arr[c].max()) for c in range(arr.shape[0])])
+        ncomp = len(names)
+        ch = [f"1\n1\n{ncomp}\n0\n({len(fabs)} 0\n"] + [b + "\n" for b in boxes] + [f")\n{len(fabs)}\n"]
+        ch += [f"FabOnDisk: Cell_D_00000 {o}\n" for o in offs]
+        for mm in (mins, maxs):
+            ch.append(f"\n{len(fabs)},{ncomp}\n")
+            ch += ["".join("%.16e," % v for v in row) + "\n" for row in mm]
+        ch.append("\n")
+        (ldir / "Cell_H").write_text("".join(ch))
+    (pdir / "Header").write_text("".join(out))
