@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="time budget of the CPU-baseline sample (boxes run until it is spent)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r01" / "pmc_forward_staged.json"),
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r01" / "pmc_forward_fused.json"),
                     help="PMC traffic summary (from profiles/collect_pmc.py) merged into roofline.traffic")
     return ap.parse_args()
 

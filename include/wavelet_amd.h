@@ -71,6 +71,7 @@ typedef struct wc_unit {
 typedef struct wc_ctx wc_ctx;
 
 /* Context lifetime.  `device` is a HIP device ordinal. */
+int wc_device_count(void);  /* HIP devices visible to this process (0 without a GPU) */
 int wc_ctx_create(int device, wc_ctx** out);
 void wc_ctx_destroy(wc_ctx* ctx);
 const char* wc_last_error(const wc_ctx* ctx);

@@ -158,3 +158,25 @@ def test_estimate_matches_oracle(run, compressed, oracle):
     lvl = base / "data" / "plt00010" / "Level_1"
     raw = sum(f.stat().st_size for f in lvl.iterdir()) / len(NAMES) * len(COMPS)
     assert size == pytest.approx(xz_bytes / raw * 100, rel=1e-12)
+
+
+def test_multi_device_workers_write_identical_files(run, compressed, tmp_path):
+    """WCAMD_DEVICES spreads chunks (and -d timesteps) over one host thread +
+    context per listed device; "0,0" runs that path on a one-GPU box."""
+    import filecmp
+    base, _ = run
+    out = base / "comp_md"
+    cli(f"datadir={base}/data/", "minfile=plt00010", "maxfile=plt00011", "minlevel=0", "maxlevel=1",
+        "components=temp pressure", f"keep={KEEP}", f"compresseddir={out}/", "-c",
+        env={"WCAMD_CHUNK_CELLS": "60000", "WCAMD_DEVICES": "0,0", "WCAMD_THREADS": "4"})
+    names = sorted(p.name for p in compressed.iterdir())
+    assert names == sorted(p.name for p in out.iterdir())
+    for n in names:
+        assert filecmp.cmp(compressed / n, out / n, shallow=False), n
+    r1, r2 = base / "regen_md1", base / "regen_md2"
+    cli(f"compresseddir={compressed}/", f"out={r1}/", "-d")
+    cli(f"compresseddir={out}/", f"out={r2}/", "-d", env={"WCAMD_DEVICES": "0,0"})
+    for root, _, files in os.walk(r1):
+        for f in files:
+            a = Path(root) / f
+            assert filecmp.cmp(a, r2 / a.relative_to(r1), shallow=False), a

@@ -1,0 +1,154 @@
+"""End-to-end timing of the wavelet-compression command line (-c, -d, -estimate)
+on a synthetic AMR run, with the reference-faithful CPU path timed beside it.
+
+Layout (scaled by --scale): level 0 = 64 boxes of 64^3,
+level 1 = 96 x 64^3, level 2 = 128 x 32^3, level 3 = 256 x 16^3 + 32 x (48x32x16),
+NCOMP components in the plotfile, all compressed, keep 0.999, fp64 FABs.
+Reported: wall seconds per mode, input GB/s of -c, units/s, and the CPU
+baseline = oracle transform/threshold/RLE/serialize + xz preset 6 (what the
+reference's compress() does per unit, single thread) on a sample of units.
+
+usage: python tools/bench_cli.py [--scale 1.0] [--ncomp 4] [--out profiles/r01/cli_e2e.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import lzma
+import os
+import random
+import shutil
+import string
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+CLI = ROOT / "wavelet-compression_amd" / "bin" / "wavelet-compression"
+
+
+def layout(scale: float):
+    def n(k):
+        return max(1, int(round(k * scale)))
+    return [
+        [(64, 64, 64)] * n(64),
+        [(64, 64, 64)] * n(96),
+        [(32, 32, 32)] * n(128),
+        [(16, 16, 16)] * n(256) + [(48, 32, 16)] * n(32),
+    ]
+
+
+def place(boxes):
+    """Non-overlapping lo corners on a simple x-major grid."""
+    out, x, y, z, row_h = [], 0, 0, 0, 0
+    for (W, H, D) in boxes:
+        out.append(((x, y, z), (W, H, D)))
+        x += W
+        row_h = max(row_h, H)
+        if x >= 1024:
+            x, y = 0, y + row_h
+            row_h = 0
+    return out
+
+
+def digit_free_dir() -> Path:
+    p = Path(tempfile.gettempdir()) / ("wcamd_e2e_" + "".join(random.choice(string.ascii_lowercase) for _ in range(8)))
+    p.mkdir()
+    return p
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--ncomp", type=int, default=4)
+    ap.add_argument("--keep", type=float, default=0.999)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--out", default=str(ROOT / "profiles" / "r01" / "cli_e2e.json"))
+    args = ap.parse_args()
+    from oracle import oracle as O
+    from wavelet_compression_amd import plotfile as pf
+
+    names = [f"var_{chr(97 + i)}" for i in range(args.ncomp)]
+    base = digit_free_dir()
+    try:
+        t0 = time.perf_counter()
+        levels = []
+        ncells = 0
+        for l, boxes in enumerate(layout(args.scale)):
+            fabs = []
+            for b, (lo, (W, H, D)) in enumerate(place(boxes)):
+                comps = [O.synth_box_f64(O.unit_seed(0, l, b, c), lo, W, H, D, sigma=0.05) + 100.0 * c
+                         for c in range(args.ncomp)]
+                fabs.append((lo, np.stack(comps)))
+                ncells += W * H * D * args.ncomp
+            levels.append(fabs)
+        pf.write_plotfile(base / "data" / "plt00100", names, 1.0, [0, 0, 0, 1, 1, 1], 2, (1024, 1024, 1024),
+                          [10, 20, 30, 40], levels)
+        t_gen = time.perf_counter() - t0
+        comp = " ".join(names)
+        common = [f"datadir={base}/data/", "minfile=plt00100", "maxfile=plt00100", "minlevel=0",
+                  f"maxlevel={len(levels) - 1}", f"components={comp}", f"keep={args.keep}"]
+
+        def run(argv):
+            t = time.perf_counter()
+            r = subprocess.run([str(CLI), *argv], capture_output=True, text=True, timeout=1800)
+            dt = time.perf_counter() - t
+            if r.returncode != 0 or "[error]" in r.stderr:
+                raise SystemExit(r.stdout + r.stderr)
+            return dt, r.stdout
+
+        t_c, _ = run(common + [f"compresseddir={base}/comp/", "-c"])
+        xz_bytes = sum(f.stat().st_size for f in (base / "comp").glob("*.xz"))
+        t_d, _ = run([f"compresseddir={base}/comp/", f"out={base}/regen/", "-d"])
+        t_e, est = run([*common[:3], "minlevel=0", "maxlevel=0", f"components={comp}", f"keep={args.keep}",
+                        f"compresseddir={base}/x/", "-estimate"])
+        nunits = sum(len(f) for f in levels) * args.ncomp
+
+        # CPU baseline: the reference's per-unit compress() work, single thread
+        keep = float(np.float32(args.keep))
+        done, cells, t_cpu = 0, 0, 0.0
+        order = [(l, b) for l, fabs in enumerate(levels) for b in range(len(fabs))]
+        random.Random(1).shuffle(order)
+        for (l, b) in order:
+            arr = levels[l][b][1]
+            for c in range(args.ncomp):
+                a32 = O.narrow(arr[c])
+                t = time.perf_counter()
+                p, _k = O.compress_payload(a32, keep)
+                lzma.compress(p, format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64, preset=6)
+                t_cpu += time.perf_counter() - t
+                done += 1
+                cells += a32.size
+            if t_cpu > args.cpu_seconds:
+                break
+        cpu_cells_s = cells / t_cpu
+        res = {
+            "workload": f"C3-like synthetic plotfile x{args.scale}: 4 levels, {args.ncomp} comps, {nunits} units, "
+                        f"{ncells} cells fp64 ({ncells * 8 / 1e9:.2f} GB), keep={args.keep}",
+            "compress_s": t_c, "decompress_s": t_d, "estimate_s": t_e,
+            "compress_input_GBps": ncells * 8 / t_c / 1e9,
+            "compress_cells_per_s": ncells / t_c,
+            "decompress_cells_per_s": ncells / t_d,
+            "xz_bytes": xz_bytes, "compressed_fraction": xz_bytes / (ncells * 8),
+            "host_threads": int(os.environ.get("WCAMD_THREADS", os.environ.get("OMP_NUM_THREADS", os.cpu_count()))),
+            "cpu_baseline": {"value": cpu_cells_s, "unit": "cells/s", "cores": 1, "kind": "port",
+                             "sample": f"{done} random units ({cells} cells): oracle transform+threshold+RLE+serialize "
+                                       f"+ xz preset 6 (Python lzma = liblzma), {t_cpu:.1f} s"},
+            "speedup_vs_cpu_compress": (ncells / t_c) / cpu_cells_s,
+            "generate_s": t_gen,
+            "estimate_output": [ln for ln in est.splitlines() if "Predicted" in ln],
+        }
+        Path(args.out).parent.mkdir(parents=True, exist_ok=True)
+        Path(args.out).write_text(json.dumps(res, indent=1) + "\n")
+        print(json.dumps(res))
+    finally:
+        shutil.rmtree(base, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -5,7 +5,7 @@
 // Box-Muller noise), then wc_forward runs `steps` times.  Prints one JSON line.
 //
 // usage: wc_bench [boxes=1024] [dim=64] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1]
-//                 [fused=0|1] [check=0|1]
+//                 [fused=1|0] [check=0|1]
 // check=1: also run the staged path once and compare every unit's payload
 // bytes with the fused path's ("paths_identical" in the JSON line).
 #include <hip/hip_runtime.h>
@@ -60,7 +60,7 @@ int main(int argc, char** argv) {
     const int steps = argc > 5 ? std::atoi(argv[5]) : 10;
     const int warmup = argc > 6 ? std::atoi(argv[6]) : 2;
     const bool inverse = argc > 7 ? std::atoi(argv[7]) != 0 : false;
-    const bool fused = argc > 8 ? std::atoi(argv[8]) != 0 : false;
+    const bool fused = argc > 8 ? std::atoi(argv[8]) != 0 : true;  // library default
     const bool check = argc > 9 ? std::atoi(argv[9]) != 0 : false;
 
     std::vector<wc_unit> units(boxes);

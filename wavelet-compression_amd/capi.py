@@ -27,7 +27,7 @@ EXPORTED = (
     "wc_payload_bound", "wc_cell_count", "wc_forward", "wc_forward_host", "wc_decompose",
     "wc_inverse", "wc_inverse_host", "wc_inverse_flat", "wc_rmse", "wc_version",
     "wc_profile_enable", "wc_profile_read", "wc_set_option", "wc_inverse_flat_host", "wc_rmse_host",
-    "wc_decompose_host",
+    "wc_decompose_host", "wc_device_count",
 )
 WC_OPT_FUSED = 1
 

@@ -21,6 +21,10 @@
 
 namespace wavelet_amd {
 
+static thread_local int t_device = -1;
+
+void set_thread_device(int device) { t_device = device; }
+
 wc_ctx* thread_ctx() {
     thread_local struct Holder {
         wc_ctx* c = nullptr;
@@ -30,7 +34,7 @@ wc_ctx* thread_ctx() {
     } h;
     if (!h.c) {
         const char* dev = std::getenv("WCAMD_DEVICE");
-        const int d = dev ? std::atoi(dev) : 0;
+        const int d = t_device >= 0 ? t_device : (dev ? std::atoi(dev) : 0);
         if (wc_ctx_create(d, &h.c) != WC_OK) fatal("wc_ctx_create failed: no usable HIP device");
     }
     return h.c;

@@ -9,9 +9,11 @@
 
 namespace wavelet_amd {
 
-// One codec context per host thread on device $WCAMD_DEVICE (default 0),
-// created on first use.  Exits like the reference's fatal paths if no GPU.
+// One codec context per host thread on device $WCAMD_DEVICE (default 0), or
+// the device set by set_thread_device() before first use; created on first
+// use.  Exits like the reference's fatal paths if no GPU.
 wc_ctx* thread_ctx();
+void set_thread_device(int device);
 
 // The reference logs with spdlog::error and calls exit(EXIT_FAILURE) on codec
 // and I/O failures (src/compressor.cpp:263-283, src/decompressor.cpp:170-231).

@@ -19,7 +19,9 @@
 #include <filesystem>
 #include <fstream>
 #include <future>
+#include <mutex>
 #include <numeric>
+#include <thread>
 
 #include "host_ctx.h"
 #include "log.h"
@@ -52,6 +54,48 @@ uint64_t chunk_cells() {
         if (n > 0) return (uint64_t)n;
     }
     return 1ull << 28;
+}
+
+// GPUs to spread a run over: $WCAMD_DEVICES = "all" or "0,2,5"; unset -> one
+// device ($WCAMD_DEVICE, default 0), as the reference runs on one process.
+std::vector<int> run_devices() {
+    std::vector<int> d;
+    const char* v = std::getenv("WCAMD_DEVICES");
+    if (!v || !*v) return {-1};  // -1: thread_ctx()'s default device
+    if (std::string(v) == "all") {
+        for (int i = 0; i < wc_device_count(); ++i) d.push_back(i);
+    } else {
+        std::string cur;
+        for (const char* p = v;; ++p) {
+            if (*p == ',' || *p == 0) {
+                if (!cur.empty()) d.push_back(std::atoi(cur.c_str()));
+                cur.clear();
+                if (*p == 0) break;
+            } else {
+                cur.push_back(*p);
+            }
+        }
+    }
+    if (d.empty()) fatal("WCAMD_DEVICES names no usable device");
+    return d;
+}
+
+// Run worker(device, threads_per_device) on one host thread per device.
+template <class F>
+void on_devices(const std::vector<int>& devs, F worker) {
+    const int tpd = std::max(1, host_threads() / (int)devs.size());
+    if (devs.size() == 1) {
+        if (devs[0] >= 0) set_thread_device(devs[0]);
+        worker(tpd);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int d : devs)
+        th.emplace_back([d, tpd, &worker]() {
+            set_thread_device(d);
+            worker(tpd);
+        });
+    for (auto& t : th) t.join();
 }
 
 // The run's layout without its cell data: plotfile headers + FAB index.
@@ -196,31 +240,43 @@ void inverse_batch(const std::vector<std::string>& payloads, const std::vector<w
 // paths, src/compressor.cpp:250-254).  `on_chunk` sees each chunk after its
 // forward pass (estimate mode keeps the cells for the RMSE).
 template <class OnChunk>
-void compress_run(const RunIndex& r, double keep, const std::filesystem::path& dir, OnChunk on_chunk) {
+void compress_run(const RunIndex& r, double keep, const std::filesystem::path& dir, OnChunk on_chunk,
+                  const std::vector<int>& devs) {
     const size_t nc = r.comp_idxs.size();
-    const int threads = host_threads();
     std::vector<Chunk> chunks = plan_chunks(r, nc, chunk_cells());
-    std::future<void> xz_done;  // xz of the previous chunk, overlapped with this one's read + GPU pass
-    std::shared_ptr<Packed> prev;
-    for (Chunk& c : chunks) {
-        load_chunk(r, c, threads);
-        auto p = std::make_shared<Packed>(forward_chunk(c, keep));
+    auto jobs_of = [&](const Chunk& c, const Packed& p) {
         std::vector<XzJob> jobs;
         for (size_t i = 0; i < c.boxes.size(); ++i)
             for (size_t k = 0; k < nc; ++k) {
                 const size_t u = i * nc + k;
                 const BoxRef& b = c.boxes[i];
-                jobs.push_back(XzJob{p->payload.data() + p->offsets[u], 20 + 8ull * p->kept[u],
+                jobs.push_back(XzJob{p.payload.data() + p.offsets[u], 20 + 8ull * p.kept[u],
                                      (dir / unit_name(b.t, b.lev, r.comp_idxs[k], b.box)).string()});
             }
+        return jobs;
+    };
+    std::atomic<size_t> next{0};
+    std::mutex cb;
+    on_devices(devs, [&](int threads) {
+        // per device: read + GPU pass of chunk i overlapped with the xz stage of chunk i-1
+        std::future<void> xz_done;
+        for (size_t i = next.fetch_add(1); i < chunks.size(); i = next.fetch_add(1)) {
+            Chunk& c = chunks[i];
+            load_chunk(r, c, threads);
+            auto p = std::make_shared<Packed>(forward_chunk(c, keep));
+            std::vector<XzJob> jobs = jobs_of(c, *p);
+            if (xz_done.valid()) xz_done.get();
+            xz_done = std::async(std::launch::async,
+                                 [jobs = std::move(jobs), p, threads]() { xz_write_files(jobs, threads); });
+            {
+                std::lock_guard<std::mutex> g(cb);
+                on_chunk(c);
+            }
+            c.cells.clear();
+            c.cells.shrink_to_fit();
+        }
         if (xz_done.valid()) xz_done.get();
-        prev = p;
-        xz_done = std::async(std::launch::async, [jobs = std::move(jobs), p, threads]() { xz_write_files(jobs, threads); });
-        on_chunk(c);
-        c.cells.clear();
-        c.cells.shrink_to_fit();
-    }
-    if (xz_done.valid()) xz_done.get();
+    });
 }
 
 }  // namespace
@@ -248,7 +304,7 @@ int compress(const Config& cfg) {
     write_amrexinfo(r.amrexinfo, cfg.compressed_dir, "amrexinfo.raw");
     log_info("Successfully processed data in " + fmt_double(since(t0)) + " seconds. Beginning compression...");
     const auto t1 = Clock::now();
-    compress_run(r, (double)cfg.keep, std::filesystem::path(cfg.compressed_dir), [](const Chunk&) {});
+    compress_run(r, (double)cfg.keep, std::filesystem::path(cfg.compressed_dir), [](const Chunk&) {}, run_devices());
     log_info("Compression completed in " + fmt_double(since(t1)) + " seconds.");
     return 0;
 }
@@ -269,58 +325,56 @@ int decompress(const Config& cfg) {
     const AMReXInfo info = read_amrex_info(cfg.compressed_dir, "amrexinfo.raw");
     const LocDimData locs = read_loc_dim_from_bin(cfg.compressed_dir, "locations.raw", counts, iterator, num_times, num_levels);
     const LocDimData dims = read_loc_dim_from_bin(cfg.compressed_dir, "dimensions.raw", counts, iterator, num_times, num_levels);
-    const int threads = host_threads();
-    double t_decode = 0;
-    // One timestep at a time: decode its files on the pool, one GPU inverse
-    // for all its units, then write its plotfile.
-    for (int t = 0; t < num_times; ++t) {
-        const auto ts = Clock::now();
-        std::vector<std::string> paths;
-        std::vector<wc_unit> units;
-        uint64_t cursor = 0;
-        for (int l = 0; l < num_levels; ++l)
-            for (int b = 0; b < counts[t][l]; ++b)
-                for (int comp : runinfo.comp_idxs) {
-                    paths.push_back(cfg.compressed_dir + unit_name(t, l, comp, b));  // string concatenation (src/modes.cpp:157)
-                    (void)comp;
-                }
-        std::vector<std::string> payloads = xz_read_files(paths, threads);
-        for (const std::string& p : payloads) {
-            if (p.size() < 20) fatal("Deserialization failed: payload shorter than its header");
-            int32_t h[3];
-            std::memcpy(h, p.data(), sizeof h);
-            wc_unit u{cursor, std::max(h[0], 0), std::max(h[1], 0), std::max(h[2], 0), 0};
-            cursor += (uint64_t)u.nx * u.ny * u.nz;
-            cursor = (cursor + 3) & ~uint64_t(3);
-            units.push_back(u);
-        }
-        std::vector<float> cells(std::max<uint64_t>(cursor, 1));
-        inverse_batch(payloads, units, cells.data());
-        payloads.clear();
-        std::vector<std::vector<std::vector<multiBox3D>>> regen(1);
-        regen[0].resize(num_levels);
-        size_t u = 0;
-        for (int l = 0; l < num_levels; ++l)
-            for (int b = 0; b < counts[t][l]; ++b) {
-                multiBox3D mb;
-                for (int c = 0; c < num_components; ++c, ++u) {
-                    Box3D box(units[u].nx, units[u].ny, units[u].nz);
-                    if (box.data_size()) std::memcpy(box.data(), cells.data() + units[u].cell_offset, 4 * box.data_size());
-                    mb.push_back(std::move(box));
-                }
-                regen[0][l].push_back(std::move(mb));
+    // One timestep at a time per device: decode its files on the pool, one GPU
+    // inverse for all its units, then write its plotfile.
+    std::atomic<int> next{0};
+    on_devices(run_devices(), [&](int threads) {
+        for (int t = next.fetch_add(1); t < num_times; t = next.fetch_add(1)) {
+            std::vector<std::string> paths;
+            std::vector<wc_unit> units;
+            uint64_t cursor = 0;
+            for (int l = 0; l < num_levels; ++l)
+                for (int b = 0; b < counts[t][l]; ++b)
+                    for (int comp : runinfo.comp_idxs)
+                        paths.push_back(cfg.compressed_dir + unit_name(t, l, comp, b));  // string concatenation (src/modes.cpp:157)
+            std::vector<std::string> payloads = xz_read_files(paths, threads);
+            for (const std::string& p : payloads) {
+                if (p.size() < 20) fatal("Deserialization failed: payload shorter than its header");
+                int32_t h[3];
+                std::memcpy(h, p.data(), sizeof h);
+                wc_unit u{cursor, std::max(h[0], 0), std::max(h[1], 0), std::max(h[2], 0), 0};
+                cursor += (uint64_t)u.nx * u.ny * u.nz;
+                cursor = (cursor + 3) & ~uint64_t(3);
+                units.push_back(u);
             }
-        t_decode += since(ts);
-        AMReXInfo one = info;
-        one.true_times = {info.true_times[t]};
-        one.geomcellinfo = {info.geomcellinfo[t]};
-        one.level_steps = {info.level_steps[t]};
-        write_plotfiles(std::move(regen), {locs[t]}, {dims[t]}, {runinfo.files[t]}, num_levels, num_components,
-                        runinfo.components, one, cfg.out_dir);
-    }
+            std::vector<float> cells(std::max<uint64_t>(cursor, 1));
+            inverse_batch(payloads, units, cells.data());
+            payloads.clear();
+            std::vector<std::vector<std::vector<multiBox3D>>> regen(1);
+            regen[0].resize(num_levels);
+            size_t u = 0;
+            for (int l = 0; l < num_levels; ++l)
+                for (int b = 0; b < counts[t][l]; ++b) {
+                    multiBox3D mb;
+                    for (int c = 0; c < num_components; ++c, ++u) {
+                        Box3D box(units[u].nx, units[u].ny, units[u].nz);
+                        if (box.data_size())
+                            std::memcpy(box.data(), cells.data() + units[u].cell_offset, 4 * box.data_size());
+                        mb.push_back(std::move(box));
+                    }
+                    regen[0][l].push_back(std::move(mb));
+                }
+            AMReXInfo one = info;
+            one.true_times = {info.true_times[t]};
+            one.geomcellinfo = {info.geomcellinfo[t]};
+            one.level_steps = {info.level_steps[t]};
+            write_plotfiles(std::move(regen), {locs[t]}, {dims[t]}, {runinfo.files[t]}, num_levels, num_components,
+                            runinfo.components, one, cfg.out_dir);
+        }
+    });
+    const double t_decode = since(t0);
     log_info("Decompression completed in " + fmt_double(t_decode) + " seconds.");
     log_info("Sucessfully wrote plotfiles.");
-    (void)t0;
     return 0;
 }
 
@@ -335,6 +389,7 @@ int estimate(Config& cfg) {
     // Keep each chunk's cells for the RMSE; min/max over the narrowed values.
     std::vector<Chunk> kept_chunks;
     std::vector<float> minv(nc, FLT_MAX), maxv(nc, FLT_MIN);  // src/preprocess.cpp:30-31 quirk
+    const std::vector<int> one_device = {run_devices()[0]};
     compress_run(r, (double)cfg.keep, scratch.path(), [&](Chunk& c) {
         for (size_t u = 0; u < c.units.size(); ++u) {
             const size_t k = u % nc;
@@ -352,11 +407,12 @@ int estimate(Config& cfg) {
         keep.ncells = c.ncells;
         keep.cells.swap(c.cells);
         kept_chunks.push_back(std::move(keep));
-    });
+    }, one_device);
     log_info("Compression complete.");
     // Decompress from the written files, then per-box RMSE on the GPU.
     std::vector<std::vector<double>> all_rmses(nc);
     const int threads = host_threads();
+    if (one_device[0] >= 0) set_thread_device(one_device[0]);
     for (Chunk& c : kept_chunks) {
         std::vector<std::string> paths;
         for (const BoxRef& b : c.boxes)

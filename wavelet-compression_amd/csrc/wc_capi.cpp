@@ -436,6 +436,11 @@ extern "C" {
 
 const char* wc_version(void) { return "wavelet_amd 0.2 (gfx950; fp-contract=off, no denormal flush)"; }
 
+int wc_device_count(void) {
+    int ndev = 0;
+    return hipGetDeviceCount(&ndev) == hipSuccess ? ndev : 0;
+}
+
 int wc_ctx_create(int device, wc_ctx** out) {
     if (!out) return WC_ERR_INVALID;
     *out = nullptr;
