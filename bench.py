@@ -39,8 +39,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="time budget of the CPU-baseline sample (boxes run until it is spent)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r01" / "pmc_forward_fused.json"),
-                    help="PMC traffic summary (from profiles/collect_pmc.py) merged into roofline.traffic")
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r01" / "pmc_forward.json"),
+                    help="PMC traffic summary (tools/pmc_summary.py) merged into roofline.traffic")
+    ap.add_argument("--pipe", action="store_true", help="run the pipelined single-launch forward (WC_OPT_PIPE)")
     return ap.parse_args()
 
 
@@ -80,6 +81,7 @@ def main():
     import wcamd
     capi = wcamd.capi
     ctx = capi.Context(local)
+    ctx.set_pipe(args.pipe)
     keep = float(np.float32(args.keep))  # Config::keep is a float (src/argparse.h:13)
     dims = [(args.dim,) * 3] * args.boxes
     units, n, extent = capi.make_units(dims)
@@ -138,12 +140,9 @@ def main():
         # algorithmic bytes each kernel owns of B = s_in*N + 8*N_kept + 20*N_units;
         # the fp32 coefficient staging between K1 and K2 is overhead, not algorithmic traffic.
         "transform": s_in * ncells,
-        "flat_count": 0,
-        "unit_scan": 0,
-        "unit_offsets": 20 * n,
-        "flat_emit": 8 * kept_step,
-        # the fused kernel owns the whole path: cells in, pairs + headers out
-        "fused": s_in * ncells + 8 * kept_step + 20 * n,
+        "flat_emit": 8 * kept_step + 20 * n,
+        # the pipelined kernel owns the whole path: cells in, pairs + headers out
+        "pipe": s_in * ncells + 8 * kept_step + 20 * n,
     }
     dom_ms = per_launch[dominant][0]
     achieved = alg_bytes_stage.get(dominant, 0) / (dom_ms * 1e-3) / 1e9

@@ -81,13 +81,32 @@ const char* wc_last_error(const wc_ctx* ctx);
 int wc_set_stream(wc_ctx* ctx, void* hip_stream);
 int wc_synchronize(wc_ctx* ctx);  /* also reports kernel-side errors of earlier async calls */
 
-/* Tuning switches.  WC_OPT_FUSED (default 1): 1 runs eligible units (even W
- * <= 64, even H, D % 8 == 0, D <= 64, W*H <= 4096 flat rows) through the
- * single-read fused forward kernel; 0 uses the staged path (transform -> HBM
- * scratch -> threshold/pack) for every unit.  Results are byte-identical
- * either way (DESIGN.md has the timings of both). */
-#define WC_OPT_FUSED 1
+/* Tuning switches.
+ * WC_OPT_PIPE (default 0): 0 runs wc_forward as two launches (transform ->
+ *   fp32 coefficient scratch in HBM -> one emit launch doing threshold,
+ *   decoupled look-back and ordered pack); 1 runs ONE persistent launch that
+ *   interleaves transform tiles (coefficients into a ring sized to stay in
+ *   the Infinity Cache) with emit tiles.  Results are byte-identical either
+ *   way (DESIGN.md has the timings of both).
+ * WC_OPT_PIPE_LAG: cells of transform work listed between a unit's last
+ *   transform tile and its first emit tile (0 = default, 4 Mi cells).
+ * WC_OPT_PIPE_RING: coefficient ring size in floats (0 = default: lag + 8 Mi
+ *   + 2 x the largest unit; never more than the batch needs). */
+#define WC_OPT_PIPE 1
+#define WC_OPT_PIPE_LAG 2
+#define WC_OPT_PIPE_RING 3
+#define WC_OPT_PIPE_CLAIM 4     /* work-list items claimed per ticket (default 1) */
+#define WC_OPT_PIPE_PREFETCH 5  /* 1: claim the next ticket while working (default 0) */
+#define WC_OPT_PIPE_WGS 6       /* workgroups per CU (0 = occupancy limit) */
+#define WC_OPT_PIPE_STATS 7     /* 1: collect wait-time counters (wc_pipe_stats) */
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
+
+/* Diagnostics of the pipelined kernel (WC_OPT_PIPE_STATS on): summed over
+ * workgroups since the last read, in 100 MHz ticks: [0] transform items,
+ * [1] of which ring waits, [2] emit items, [3] of which waits for the unit's
+ * transform tiles, [4] of which look-back, [5] ticket waits; [6] transform
+ * and [7] emit item counts.  Synchronizes the context stream. */
+int wc_pipe_stats(wc_ctx* ctx, uint64_t* out, int n);
 
 /* Host-side helpers (no device work). */
 uint64_t wc_payload_bound(const wc_unit* units, int n);  /* worst case: every coefficient kept */
@@ -138,14 +157,14 @@ int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* 
  * wc_profile_read() returns the summed milliseconds and launch counts since
  * the previous read, then resets. */
 #define WC_STAGE_TRANSFORM 0  /* K1  */
-#define WC_STAGE_COUNT 1      /* K2a */
-#define WC_STAGE_SCAN 2       /* K2b */
-#define WC_STAGE_OFFSETS 3    /* K2c */
-#define WC_STAGE_EMIT 4       /* K2d */
+#define WC_STAGE_COUNT 1      /* unused since the look-back emit (kept for numbering) */
+#define WC_STAGE_SCAN 2       /* unused */
+#define WC_STAGE_OFFSETS 3    /* unused */
+#define WC_STAGE_EMIT 4       /* K2  threshold + look-back + pack (k_emit_lb) */
 #define WC_STAGE_DECODE 5     /* K5a-c */
 #define WC_STAGE_INVERSE 6    /* K6  */
 #define WC_STAGE_RMSE 7       /* K7  */
-#define WC_STAGE_FUSED 8      /* fused single-read forward kernel */
+#define WC_STAGE_PIPE 8       /* pipelined forward kernel (whole wc_forward) */
 #define WC_NUM_STAGES 9
 int wc_profile_enable(wc_ctx* ctx, int on);
 int wc_profile_read(wc_ctx* ctx, double* total_ms, uint32_t* launches, int nstages);

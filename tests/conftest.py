@@ -7,6 +7,10 @@ import pytest
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
+# Registers the package under its importable name `wavelet_compression_amd`
+# (the directory name has a dash); loading it does not touch the GPU.
+import wcamd  # noqa: E402,F401
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")

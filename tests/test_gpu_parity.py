@@ -35,13 +35,13 @@ def pack(wc, boxes, dtype=np.float64, offsets=None):
     return units, n, extent, cells
 
 
-def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None, fused=True):
+def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None, pipe=True, lag=0, ring=0):
     units, n, extent, cells = pack(wc, boxes, dtype, offsets)
-    ctx.set_fused(fused)
+    ctx.set_pipe(pipe, lag=lag, ring=ring)
     try:
         payload, offs, kept = ctx.forward_host(cells, units, n, keep)
     finally:
-        ctx.set_fused(True)  # library default
+        ctx.set_pipe(False)  # library default
     return [wc.capi.unit_payload(payload, offs, kept, i) for i in range(n)], kept
 
 
@@ -50,36 +50,36 @@ def oracle_payload(O, b, keep):
     return O.compress_payload(b32, keep)[0]
 
 
-PATHS = [pytest.param(True, id="fused"), pytest.param(False, id="staged")]
+PATHS = [pytest.param(True, id="pipe"), pytest.param(False, id="staged")]
 
 
-@pytest.mark.parametrize("fused", PATHS)
+@pytest.mark.parametrize("pipe", PATHS)
 @pytest.mark.parametrize("keep", KEEPS)
-def test_forward_payload_bit_exact_fp64(wc, ctx, oracle, keep, fused):
+def test_forward_payload_bit_exact_fp64(wc, ctx, oracle, keep, pipe):
     boxes = synth(oracle, DIMS)
-    got, kept = gpu_payloads(wc, ctx, boxes, keep, fused=fused)
+    got, kept = gpu_payloads(wc, ctx, boxes, keep, pipe=pipe)
     for i, b in enumerate(boxes):
         want = oracle_payload(oracle, b, keep)
         assert got[i] == want, f"unit {i} dims {DIMS[i]} keep {keep}"
 
 
-@pytest.mark.parametrize("fused", PATHS)
-def test_forward_payload_bit_exact_fp32_input(wc, ctx, oracle, fused):
+@pytest.mark.parametrize("pipe", PATHS)
+def test_forward_payload_bit_exact_fp32_input(wc, ctx, oracle, pipe):
     keep = KEEPS[1]
     boxes = [oracle.narrow(b) for b in synth(oracle, DIMS, seed0=1)]
-    got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, fused=fused)
+    got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, pipe=pipe)
     for i, b in enumerate(boxes):
         assert got[i] == oracle.compress_payload(b, keep)[0], f"unit {i} dims {DIMS[i]}"
 
 
-@pytest.mark.parametrize("fused", PATHS)
-def test_unaligned_offsets(wc, ctx, oracle, fused):
+@pytest.mark.parametrize("pipe", PATHS)
+def test_unaligned_offsets(wc, ctx, oracle, pipe):
     """Odd cell offsets disable the vector loads; results must not change."""
     keep = KEEPS[1]
     dims = [(8, 8, 8), (6, 4, 2), (16, 2, 4), (4, 4, 16)]
     boxes = synth(oracle, dims, seed0=2)
     offs = [1, 1 + 512 + 3, 1 + 512 + 3 + 48 + 5, 1 + 512 + 3 + 48 + 5 + 128 + 7]
-    got, _ = gpu_payloads(wc, ctx, boxes, keep, offsets=offs, fused=fused)
+    got, _ = gpu_payloads(wc, ctx, boxes, keep, offsets=offs, pipe=pipe)
     for i, b in enumerate(boxes):
         assert got[i] == oracle_payload(oracle, b, keep)
 
@@ -148,7 +148,7 @@ def special_boxes():
     b = np.full((2, 4, 2), np.float32(1e-40), np.float32); b[1, 1, 1] = np.float32(3e-39)
     out["denormal"] = (b, None)
     out["const_3902"] = (np.full((64, 32, 16), np.float32(3902.4), np.float32), 4096)
-    # the same quirks on fused-eligible shapes (even W, H and D % 8 == 0)
+    # the same quirks on fast-transform shapes (even W, H and D % 8 == 0)
     b = np.full((8, 4, 4), 5.0, np.float32); b[5, 2, 3] = 7.5
     out["plus5_spike_f"] = (b, 23)
     out["minus5_sign_quirk_f"] = (np.full((8, 4, 4), -5.0, np.float32), 128)
@@ -168,12 +168,12 @@ def special_boxes():
     return out
 
 
-@pytest.mark.parametrize("fused", PATHS)
-def test_special_boxes(wc, ctx, oracle, fused):
+@pytest.mark.parametrize("pipe", PATHS)
+def test_special_boxes(wc, ctx, oracle, pipe):
     keep = KEEPS[1]
     sp = special_boxes()
     names = list(sp)
-    got, kept = gpu_payloads(wc, ctx, [sp[k][0] for k in names], keep, dtype=np.float32, fused=fused)
+    got, kept = gpu_payloads(wc, ctx, [sp[k][0] for k in names], keep, dtype=np.float32, pipe=pipe)
     for i, k in enumerate(names):
         b, expect_kept = sp[k]
         want, wk = oracle.compress_payload(b, keep)
@@ -281,30 +281,65 @@ def test_rle_decode_out_of_range_pairs_dropped(wc, ctx, oracle):
     assert out.tobytes() == want.tobytes()
 
 
-@pytest.mark.parametrize("fused", PATHS)
-def test_large_batch_64cubed_fp64(wc, ctx, oracle, fused):
+@pytest.mark.parametrize("pipe", PATHS)
+def test_large_batch_64cubed_fp64(wc, ctx, oracle, pipe):
     """64 boxes of the headline shape (64^3 fp64, keep 0.999f): every payload byte."""
     keep = KEEPS[1]
     dims = [(64, 64, 64)] * 64
     boxes = [oracle.synth_box_f64(oracle.unit_seed(0, 0, i, 0), (64 * (i % 8), 64 * (i // 8), 0), 64, 64, 64)
              for i in range(64)]
-    got, kept = gpu_payloads(wc, ctx, boxes, keep, fused=fused)
+    got, kept = gpu_payloads(wc, ctx, boxes, keep, pipe=pipe)
     frac = kept.sum() / (64 * 64 ** 3)
     assert 0.05 < frac < 0.95
     for i, b in enumerate(boxes):
         assert got[i] == oracle_payload(oracle, b, keep), i
 
 
-@pytest.mark.parametrize("fused", PATHS)
-def test_128cubed_fp32_and_mixed_sizes(wc, ctx, oracle, fused):
-    """C5 shape (128^3 fp32, keep 0.9999f: staged, W > 64) beside fused-eligible and
+@pytest.mark.parametrize("pipe", PATHS)
+def test_128cubed_fp32_and_mixed_sizes(wc, ctx, oracle, pipe):
+    """C5 shape (128^3 fp32, keep 0.9999f: z split over tiles) beside fast-transform and
     other AMR-style mixed boxes in one batch."""
     keep = KEEPS[2]
     dims = [(128, 128, 128), (32, 32, 32), (16, 16, 16), (48, 32, 16), (64, 64, 64), (128, 64, 32)]
     boxes = [oracle.narrow(b) for b in synth(oracle, dims, seed0=8)]
-    got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, fused=fused)
+    got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, pipe=pipe)
     for i, b in enumerate(boxes):
         assert got[i] == oracle.compress_payload(b, keep)[0], dims[i]
+
+
+@pytest.mark.parametrize("lag,ring", [(0, 4096), (1, 8192), (100_000, 40_000), (1, 300_000)])
+def test_pipe_ring_reuse_and_waits(wc, ctx, oracle, lag, ring):
+    """The pipelined kernel with a coefficient ring far smaller than the batch:
+    transform tiles wait for the emit tiles of the units whose ring chunks they
+    overwrite (wait lists), and emit tiles come right after (lag 1) or long
+    after their unit's transform tiles.  Mixed shapes, odd dims, an empty unit
+    and a unit larger than the requested ring (the ring grows to fit it)."""
+    keep = KEEPS[1]
+    dims = [(16, 16, 16), (32, 32, 32), (3, 5, 7), (64, 64, 64), (0, 4, 4), (48, 32, 16), (16, 16, 16),
+            (33, 17, 9), (64, 64, 64), (8, 4, 2), (32, 32, 32), (2, 200, 3)] * 3
+    boxes = synth(oracle, dims, seed0=11)
+    got, kept = gpu_payloads(wc, ctx, boxes, keep, pipe=True, lag=lag, ring=ring)
+    for i, b in enumerate(boxes):
+        assert got[i] == oracle_payload(oracle, b, keep), (i, dims[i])
+
+
+def test_pipe_stats_counters(wc, ctx, oracle):
+    """WC_OPT_PIPE_STATS: the diagnostics count every work-list item once."""
+    dims = [(64, 64, 64)] * 8 + [(16, 16, 16)] * 4
+    boxes = synth(oracle, dims, seed0=12)
+    units, n, extent, cells = pack(wc, boxes)
+    ctx.set_pipe(True)
+    ctx.set_option(wc.capi.WC_OPT_PIPE_STATS, 1)
+    try:
+        payload, offs, kept = ctx.forward_host(cells, units, n, KEEPS[1])
+        st = ctx.pipe_stats()
+    finally:
+        ctx.set_option(wc.capi.WC_OPT_PIPE_STATS, 0)
+        ctx.set_pipe(False)
+    assert st[6] == 8 * 32 + 4 * 1   # transform tiles: 64^3 -> 32 tiles of 64x2x64, 16^3 -> 1
+    assert st[7] == 8 * 32 + 4 * 1   # emit tiles of 8192 coefficients
+    for i, b in enumerate(boxes):
+        assert wc.capi.unit_payload(payload, offs, kept, i) == oracle_payload(oracle, b, KEEPS[1])
 
 
 def test_reference_wavelet_decomposition_case(wc):
@@ -333,8 +368,8 @@ def test_reference_calc_rmse_case(wc):
     assert wc.calc_rmse_per_box(a, p, 2) == [3.5, 3.5]
 
 
-@pytest.mark.parametrize("fused", PATHS)
-def test_gpu_matches_committed_golden_fixtures(wc, ctx, fused):
+@pytest.mark.parametrize("pipe", PATHS)
+def test_gpu_matches_committed_golden_fixtures(wc, ctx, pipe):
     """Stored vectors (tests/golden/codec_golden.npz): payload bytes and reconstructions."""
     import json
     from pathlib import Path
@@ -346,7 +381,7 @@ def test_gpu_matches_committed_golden_fixtures(wc, ctx, fused):
         by_keep.setdefault(case["keep"], []).append(case)
     for keep, cases in by_keep.items():
         boxes = [z[c["box"]] for c in cases]
-        got, kept = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, fused=fused)
+        got, kept = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, pipe=pipe)
         for i, c in enumerate(cases):
             assert got[i] == z[c["name"] + "/payload"].tobytes(), c["name"]
             assert int(kept[i]) == c["kept"], c["name"]

@@ -15,10 +15,8 @@ import json
 import re
 from collections import defaultdict
 
-STAGE_OF = [("k_forward_fused", "fused"), ("k_transform", "transform"), ("k_flat_count", "flat_count"), ("k_unit_scan", "unit_scan"),
-            ("k_unit_offsets", "unit_offsets"), ("k_flat_emit", "flat_emit"),
-            ("k_decode", "decode"), ("k_inverse", "inverse"), ("k_rmse", "rmse"),
-            ("k_fwd", "transform")]
+STAGE_OF = [("k_forward_pipe", "pipe"), ("k_transform", "transform"), ("k_emit_lb", "flat_emit"),
+            ("k_decode", "decode"), ("k_inverse", "inverse"), ("k_rmse", "rmse")]
 
 
 def stage(name):

@@ -10,7 +10,7 @@
 #         --write gpurun_out/prof_write/write_counter_collection.csv --out profiles/<round>/summary.json
 set -o pipefail
 W="${WCB_ARGS:-1024 64 f64 0.999}"
-F="${WCB_FUSED:-1}"   # 1: the default fused kernel, 0: the staged kernels
+F="${WCB_PIPE:-0}"    # 0: the default staged kernels, 1: the pipelined kernel
 exec tools/gpu_run.sh \
   "kt_bench:300:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_bench -o bench -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline" \
   "kt_wcb:200:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_wcb -o wcb -- tools/bin/wc_bench $W 10 2 0 $F" \

@@ -5,9 +5,10 @@
 // Box-Muller noise), then wc_forward runs `steps` times.  Prints one JSON line.
 //
 // usage: wc_bench [boxes=1024] [dim=64] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1]
-//                 [fused=1|0] [check=0|1]
+//                 [pipe=1|0] [check=0|1] [lag=0] [ring=0] [claim=1] [prefetch=0] [wgs=0] [stats=0]
 // check=1: also run the staged path once and compare every unit's payload
-// bytes with the fused path's ("paths_identical" in the JSON line).
+// bytes with the pipelined path's ("paths_identical" in the JSON line).
+// lag / ring: WC_OPT_PIPE_LAG / WC_OPT_PIPE_RING (0 = library defaults).
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -60,8 +61,14 @@ int main(int argc, char** argv) {
     const int steps = argc > 5 ? std::atoi(argv[5]) : 10;
     const int warmup = argc > 6 ? std::atoi(argv[6]) : 2;
     const bool inverse = argc > 7 ? std::atoi(argv[7]) != 0 : false;
-    const bool fused = argc > 8 ? std::atoi(argv[8]) != 0 : true;  // library default
+    const bool pipe = argc > 8 ? std::atoi(argv[8]) != 0 : true;  // library default
     const bool check = argc > 9 ? std::atoi(argv[9]) != 0 : false;
+    const long long lag = argc > 10 ? std::atoll(argv[10]) : 0;
+    const long long ring = argc > 11 ? std::atoll(argv[11]) : 0;
+    const int claim = argc > 12 ? std::atoi(argv[12]) : 1;
+    const int prefetch = argc > 13 ? std::atoi(argv[13]) : 0;
+    const int wgs = argc > 14 ? std::atoi(argv[14]) : 0;
+    const int stats = argc > 15 ? std::atoi(argv[15]) : 0;
 
     std::vector<wc_unit> units(boxes);
     const unsigned long long per = (unsigned long long)dim * dim * dim;
@@ -90,7 +97,12 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "wc_ctx_create failed\n");
         return 2;
     }
-    wc_set_option(ctx, WC_OPT_FUSED, fused ? 1 : 0);
+    wc_set_option(ctx, WC_OPT_PIPE, pipe ? 1 : 0);
+    wc_set_option(ctx, WC_OPT_PIPE_LAG, lag);
+    wc_set_option(ctx, WC_OPT_PIPE_RING, ring);
+    wc_set_option(ctx, WC_OPT_PIPE_CLAIM, claim);
+    wc_set_option(ctx, WC_OPT_PIPE_PREFETCH, prefetch);
+    wc_set_option(ctx, WC_OPT_PIPE_WGS, wgs);
     auto fwd = [&]() {
         int rc = wc_forward(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, keep, payload, cap, offsets, kept);
         if (rc != WC_OK) {
@@ -110,6 +122,7 @@ int main(int argc, char** argv) {
         if (inverse) inv();
     }
     wc_synchronize(ctx);
+    if (stats) wc_set_option(ctx, WC_OPT_PIPE_STATS, 1);
     wc_profile_enable(ctx, 1);
     double ms[WC_NUM_STAGES];
     uint32_t cnt[WC_NUM_STAGES];
@@ -130,20 +143,25 @@ int main(int argc, char** argv) {
         wc_profile_read(ctx, ims, icnt, WC_NUM_STAGES);
     }
     const double step_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() / steps;
+    uint64_t st[8] = {};
+    if (stats) {
+        wc_pipe_stats(ctx, st, 8);
+        wc_set_option(ctx, WC_OPT_PIPE_STATS, 0);
+    }
     int identical = -1;
     if (check) {
-        // Fused vs staged: every unit's serialized bytes must match.
+        // Pipelined vs staged: every unit's serialized bytes must match.
         std::vector<uint64_t> off_a(boxes + 1), off_b(boxes + 1);
         std::vector<uint32_t> k_a(boxes), k_b(boxes);
         std::vector<uint8_t> pa(cap), pb(cap);
-        wc_set_option(ctx, WC_OPT_FUSED, 1);
+        wc_set_option(ctx, WC_OPT_PIPE, 1);
         fwd();
         wc_synchronize(ctx);
         CK(hipMemcpy(off_a.data(), offsets, 8 * (boxes + 1), hipMemcpyDeviceToHost));
         CK(hipMemcpy(k_a.data(), kept, 4 * boxes, hipMemcpyDeviceToHost));
         CK(hipMemcpy(pa.data(), payload, cap, hipMemcpyDeviceToHost));
         CK(hipMemset(payload, 0xA5, cap));
-        wc_set_option(ctx, WC_OPT_FUSED, 0);
+        wc_set_option(ctx, WC_OPT_PIPE, 0);
         fwd();
         wc_synchronize(ctx);
         CK(hipMemcpy(off_b.data(), offsets, 8 * (boxes + 1), hipMemcpyDeviceToHost));
@@ -154,7 +172,7 @@ int main(int argc, char** argv) {
             if (k_a[i] != k_b[i] || off_a[i] != off_b[i]) identical = 0;
             else if (std::memcmp(pa.data() + off_a[i], pb.data() + off_b[i], 20 + 8ull * k_a[i]) != 0) identical = 0;
         }
-        wc_set_option(ctx, WC_OPT_FUSED, fused ? 1 : 0);
+        wc_set_option(ctx, WC_OPT_PIPE, pipe ? 1 : 0);
     }
     uint64_t total = 0;
     CK(hipMemcpy(&total, offsets + boxes, 8, hipMemcpyDeviceToHost));
@@ -163,12 +181,12 @@ int main(int argc, char** argv) {
     double ksum = 0;
     for (uint32_t k : hk) ksum += k;
     const char* names[WC_NUM_STAGES] = {"transform", "flat_count", "unit_scan", "unit_offsets",
-                                        "flat_emit", "decode", "inverse", "rmse", "fused"};
+                                        "flat_emit", "decode", "inverse", "rmse", "pipe"};
     std::printf("{\"boxes\": %d, \"dim\": %d, \"dtype\": \"%s\", \"keep\": %.17g, \"steps\": %d, "
                 "\"ms_per_step\": %.4f, \"cells_per_s\": %.6e, \"kept_fraction\": %.6f, \"payload_bytes\": %llu, "
-                "\"fused\": %d, \"paths_identical\": %d, \"stage_ms\": {",
+                "\"pipe\": %d, \"lag\": %lld, \"ring\": %lld, \"paths_identical\": %d, \"stage_ms\": {",
                 boxes, dim, f64 ? "f64" : "f32", keep, steps, step_ms, per * boxes / (step_ms * 1e-3),
-                ksum / (double)(per * boxes), (unsigned long long)total, fused ? 1 : 0, identical);
+                ksum / (double)(per * boxes), (unsigned long long)total, pipe ? 1 : 0, lag, ring, identical);
     bool first = true;
     for (int s = 0; s < WC_NUM_STAGES; ++s)
         if (cnt[s]) {
@@ -184,7 +202,16 @@ int main(int argc, char** argv) {
                 first = false;
             }
     }
-    std::printf("}}\n");
+    std::printf("}");
+    if (stats) {
+        // per item averages in microseconds (ticks are 10 ns)
+        const double nT = st[6] ? (double)st[6] : 1.0, nE = st[7] ? (double)st[7] : 1.0;
+        std::printf(", \"pipe_us\": {\"T\": %.2f, \"T_ringwait\": %.2f, \"E\": %.2f, \"E_tdwait\": %.2f, "
+                    "\"E_lookback\": %.2f, \"claim_per_batch\": %.2f, \"nT\": %.0f, \"nE\": %.0f}",
+                    st[0] / nT / 100.0, st[1] / nT / 100.0, st[2] / nE / 100.0, st[3] / nE / 100.0,
+                    st[4] / nE / 100.0, st[5] / ((nT + nE) / claim) / 100.0, nT / steps, nE / steps);
+    }
+    std::printf("}\n");
     wc_ctx_destroy(ctx);
     (void)hipFree(cells);
     (void)hipFree(payload);

@@ -27,13 +27,14 @@ EXPORTED = (
     "wc_payload_bound", "wc_cell_count", "wc_forward", "wc_forward_host", "wc_decompose",
     "wc_inverse", "wc_inverse_host", "wc_inverse_flat", "wc_rmse", "wc_version",
     "wc_profile_enable", "wc_profile_read", "wc_set_option", "wc_inverse_flat_host", "wc_rmse_host",
-    "wc_decompose_host", "wc_device_count",
+    "wc_decompose_host", "wc_device_count", "wc_pipe_stats",
 )
-WC_OPT_FUSED = 1
+WC_OPT_PIPE, WC_OPT_PIPE_LAG, WC_OPT_PIPE_RING = 1, 2, 3
+WC_OPT_PIPE_CLAIM, WC_OPT_PIPE_PREFETCH, WC_OPT_PIPE_WGS, WC_OPT_PIPE_STATS = 4, 5, 6, 7
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*), kernel names as rocprof shows them.
 STAGES = ("transform", "flat_count", "unit_scan", "unit_offsets", "flat_emit", "decode", "inverse", "rmse",
-          "fused")
+          "pipe")
 
 
 class WcUnit(ctypes.Structure):
@@ -86,6 +87,7 @@ def load_library() -> ctypes.CDLL:
         "wc_rmse_host": (i32, [vp, vp, i32, vp, up, i32, vp]),
         "wc_decompose_host": (i32, [vp, vp, i32, up, i32, vp]),
         "wc_profile_read": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32), i32]),
+        "wc_pipe_stats": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), i32]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -179,9 +181,18 @@ class Context:
     def set_option(self, option: int, value: int):
         self._check(self._L.wc_set_option(self._h, int(option), int(value)))
 
-    def set_fused(self, on: bool):
-        """Route eligible units through the fused single-read kernel (default on)."""
-        self.set_option(WC_OPT_FUSED, 1 if on else 0)
+    def set_pipe(self, on: bool, lag: int = 0, ring: int = 0):
+        """wc_forward as one pipelined launch or as the staged kernels (default);
+        lag / ring tune the pipeline (0 = library defaults)."""
+        self.set_option(WC_OPT_PIPE, 1 if on else 0)
+        self.set_option(WC_OPT_PIPE_LAG, lag)
+        self.set_option(WC_OPT_PIPE_RING, ring)
+
+    def pipe_stats(self) -> list:
+        """wc_pipe_stats: pipelined-kernel diagnostics since the last read (8 counters)."""
+        out = (ctypes.c_uint64 * 8)()
+        self._check(self._L.wc_pipe_stats(self._h, out, 8))
+        return list(out)
 
     def profile_enable(self, on: bool = True):
         self._check(self._L.wc_profile_enable(self._h, 1 if on else 0))

@@ -5,12 +5,14 @@
 // exists: every computing entry point launches HIP kernels and fails with
 // WC_ERR_HIP if the device or code object is absent.
 //
-// Forward path per batch (wc_forward):
-//   fused units  (even dims, D % 8 == 0, W <= 64, D <= 64, <= kMaxFusedTiles tiles)
-//       -> k_forward_fused: one read of the cells, pairs written in place
-//   staged units (everything else: odd dims, short z, huge boxes)
-//       -> k_transform{,_fast} -> flat coefficients in HBM scratch
-//       -> k_flat_count -> k_unit_scan -> k_unit_offsets -> k_flat_emit
+// Forward path per batch (wc_forward), every unit shape:
+//   WC_OPT_PIPE = 0 (default): staged kernels: k_transform{,_fast} -> flat
+//       coefficients in HBM scratch -> k_emit_lb (threshold + decoupled
+//       look-back + pack)
+//   WC_OPT_PIPE = 1: k_forward_pipe, one persistent launch: transform
+//       tiles -> coefficient ring (Infinity-Cache resident) -> emit tiles
+//       (threshold + decoupled look-back + pack), interleaved by a host-built
+//       work list (wc_pipe.hip); latency-bound today
 // Both write unit u's serialized bytes at its fixed slot offsets[u].
 #include "wavelet_amd.h"
 #include "wc_internal.h"
@@ -25,19 +27,12 @@
 namespace wc {
 size_t transform_lds_bytes(int lbx, int lby, int lbz);
 size_t transform_fast_lds_bytes(int lbx, int lby, int lbz);
-size_t fused_lds_bytes(int lbx, int lby, int lbz, uint32_t ntile);
+size_t pipe_lds_bytes(size_t tile_lds);
+uint32_t pipe_grid(int dtype, size_t lds, int max_per_cu);
 hipError_t launch_transform(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
                             float*, int, unsigned long long*);
 hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
                                  float*, int, unsigned long long*);
-hipError_t launch_flat_count(hipStream_t, const float*, const UnitDev*, const FTile*, uint32_t,
-                             const unsigned long long*, double, uint32_t*, uint32_t*);
-hipError_t launch_unit_scan(hipStream_t, const UnitDev*, int, const uint32_t*, const uint32_t*, uint32_t*,
-                            uint32_t*, uint32_t*);
-hipError_t launch_unit_offsets(hipStream_t, const UnitDev*, int, const uint32_t*, uint8_t*, uint64_t*);
-hipError_t launch_flat_emit(hipStream_t, const float*, const UnitDev*, const FTile*, uint32_t,
-                            const unsigned long long*, double, const uint32_t*, const uint32_t*,
-                            const uint64_t*, uint8_t*);
 hipError_t launch_pack(hipStream_t, const UnitDev*, int, const uint32_t*, const uint8_t*, uint64_t*, uint8_t*);
 hipError_t launch_decode(hipStream_t, const UnitDev*, int, const FTile*, uint32_t, const uint8_t*,
                          const uint64_t*, uint64_t*, uint64_t*, float*, uint32_t*);
@@ -45,7 +40,8 @@ hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const 
                           float*);
 hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDev*, int, const FTile*,
                        uint32_t, double*, double*);
-hipError_t launch_forward_fused(hipStream_t, int, size_t, const FusedParams&);
+hipError_t launch_forward_pipe(hipStream_t, int, size_t, uint32_t, const PipeParams&);
+hipError_t launch_emit_lb(hipStream_t, const PipeParams&, const float*, uint32_t);
 }  // namespace wc
 
 using namespace wc;
@@ -58,24 +54,26 @@ struct DevBuf {
 };
 
 // A batch plan: unit descriptors and tile lists, mirrored in HBM.
-//   xtiles = [generic staged | fast staged | fused]  (unit-major in each part;
-//            the inverse transform runs over all of them)
-//   ftiles = [staged units | fused units]            (flat tiles; the staged
-//            forward uses the first part, decode and RMSE use all)
+//   xtiles = [generic | fast]   transform tiles, unit-major in each part (the
+//                               staged kernels launch each part; the inverse
+//                               and the pipe's work list index all of them)
+//   ftiles                      kFlatTile flat tiles (staged forward, decode, RMSE)
+//   etiles, items, waits        the pipelined forward's emit tiles, work list
+//                               and ring wait lists (built when WC_OPT_PIPE)
 struct Plan {
     std::vector<wc_unit> key;
-    bool fused_enabled = true;
+    bool pipe = true;
+    int64_t lag = 0, ring_req = 0;
     std::vector<UnitDev> units;
     std::vector<XTile> xtiles;
-    std::vector<FTile> ftiles;
-    uint32_t ngen = 0, nfast = 0, nfused = 0;  // xtiles partition
-    uint32_t nft_staged = 0;
-    uint32_t nstaged_units = 0;  // units (including empty ones) the staged kernels finish
+    std::vector<FTile> ftiles, etiles;
+    std::vector<uint32_t> items, waits;
+    uint32_t ngen = 0, nfast = 0;
     uint64_t coef_extent = 0;  // floats of staged coefficient scratch
-    uint64_t ntab = 0;         // fused row-table granules
-    size_t lds_gen = 0, lds_fast = 0, lds_fused = 0, lds_inverse = 0;
-    size_t flags_bytes = 0;    // ticket + keyslot[nfused]
-    DevBuf d_units, d_xtiles, d_ftiles;
+    uint64_t ring_floats = 0;  // pipe coefficient ring
+    size_t lds_gen = 0, lds_fast = 0, lds_inverse = 0, lds_pipe = 0;
+    size_t state_bytes = 0;    // pipe per-call state: ticket | key[n] | tdone[n] | edone[n] | status[netiles]
+    DevBuf d_units, d_xtiles, d_ftiles, d_etiles, d_items, d_waits;
 };
 
 int ceil_log2(int64_t v) {
@@ -93,10 +91,16 @@ struct wc_ctx {
     std::string err;
     Plan plan;
     bool plan_valid = false;
-    bool opt_fused = true;   // WC_OPT_FUSED default (see include/wavelet_amd.h)
+    bool opt_pipe = false;   // WC_OPT_PIPE default (see include/wavelet_amd.h)
+    int64_t opt_lag = 0;     // WC_OPT_PIPE_LAG (0 = default)
+    int64_t opt_ring = 0;    // WC_OPT_PIPE_RING (0 = default)
+    uint32_t opt_claim = 1;  // WC_OPT_PIPE_CLAIM
+    bool opt_prefetch = false;  // WC_OPT_PIPE_PREFETCH
+    int opt_wgs = 0;         // WC_OPT_PIPE_WGS (0 = occupancy limit)
+    bool opt_stats = false;  // WC_OPT_PIPE_STATS
     bool err_check_pending = false;
     // scratch (grow-only)
-    DevBuf coef, keys, tcount, tlast, toff, tprev, tsum, tbase, part, errflag, flags, table;
+    DevBuf coef, tsum, tbase, part, errflag, ring, state, stats;
     // host-path staging
     DevBuf h_cells, h_payload, h_packed, h_offsets, h_poff, h_kept, h_out;
     // per-kernel event timing (wc_profile_enable / wc_profile_read)
@@ -206,22 +210,124 @@ void push_tiles(std::vector<XTile>& v, const UnitDev& d, uint32_t u) {
             for (int bx = 0; bx < d.nbx; bx += TX) v.push_back(XTile{u, (uint32_t)bx, (uint32_t)by, (uint32_t)bz});
 }
 
+constexpr int64_t kDefaultLag = int64_t(4) << 20;    // cells of transform work between a unit and its emit tiles
+constexpr int64_t kDefaultRingExtra = int64_t(8) << 20;  // ring floats beyond the lag (tiles in flight)
+
+uint64_t round_up(uint64_t v, uint64_t m) { return (v + m - 1) / m * m; }
+
+// Pipelined forward: emit tiles, coefficient ring with wait lists, work list.
+// Emit tiles (both forward paths): kEmitTile flat coefficients each, at
+// least one per unit (an empty unit's tile writes its header).
+void build_etiles(Plan& P, int n) {
+    P.etiles.clear();
+    for (int i = 0; i < n; ++i) {
+        UnitDev& d = P.units[i];
+        d.et_begin = (uint32_t)P.etiles.size();
+        d.net = (uint32_t)std::max<uint64_t>(1, (d.ncells + kEmitTile - 1) / kEmitTile);
+        for (uint32_t t = 0; t < d.net; ++t) P.etiles.push_back(FTile{(uint32_t)i, t});
+    }
+    P.state_bytes = round_up(16 + 16ull * n + 8ull * P.etiles.size(), 16);
+}
+
+void build_pipe(Plan& P, int n) {
+    P.items.clear();
+    P.waits.clear();
+    uint64_t maxa = kRingChunk, total = 0;
+    for (int i = 0; i < n; ++i) {
+        const UnitDev& d = P.units[i];
+        const uint64_t a = round_up(d.ncells, kRingChunk);
+        maxa = std::max(maxa, a);
+        total += a;
+    }
+    const int64_t lag = P.lag > 0 ? P.lag : kDefaultLag;
+    uint64_t R = P.ring_req > 0 ? round_up((uint64_t)P.ring_req, kRingChunk)
+                                : round_up((uint64_t)lag + kDefaultRingExtra + 2 * maxa, kRingChunk);
+    R = std::max(R, 2 * maxa);
+    R = std::min(R, std::max<uint64_t>(total, kRingChunk));  // no reuse needed: no waits
+    R = std::max(R, maxa);
+    P.ring_floats = R;
+    // Ring regions, chunk aligned; a chunk has one writer per lap, so each
+    // unit waits for the last writers of its chunks (earlier laps follow by
+    // transitivity: that writer's transform waited for them).
+    std::vector<int32_t> last(R / kRingChunk, -1);
+    uint64_t cur = 0;
+    for (int i = 0; i < n; ++i) {
+        UnitDev& d = P.units[i];
+        d.wl_off = (uint32_t)P.waits.size();
+        d.wl_len = 0;
+        d.ring_off = 0;
+        if (d.ncells == 0) continue;
+        const uint64_t a = round_up(d.ncells, kRingChunk);
+        if (cur + a > R) cur = 0;
+        d.ring_off = cur;
+        std::vector<uint32_t> w;
+        for (uint64_t ch = cur / kRingChunk; ch < (cur + a) / kRingChunk; ++ch) {
+            if (last[ch] >= 0 && last[ch] != i) w.push_back((uint32_t)last[ch]);
+            last[ch] = i;
+        }
+        std::sort(w.begin(), w.end());
+        w.erase(std::unique(w.begin(), w.end()), w.end());
+        P.waits.insert(P.waits.end(), w.begin(), w.end());
+        d.wl_len = (uint32_t)w.size();
+        cur += a;
+    }
+    // Work list: transform tiles in unit order; a unit's emit tiles once
+    // `lag` more cells of transform work have been listed after its last
+    // transform tile; all emit tiles of the units a transform waits for come
+    // before it.  Every wait is therefore on an earlier item.
+    std::vector<int64_t> tend(n);
+    const uint32_t NE = (uint32_t)P.etiles.size();
+    uint32_t ep = 0;
+    int64_t tc = 0;
+    auto emit_until = [&](uint32_t target) {
+        for (; ep < target; ++ep) P.items.push_back(0x80000000u | ep);
+    };
+    auto emit_eligible = [&](int upto_unit) {
+        while (ep < NE) {
+            const uint32_t v = P.etiles[ep].unit;
+            if ((int)v > upto_unit || tend[v] + lag > tc) break;
+            P.items.push_back(0x80000000u | ep++);
+        }
+    };
+    for (int u = 0; u < n; ++u) {
+        const UnitDev& d = P.units[u];
+        for (uint32_t k = 0; k < d.wl_len; ++k) {
+            const UnitDev& v = P.units[P.waits[d.wl_off + k]];
+            emit_until(std::max(ep, v.et_begin + v.net));
+        }
+        const int64_t tcells = (int64_t)8 << (d.lbx + d.lby + d.lbz);
+        for (uint32_t g = 0; g < d.ntx; ++g) {
+            P.items.push_back(d.xt_begin + g);
+            tc += tcells;
+            if (g + 1 == d.ntx) tend[u] = tc;
+            emit_eligible(u - 1);
+        }
+        if (d.ntx == 0) tend[u] = tc;
+        emit_eligible(u);
+    }
+    emit_until(NE);
+}
+
 // Build (or reuse) the plan for this batch and upload it.
 int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     Plan& P = c->plan;
-    if (c->plan_valid && P.fused_enabled == c->opt_fused && (int)P.key.size() == n &&
-        (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0))
+    if (c->plan_valid && P.pipe == c->opt_pipe && P.lag == c->opt_lag && P.ring_req == c->opt_ring &&
+        (int)P.key.size() == n && (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0))
         return WC_OK;
     c->plan_valid = false;
     P.key.assign(units, units + n);
-    P.fused_enabled = c->opt_fused;
+    P.pipe = c->opt_pipe;
+    P.items.clear();
+    P.waits.clear();
+    P.lag = c->opt_lag;
+    P.ring_req = c->opt_ring;
     P.units.assign(n, UnitDev{});
     P.xtiles.clear();
     P.ftiles.clear();
-    P.ngen = P.nfast = P.nfused = P.nft_staged = P.nstaged_units = 0;
-    P.lds_gen = P.lds_fast = P.lds_fused = P.lds_inverse = 0;
-    std::vector<XTile> gen, fast, fused;
-    uint64_t coef_cursor = 0, pay_cursor = 4, tab_cursor = 0;
+    P.ngen = P.nfast = 0;
+    P.lds_gen = P.lds_fast = P.lds_inverse = P.lds_pipe = 0;
+    std::vector<XTile> gen, fast;
+    uint64_t coef_cursor = 0, pay_cursor = 4;
     for (int i = 0; i < n; ++i) {
         const wc_unit& u = units[i];
         UnitDev& d = P.units[i];
@@ -240,65 +346,46 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         d.ntz = (d.nbz + (1 << d.lbz) - 1) >> d.lbz;
         d.pay_off = pay_cursor;  // slot of 20 + 8*ncells bytes + 4 pad: next slot stays == 4 (mod 8)
         pay_cursor += 24 + 8 * d.ncells;
-        if (d.ncells == 0) {
-            ++P.nstaged_units;  // header-only payload, written by k_unit_offsets
-            continue;
-        }
-        const bool fast_ok = (u.nx % 2 == 0) && (u.ny % 2 == 0) && (u.nz % 8 == 0);
-        const uint64_t ntile = (uint64_t)((d.nbx + (1 << d.lbx) - 1) >> d.lbx) *
-                               ((d.nby + (1 << d.lby) - 1) >> d.lby) * d.ntz;
-        // fused: tiles span the whole x and z extent (one tile row per y block
-        // range), G <= kMaxFusedTiles, the row table fits kMaxFusedRows.
-        const uint64_t nrows_tile = (uint64_t)4 << (d.lbx + d.lby);
-        const bool fused_ok = fast_ok && (u.cell_offset % 2 == 0) && d.nbx <= (1 << d.lbx) && d.ntz == 1 &&
-                              ntile <= kMaxFusedTiles &&
-                              ntile * nrows_tile <= kMaxFusedRows;
-        if (fused_ok && c->opt_fused) {
-            d.fused = 1;
-            d.xt_begin = (uint32_t)fused.size();
-            d.ntile_u = (uint32_t)ntile;
-            d.tab_off = tab_cursor;
-            tab_cursor += ntile * nrows_tile / 4;
-            push_tiles(fused, d, (uint32_t)i);
-            P.lds_fused = std::max(P.lds_fused, fused_lds_bytes(d.lbx, d.lby, d.lbz, (uint32_t)ntile));
-        } else {
-            ++P.nstaged_units;
-            d.coef_off = (coef_cursor + 3) & ~uint64_t(3);
-            coef_cursor = d.coef_off + d.ncells;
-            if (fast_ok) {
-                push_tiles(fast, d, (uint32_t)i);
-                P.lds_fast = std::max(P.lds_fast, transform_fast_lds_bytes(d.lbx, d.lby, d.lbz));
-            } else {
-                push_tiles(gen, d, (uint32_t)i);
-                P.lds_gen = std::max(P.lds_gen, transform_lds_bytes(d.lbx, d.lby, d.lbz));
-            }
-        }
+        d.coef_off = (coef_cursor + 3) & ~uint64_t(3);
+        coef_cursor = d.coef_off + d.ncells;
+        if (d.ncells == 0) continue;
+        d.fast = (u.nx % 2 == 0) && (u.ny % 2 == 0) && (u.nz % 8 == 0);
+        std::vector<XTile>& dst = d.fast ? fast : gen;
+        const size_t before = dst.size();
+        push_tiles(dst, d, (uint32_t)i);
+        d.ntx = (uint32_t)(dst.size() - before);
+        d.xt_begin = (uint32_t)before;  // rebased below for fast units
+        if (d.fast)
+            P.lds_fast = std::max(P.lds_fast, transform_fast_lds_bytes(d.lbx, d.lby, d.lbz));
+        else
+            P.lds_gen = std::max(P.lds_gen, transform_lds_bytes(d.lbx, d.lby, d.lbz));
         P.lds_inverse = std::max(P.lds_inverse, transform_lds_bytes(d.lbx, d.lby, d.lbz));
-    }
-    // flat tiles: staged units first, then fused units
-    for (int pass = 0; pass < 2; ++pass) {
-        for (int i = 0; i < n; ++i) {
-            UnitDev& d = P.units[i];
-            if ((pass == 0) == (d.fused != 0)) continue;
-            d.ftile_begin = (uint32_t)P.ftiles.size();
-            d.nftiles = (uint32_t)((d.ncells + kFlatTile - 1) / kFlatTile);
-            for (uint32_t t = 0; t < d.nftiles; ++t) P.ftiles.push_back(FTile{(uint32_t)i, t});
-        }
-        if (pass == 0) P.nft_staged = (uint32_t)P.ftiles.size();
     }
     P.ngen = (uint32_t)gen.size();
     P.nfast = (uint32_t)fast.size();
-    P.nfused = (uint32_t)fused.size();
+    for (UnitDev& d : P.units)
+        if (d.fast) d.xt_begin += P.ngen;
     P.xtiles = std::move(gen);
     P.xtiles.insert(P.xtiles.end(), fast.begin(), fast.end());
-    P.xtiles.insert(P.xtiles.end(), fused.begin(), fused.end());
+    for (int i = 0; i < n; ++i) {
+        UnitDev& d = P.units[i];
+        d.ftile_begin = (uint32_t)P.ftiles.size();
+        d.nftiles = (uint32_t)((d.ncells + kFlatTile - 1) / kFlatTile);
+        for (uint32_t t = 0; t < d.nftiles; ++t) P.ftiles.push_back(FTile{(uint32_t)i, t});
+    }
     P.coef_extent = coef_cursor ? coef_cursor + kFlatTile : 0;  // slack: flat tiles read whole float4 groups
-    P.ntab = tab_cursor;
-    P.flags_bytes = 16 + 8 * (size_t)P.nfused;
+    build_etiles(P, n);
+    if (P.pipe) {
+        build_pipe(P, n);
+        P.lds_pipe = pipe_lds_bytes(std::max(P.lds_gen, P.lds_fast));
+    }
     int rc;
     if ((rc = upload(c, P.d_units, P.units.data(), sizeof(UnitDev) * P.units.size(), "upload units")) ||
         (rc = upload(c, P.d_xtiles, P.xtiles.data(), sizeof(XTile) * P.xtiles.size(), "upload xtiles")) ||
-        (rc = upload(c, P.d_ftiles, P.ftiles.data(), sizeof(FTile) * P.ftiles.size(), "upload ftiles")))
+        (rc = upload(c, P.d_ftiles, P.ftiles.data(), sizeof(FTile) * P.ftiles.size(), "upload ftiles")) ||
+        (rc = upload(c, P.d_etiles, P.etiles.data(), sizeof(FTile) * P.etiles.size(), "upload etiles")) ||
+        (rc = upload(c, P.d_items, P.items.data(), sizeof(uint32_t) * P.items.size(), "upload items")) ||
+        (rc = upload(c, P.d_waits, P.waits.data(), sizeof(uint32_t) * P.waits.size(), "upload waits")))
         return rc;
     // The host vectors back the async copies: finish them before returning.
     hipError_t e = hipStreamSynchronize(c->stream);
@@ -307,17 +394,25 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     return WC_OK;
 }
 
+// Scratch of the staged forward, the inverse and the RMSE (grow-only).
 int ensure_scratch(wc_ctx* c) {
     const Plan& P = c->plan;
-    const size_t n = P.units.size(), nft = P.ftiles.size();
+    const size_t nft = P.ftiles.size();
     int rc;
     if ((rc = ensure(c, c->coef, sizeof(float) * std::max<uint64_t>(P.coef_extent, 1))) ||
-        (rc = ensure(c, c->keys, sizeof(unsigned long long) * n)) ||
-        (rc = ensure(c, c->tcount, sizeof(uint32_t) * nft)) || (rc = ensure(c, c->tlast, sizeof(uint32_t) * nft)) ||
-        (rc = ensure(c, c->toff, sizeof(uint32_t) * nft)) || (rc = ensure(c, c->tprev, sizeof(uint32_t) * nft)) ||
         (rc = ensure(c, c->tsum, sizeof(uint64_t) * nft)) || (rc = ensure(c, c->tbase, sizeof(uint64_t) * nft)) ||
         (rc = ensure(c, c->part, sizeof(double) * nft)) || (rc = ensure(c, c->errflag, 16)) ||
-        (rc = ensure(c, c->flags, P.flags_bytes)) || (rc = ensure(c, c->table, 8 * P.ntab)))
+        (rc = ensure(c, c->state, P.state_bytes)))
+        return rc;
+    return WC_OK;
+}
+
+// Scratch of the pipelined forward.
+int ensure_pipe_scratch(wc_ctx* c) {
+    const Plan& P = c->plan;
+    int rc;
+    if ((rc = ensure(c, c->ring, sizeof(float) * P.ring_floats)) || (rc = ensure(c, c->state, P.state_bytes)) ||
+        (rc = ensure(c, c->errflag, 16)))
         return rc;
     return WC_OK;
 }
@@ -327,7 +422,7 @@ int set_device(wc_ctx* c) {
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "hipSetDevice");
 }
 
-// Surface an error bit a kernel raised (fused hand-off timeout) at the next
+// Surface an error bit a kernel raised (pipe dependency timeout) at the next
 // synchronisation point.
 int check_kernel_errors(wc_ctx* c) {
     if (!c->err_check_pending) return WC_OK;
@@ -336,78 +431,90 @@ int check_kernel_errors(wc_ctx* c) {
     hipError_t e = hipMemcpyAsync(&flag, c->errflag.p, 4, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "error flag readback");
-    if (flag & kErrTimeout) return fail(c, WC_ERR_HIP, "fused forward: hand-off wait timed out");
+    if (flag & kErrTimeout) return fail(c, WC_ERR_HIP, "pipelined forward: a dependency wait timed out");
     return WC_OK;
 }
 
-int forward_impl(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
+// Parameter block shared by k_forward_pipe and k_emit_lb; the per-call state
+// block [ticket | key[n] | tdone[n] | edone[n] | status[netiles]] is zeroed
+// by one memset.
+PipeParams pipe_params(wc_ctx* c, const void* d_cells, int n, double keep, uint8_t* d_payload,
+                       uint64_t* d_offsets, uint32_t* d_kept) {
+    Plan& P = c->plan;
+    uint8_t* st = (uint8_t*)c->state.p;
+    PipeParams p{};
+    p.cells = d_cells;
+    p.units = (const UnitDev*)P.d_units.p;
+    p.xtiles = (const XTile*)P.d_xtiles.p;
+    p.etiles = (const FTile*)P.d_etiles.p;
+    p.items = (const uint32_t*)P.d_items.p;
+    p.waits = (const uint32_t*)P.d_waits.p;
+    p.ring = (float*)c->ring.p;
+    p.ring_bytes = (uint32_t)(sizeof(float) * P.ring_floats);
+    p.nitems = (uint32_t)P.items.size();
+    p.n = n;
+    p.ticket = (uint32_t*)st;
+    p.key = (unsigned long long*)(st + 16);
+    p.tdone = (uint32_t*)(st + 16 + 8ull * n);
+    p.edone = (uint32_t*)(st + 16 + 12ull * n);
+    p.status = (unsigned long long*)(st + 16 + 16ull * n);
+    p.payload = d_payload;
+    p.offsets = d_offsets;
+    p.kept = d_kept;
+    p.err = (uint32_t*)c->errflag.p;
+    p.keep = keep;
+    p.claim = 1;
+    return p;
+}
+
+int forward_pipe(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
                  uint64_t* d_offsets, uint32_t* d_kept) {
+    Plan& P = c->plan;
+    hipError_t e;
+    if ((e = hipMemsetAsync(c->state.p, 0, P.state_bytes, c->stream)) != hipSuccess ||
+        (e = hipMemsetAsync(c->errflag.p, 0, 4, c->stream)) != hipSuccess)
+        return hip_fail(c, e, "memset pipe state");
+    PipeParams p = pipe_params(c, d_cells, n, keep, d_payload, d_offsets, d_kept);
+    p.claim = c->opt_claim;
+    p.prefetch = c->opt_prefetch ? 1u : 0u;
+    p.stats = nullptr;
+    if (c->opt_stats) {
+        int rc = ensure(c, c->stats, sizeof(unsigned long long) * kPipeStats);
+        if (rc) return rc;
+        p.stats = (unsigned long long*)c->stats.p;
+    }
+    const uint32_t nbatch = (p.nitems + p.claim - 1) / p.claim;
+    const uint32_t grid = std::min<uint32_t>(pipe_grid(dtype, P.lds_pipe, c->opt_wgs), nbatch);
+    {
+        StageTimer t(c, WC_STAGE_PIPE);
+        e = launch_forward_pipe(c->stream, dtype, P.lds_pipe, grid, p);
+    }
+    if (e != hipSuccess) return hip_fail(c, e, "pipe launch");
+    c->err_check_pending = true;
+    return WC_OK;
+}
+
+int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
+                   uint64_t* d_offsets, uint32_t* d_kept) {
     Plan& P = c->plan;
     const UnitDev* du = (const UnitDev*)P.d_units.p;
     const XTile* dxt = (const XTile*)P.d_xtiles.p;
-    const FTile* dft = (const FTile*)P.d_ftiles.p;
     hipError_t e = hipSuccess;
-    if (P.nfused) {
-        uint8_t* fl = (uint8_t*)c->flags.p;
-        if ((e = hipMemsetAsync(fl, 0, P.flags_bytes, c->stream)) != hipSuccess ||
-            (e = hipMemsetAsync(c->table.p, 0, 8 * P.ntab, c->stream)) != hipSuccess ||
-            (e = hipMemsetAsync(c->errflag.p, 0, 4, c->stream)) != hipSuccess)
-            return hip_fail(c, e, "memset fused flags");
-        FusedParams fp{};
-        fp.cells = d_cells;
-        fp.units = du;
-        fp.tiles = dxt + P.ngen + P.nfast;
-        fp.ntiles = P.nfused;
-        fp.n = n;
-        fp.ticket = (uint32_t*)fl;
-        fp.keyslot = (unsigned long long*)(fl + 16);
-        fp.table = (unsigned long long*)c->table.p;
-        fp.payload = d_payload;
-        fp.offsets = d_offsets;
-        fp.kept = d_kept;
-        fp.err = (uint32_t*)c->errflag.p;
-        fp.keep = keep;
-        {
-            StageTimer t(c, WC_STAGE_FUSED);
-            e = launch_forward_fused(c->stream, dtype, P.lds_fused, fp);
-        }
-        if (e != hipSuccess) return hip_fail(c, e, "fused launch");
-        c->err_check_pending = true;
-    }
-    if (P.nstaged_units == 0) return WC_OK;  // every unit was fused
-    if ((e = hipMemsetAsync(c->keys.p, 0, sizeof(unsigned long long) * n, c->stream)) != hipSuccess)
-        return hip_fail(c, e, "memset keys");
-    unsigned long long* keys = (unsigned long long*)c->keys.p;
+    if ((e = hipMemsetAsync(c->state.p, 0, P.state_bytes, c->stream)) != hipSuccess)
+        return hip_fail(c, e, "memset state");
+    PipeParams p = pipe_params(c, d_cells, n, keep, d_payload, d_offsets, d_kept);
     float* coef = (float*)c->coef.p;
     {
         StageTimer t(c, WC_STAGE_TRANSFORM);
-        e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, coef, 0, keys);
+        e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, coef, 0, p.key);
         if (e == hipSuccess)
             e = launch_transform_fast(c->stream, d_cells, dtype, du, dxt + P.ngen, P.nfast, P.lds_fast, coef, 0,
-                                      keys);
+                                      p.key);
     }
     if (e != hipSuccess) return hip_fail(c, e, "transform launch");
     {
-        StageTimer t(c, WC_STAGE_COUNT);
-        e = launch_flat_count(c->stream, coef, du, dft, P.nft_staged, keys, keep, (uint32_t*)c->tcount.p,
-                              (uint32_t*)c->tlast.p);
-    }
-    if (e != hipSuccess) return hip_fail(c, e, "count launch");
-    {
-        StageTimer t(c, WC_STAGE_SCAN);
-        e = launch_unit_scan(c->stream, du, n, (const uint32_t*)c->tcount.p, (const uint32_t*)c->tlast.p,
-                             (uint32_t*)c->toff.p, (uint32_t*)c->tprev.p, d_kept);
-    }
-    if (e != hipSuccess) return hip_fail(c, e, "scan launch");
-    {
-        StageTimer t(c, WC_STAGE_OFFSETS);
-        e = launch_unit_offsets(c->stream, du, n, d_kept, d_payload, d_offsets);
-    }
-    if (e != hipSuccess) return hip_fail(c, e, "offsets launch");
-    {
         StageTimer t(c, WC_STAGE_EMIT);
-        e = launch_flat_emit(c->stream, coef, du, dft, P.nft_staged, keys, keep, (const uint32_t*)c->toff.p,
-                             (const uint32_t*)c->tprev.p, d_offsets, d_payload);
+        e = launch_emit_lb(c->stream, p, coef, (uint32_t)P.etiles.size());
     }
     if (e != hipSuccess) return hip_fail(c, e, "emit launch");
     return WC_OK;
@@ -420,15 +527,9 @@ uint64_t cells_extent(const wc_unit* units, int n) {
     return ext;
 }
 
-// Plan with the fused path switched off (transform-only and inverse calls
-// need flat coefficient scratch for every unit).
-int get_plan_staged(wc_ctx* c, const wc_unit* units, int n) {
-    const bool saved = c->opt_fused;
-    c->opt_fused = false;
-    int rc = get_plan(c, units, n);
-    c->opt_fused = saved;
-    return rc;
-}
+// Transform-only, inverse and RMSE calls use the plan's tiles and flat
+// scratch, which every plan has (the pipe's work list is only extra).
+int get_plan_staged(wc_ctx* c, const wc_unit* units, int n) { return get_plan(c, units, n); }
 
 }  // namespace
 
@@ -466,11 +567,11 @@ void wc_ctx_destroy(wc_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->coef,      &c->keys,      &c->tcount,    &c->tlast,      &c->toff,
-                      &c->tprev,     &c->tsum,      &c->tbase,     &c->part,       &c->errflag,
-                      &c->flags,     &c->table,     &c->h_cells,    &c->h_payload,
+    DevBuf* bufs[] = {&c->coef,      &c->tsum,      &c->tbase,     &c->part,       &c->errflag,
+                      &c->ring,      &c->state,     &c->stats,      &c->h_cells,    &c->h_payload,
                       &c->h_packed,  &c->h_offsets, &c->h_poff,    &c->h_kept,     &c->h_out,
-                      &c->plan.d_units, &c->plan.d_xtiles, &c->plan.d_ftiles};
+                      &c->plan.d_units, &c->plan.d_xtiles, &c->plan.d_ftiles, &c->plan.d_etiles,
+                      &c->plan.d_items, &c->plan.d_waits};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& m : c->marks) {
@@ -493,8 +594,36 @@ int wc_set_stream(wc_ctx* c, void* s) {
 int wc_set_option(wc_ctx* c, int option, int64_t value) {
     if (!c) return WC_ERR_INVALID;
     switch (option) {
-        case WC_OPT_FUSED:
-            c->opt_fused = value != 0;
+        case WC_OPT_PIPE:
+            c->opt_pipe = value != 0;
+            return WC_OK;
+        case WC_OPT_PIPE_LAG:
+            if (value < 0) return fail(c, WC_ERR_INVALID, "lag < 0");
+            c->opt_lag = value;
+            return WC_OK;
+        case WC_OPT_PIPE_RING:
+            if (value < 0 || value > (int64_t(1) << 28)) return fail(c, WC_ERR_INVALID, "ring floats out of range");
+            c->opt_ring = value;
+            return WC_OK;
+        case WC_OPT_PIPE_CLAIM:
+            if (value < 1 || value > 64) return fail(c, WC_ERR_INVALID, "claim must be 1..64");
+            c->opt_claim = (uint32_t)value;
+            return WC_OK;
+        case WC_OPT_PIPE_PREFETCH:
+            c->opt_prefetch = value != 0;
+            return WC_OK;
+        case WC_OPT_PIPE_WGS:
+            if (value < 0 || value > 64) return fail(c, WC_ERR_INVALID, "workgroups per CU must be 0..64");
+            c->opt_wgs = (int)value;
+            return WC_OK;
+        case WC_OPT_PIPE_STATS:
+            c->opt_stats = value != 0;
+            if (c->opt_stats) {
+                int rc = ensure(c, c->stats, sizeof(unsigned long long) * kPipeStats);
+                if (rc) return rc;
+                hipError_t e = hipMemset(c->stats.p, 0, sizeof(unsigned long long) * kPipeStats);
+                if (e != hipSuccess) return hip_fail(c, e, "memset stats");
+            }
             return WC_OK;
         default:
             return fail(c, WC_ERR_INVALID, "unknown option");
@@ -529,8 +658,13 @@ int wc_forward(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, 
     if (n == 0) return WC_OK;
     if (!d_cells || !d_payload || !d_offsets || !d_kept) return fail(c, WC_ERR_INVALID, "null buffer");
     if (cap < wc_payload_bound(units, n)) return fail(c, WC_ERR_INVALID, "payload_capacity < wc_payload_bound");
-    if ((rc = set_device(c)) || (rc = get_plan(c, units, n)) || (rc = ensure_scratch(c))) return rc;
-    return forward_impl(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
+    if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
+    if (c->plan.pipe) {
+        if ((rc = ensure_pipe_scratch(c))) return rc;
+        return forward_pipe(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
+    }
+    if ((rc = ensure_scratch(c))) return rc;
+    return forward_staged(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
 }
 
 int wc_decompose(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, int n, float* d_flat) {
@@ -620,6 +754,19 @@ int wc_rmse(wc_ctx* c, const void* d_orig, int dtype, const float* d_regen, cons
     hipError_t e = launch_rmse(c->stream, d_orig, dtype, d_regen, (const UnitDev*)P.d_units.p, n,
                                (const FTile*)P.d_ftiles.p, (uint32_t)P.ftiles.size(), (double*)c->part.p, d_rmse);
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "rmse launch");
+}
+
+int wc_pipe_stats(wc_ctx* c, uint64_t* out, int n) {
+    if (!c || n < 0 || (n > 0 && !out)) return WC_ERR_INVALID;
+    if (!c->opt_stats || !c->stats.p) return fail(c, WC_ERR_INVALID, "WC_OPT_PIPE_STATS is off");
+    unsigned long long h[kPipeStats] = {};
+    hipError_t e;
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess ||
+        (e = hipMemcpy(h, c->stats.p, sizeof h, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemset(c->stats.p, 0, sizeof h)) != hipSuccess)
+        return hip_fail(c, e, "pipe stats readback");
+    for (int i = 0; i < n && i < kPipeStats; ++i) out[i] = h[i];
+    return WC_OK;
 }
 
 int wc_profile_enable(wc_ctx* c, int on) {

@@ -26,14 +26,19 @@ struct UnitDev {
     int32_t hx, hy, hz;  // n/2 per axis (number of pairs)
     int32_t nbx, nby, nbz;  // blocks per axis = ceil(n/2)
     int32_t lbx, lby, lbz;  // log2 of the transform tile shape in blocks
-    uint32_t ftile_begin;   // first flat (threshold/compaction) tile of this unit
+    uint32_t ftile_begin;   // first flat tile (kFlatTile) of this unit: staged forward, decode, RMSE
     uint32_t nftiles;       // number of flat tiles = ceil(ncells / kFlatTile)
     uint64_t pay_off;       // payload slot: prefix of worst-case sizes, == 4 (mod 8)
-    uint64_t tab_off;       // fused units: first row-table granule (4 rows per granule)
-    uint32_t xt_begin;      // fused units: first tile in the fused tile list
-    uint32_t ntile_u;       // fused units: tiles G of this unit
-    int32_t ntz;            // z tiles per unit (segments per flat row half)
-    int32_t fused;          // 1: handled by k_forward_fused, 0: staged path
+    int32_t ntz;            // z tiles per unit
+    int32_t fast;           // 1: even dims, D % 8 == 0 -> the fast transform body
+    // pipelined forward (wc_pipe.hip)
+    uint64_t ring_off;      // element offset of the unit's coefficients in the ring (chunk aligned)
+    uint32_t ntx;           // transform tiles of the unit
+    uint32_t et_begin;      // first emit tile (kEmitTile coefficients) of the unit
+    uint32_t net;           // emit tiles = max(1, ceil(ncells / kEmitTile))
+    uint32_t wl_off;        // ring wait list: units whose emit tiles must finish before
+    uint32_t wl_len;        //   this unit's transform tiles overwrite their ring chunks
+    uint32_t xt_begin;      // first transform tile of the unit in the plan's tile list
 };
 
 // A transform tile: a (1<<lbx) x (1<<lby) x (1<<lbz) box of 2x2x2 blocks.
@@ -58,25 +63,47 @@ constexpr uint32_t kErrNegativeRun = 2u; // a run length < 0 (reference: UB)
 constexpr uint32_t kErrTooManyPairs = 4u;// nrle > ncoeff
 constexpr uint32_t kErrTimeout = 8u;     // a fused-kernel hand-off wait hit its bound
 
-// The fused forward kernel keeps a unit's G tiles co-resident; cap G well
-// below the resident grid (>= 1024 tiles of 256 threads on 256 CUs).
-constexpr uint32_t kMaxFusedTiles = 256;
-// ... and the unit's row table (one 14-bit record per flat row, kept in LDS).
-constexpr uint64_t kMaxFusedRows = 4096;
+// Pipelined forward kernel (wc_pipe.hip).
+constexpr int kEmitTile = 8192;          // coefficients per emit tile (32 per thread)
+constexpr uint32_t kRingChunk = 4096;    // ring allocation granule (floats); one writer per chunk per lap
 
-// Parameter block of k_forward_fused (wc_fused.hip), filled by wc_capi.cpp.
-struct FusedParams {
+// Pipe diagnostics (s_memrealtime ticks, 100 MHz), summed over workgroups.
+enum PipeStat {
+    kStT = 0,        // transform items: ticks from start to end
+    kStTWait,        // ... of which waiting for ring space
+    kStE,            // emit items: ticks from start to end
+    kStEWait,        // ... of which waiting for the unit's transform tiles
+    kStELook,        // ... of which in the look-back
+    kStClaim,        // waiting for a claimed ticket to return
+    kStNT,           // transform items
+    kStNE,           // emit items
+    kPipeStats = 8
+};
+
+// Parameter block of k_forward_pipe, filled by wc_capi.cpp.
+struct PipeParams {
     const void* cells;
     const UnitDev* units;
-    const XTile* tiles;           // fused tiles, unit-major
-    uint32_t ntiles;
+    const XTile* xtiles;           // transform tiles, unit-major
+    const FTile* etiles;           // emit tiles, unit-major
+    const uint32_t* items;         // work list: bit 31 set = emit tile, else transform tile
+    const uint32_t* waits;         // ring wait lists (unit indices)
+    float* ring;                   // coefficient ring (MALL-resident by size)
+    uint32_t ring_bytes;
+    uint32_t nitems;
     int n;
-    uint32_t* ticket;             // zeroed per call
-    unsigned long long* keyslot;  // [ntiles], zeroed per call
-    unsigned long long* table;    // row-table granules, zeroed per call
+    uint32_t claim;                // items per ticket (consecutive), >= 1
+    uint32_t prefetch;             // 1: claim the next batch while working on the current one
+    unsigned long long* stats;     // optional (WC_OPT_PIPE_STATS): kPipeStats counters, or null
+    // per-call state, zeroed by one memset: [ticket | key[n] | tdone[n] | edone[n] | status[net]]
+    uint32_t* ticket;
+    unsigned long long* key;       // unit max keys (wc_xform.h coef_key)
+    uint32_t* tdone;               // transform tiles finished, per unit
+    uint32_t* edone;               // emit tiles that finished reading the ring, per unit
+    unsigned long long* status;    // decoupled look-back granules, per emit tile
     uint8_t* payload;
-    uint64_t* offsets;            // [n + 1]
-    uint32_t* kept;               // [n]
+    uint64_t* offsets;             // [n + 1]
+    uint32_t* kept;                // [n]
     uint32_t* err;
     double keep;
 };

@@ -1,0 +1,426 @@
+// wc_pipe.hip — pipelined forward path: transform + keep threshold + ordered
+// pack for a whole batch in ONE persistent launch.
+//
+//   src/compressor.cpp:85-185  wavelet_decompose  -> transform items (wc_xform.h bodies)
+//   src/compressor.cpp:212-216 signed max, thresh -> unit max key (64-bit atomicMax)
+//   src/compressor.cpp:222-238 mask + rle_encode  -> emit items (decoupled look-back)
+//   src/compressor.cpp:55-80   serialize          -> header + pairs written in the unit's slot
+//
+// The work list (built on the host, wc_capi.cpp) interleaves two streams:
+//   T(u, g): transform tile g of unit u: read its cells once, transform, write
+//            the fp32 coefficients into the unit's region of a coefficient
+//            RING (write-through sc1 stores), fold its max key into key[u],
+//            count tdone[u].
+//   E(u, e): emit tile e of unit u = kEmitTile consecutive flat coefficients:
+//            wait tdone[u] == ntx (all transform tiles of u), thresh from
+//            key[u], read its coefficients from the ring (sc1 loads), count,
+//            decoupled look-back over the unit's earlier emit tiles for the
+//            pair offset and the previous kept index, emit (run, value) pairs.
+// E items of a unit are placed `lag` cells of transform work after its last
+// T item, so by the time an E item runs its unit is long finished: the waits
+// confirm instead of block.  The ring is sized to a few tens of MB so the
+// coefficients stay in the 256 MiB Infinity Cache between their write and
+// read; a T item that reuses ring chunks first waits until the units that
+// last wrote them have finished their emit reads (wait lists).
+//
+// Items are claimed in list order from one ticket counter, and every wait
+// is on an item EARLIER in the list: the earliest unfinished item never
+// waits, so the grid drains whatever the residency.  Every spin is bounded
+// and raises kErrTimeout.
+//
+// Hand-offs (MI355X_MICROARCH.md, Valid forms, table row 1): ring stores are
+// 16-B sc1 buffer stores drained by every storing wave before the workgroup
+// barrier and the one-lane tdone add; consumers poll tdone with an sc1 load
+// and read the ring only with sc1 loads after a barrier.  Look-back status
+// words are self-validating 8-byte granules (R2).
+#include "wc_xform.h"
+
+namespace wc {
+
+namespace {
+
+constexpr uint32_t kSpinLimit = 1u << 22;
+constexpr unsigned long long kFlagAgg = 1ull << 62;
+constexpr unsigned long long kFlagIncl = 2ull << 62;
+constexpr unsigned long long kMask31 = 0x7fffffffull;
+
+using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t ld_rlx(const uint32_t* p) {
+    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_rlx(const unsigned long long* p) {
+    return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rlx(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void add_rlx(uint32_t* p, uint32_t v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Ring access: buffer instructions with aux = 16 (sc1): stores write through
+// to the memory side, loads bypass this CU's L1.
+__device__ __forceinline__ void ring_st4(__amdgpu_buffer_rsrc_t r, uint32_t byte, float4 v) {
+    u32x4 d;
+    d.x = __float_as_uint(v.x);
+    d.y = __float_as_uint(v.y);
+    d.z = __float_as_uint(v.z);
+    d.w = __float_as_uint(v.w);
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)byte, 0, 16);
+}
+__device__ __forceinline__ void ring_st1(__amdgpu_buffer_rsrc_t r, uint32_t byte, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)byte, 0, 16);
+}
+__device__ __forceinline__ float4 ring_ld4(__amdgpu_buffer_rsrc_t r, uint32_t byte) {
+    const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte, 0, 16);
+    return make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
+}
+
+__device__ __forceinline__ bool spin_fail(uint32_t& spins, uint32_t* err) {
+    if (++spins > kSpinLimit) {
+        atomicOr(err, kErrTimeout);
+        return true;
+    }
+    __builtin_amdgcn_s_sleep(2);
+    return false;
+}
+
+__device__ __forceinline__ unsigned long long now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+
+// ---------------------------------------------------------------------------
+// T item: transform tile `xt` into the ring.
+template <typename T>
+__device__ __forceinline__ void pipe_transform(const PipeParams& P, __amdgpu_buffer_rsrc_t ring, uint32_t xt,
+                                               float* lds, int tid, unsigned long long* st) {
+    const XTile td = P.xtiles[xt];
+    const UnitDev& U = P.units[td.unit];
+    const T* src = static_cast<const T*>(P.cells) + U.cell_off;
+    if (U.fast)
+        xform_fast_p1<T, false>(src, U, td, lds, tid);
+    else
+        xform_generic_p1<T>(src, U, td, lds, tid);
+    const int lane = tid & 63;
+    // Ring reuse: the units that last wrote this unit's chunks must have
+    // finished reading them (their emit tiles sit earlier in the list).
+    if (tid < 64 && U.wl_len) {
+        const unsigned long long t0 = P.stats ? now_ticks() : 0;
+        for (uint32_t i0 = 0; i0 < U.wl_len; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool need = i < U.wl_len;
+            const uint32_t v = need ? P.waits[U.wl_off + i] : 0u;
+            const uint32_t want = need ? P.units[v].net : 0u;
+            for (uint32_t spins = 0;;) {
+                const bool ok = !need || ld_rlx(P.edone + v) >= want;
+                if (__all(ok)) break;
+                if (spin_fail(spins, P.err)) break;
+            }
+        }
+        if (P.stats && tid == 0) st[kStTWait] += now_ticks() - t0;
+    }
+    __syncthreads();
+    const uint32_t base = 4u * (uint32_t)U.ring_off;
+    unsigned long long kmax;
+    if (U.fast)
+        kmax = xform_fast_p2<true>(U, td, lds, tid,
+                                   [&](int64_t f, float4 v) { ring_st4(ring, base + 4u * (uint32_t)f, v); });
+    else
+        kmax = xform_generic_p2<true>(U, td, lds, tid,
+                                      [&](int64_t f, float v) { ring_st1(ring, base + 4u * (uint32_t)f, v); });
+    kmax = wave_max_u64(kmax);
+    if (lane == 0 && kmax != 0)
+        __hip_atomic_fetch_max(P.key + td.unit, kmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    drain();  // every storing wave: ring stores and the key atomic are complete
+    __syncthreads();
+    if (tid == 0) add_rlx(P.tdone + td.unit, 1u);
+}
+
+// ---------------------------------------------------------------------------
+// E item: threshold + ordered pack of emit tile `et`.
+// Thread t = (wave w, lane l) owns elements w*2048 + it*256 + 4l + j, it 0..7.
+// sm: 16 LDS words of scratch.
+// RING: inside k_forward_pipe (coefficients in the ring, dependency waits);
+// else inside k_emit_lb (coefficients in the staged flat scratch, written by
+// an earlier launch).
+template <bool RING>
+__device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_rsrc_t ring,
+                                          const float* __restrict__ coef, uint32_t et, uint32_t* sm, int tid,
+                                          unsigned long long* st) {
+    const FTile ft = P.etiles[et];
+    const uint32_t u = ft.unit;
+    const UnitDev& U = P.units[u];
+    const int w = tid >> 6, l = tid & 63;
+    unsigned long long* smk = reinterpret_cast<unsigned long long*>(sm);  // sm[0..1]: key
+
+    // 1. the unit's transform tiles are all in the ring
+    if (tid == 0) {
+        if constexpr (RING) {
+            const unsigned long long t0 = P.stats ? now_ticks() : 0;
+            for (uint32_t spins = 0;;) {
+                if (ld_rlx(P.tdone + u) >= U.ntx) break;
+                if (spin_fail(spins, P.err)) break;
+            }
+            smk[0] = ld_rlx(P.key + u);
+            if (P.stats) st[kStEWait] += now_ticks() - t0;
+        } else {
+            smk[0] = P.key[u];
+        }
+    }
+    __syncthreads();
+    const float tf = thresh_as_float(key_thresh(smk[0], P.keep));
+    const uint32_t start = ft.index * (uint32_t)kEmitTile;
+    const uint32_t len = (uint32_t)min((uint64_t)kEmitTile, U.ncells - start);
+
+    // 2. coefficients -> keep bits (bit it*4 + j)
+    float4 q[8];
+    if constexpr (RING) {
+        const uint32_t base = 4u * ((uint32_t)U.ring_off + start);
+#pragma unroll
+        for (int it = 0; it < 8; ++it) q[it] = ring_ld4(ring, base + 16u * (uint32_t)(w * 512 + it * 64 + l));
+    } else {
+        // flat scratch: 16-B aligned per unit, kFlatTile slack past the last unit
+        const float4* __restrict__ p4 = reinterpret_cast<const float4*>(coef + U.coef_off + start);
+#pragma unroll
+        for (int it = 0; it < 8; ++it) q[it] = (uint32_t)(w * 2048 + it * 256 + 4 * l) < len ? p4[w * 512 + it * 64 + l]
+                                                                                              : make_float4(0, 0, 0, 0);
+    }
+    uint32_t kb = 0;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const float e[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t idx = (uint32_t)(w * 2048 + it * 256 + l * 4 + j);
+            kb |= (uint32_t)(idx < len && fabsf(e[j]) > tf) << (it * 4 + j);
+        }
+    }
+    // per-wave count and last kept (tile-relative index + 1)
+    const uint32_t wcnt = wave_sum((uint32_t)__popc(kb));
+    const int hb = kb ? 31 - __clz(kb) : 0;
+    const uint32_t mylast = kb ? (uint32_t)(w * 2048 + (hb >> 2) * 256 + l * 4 + (hb & 3) + 1) : 0u;
+    const uint32_t wlast = wave_max_u32(mylast);
+    if (l == 0) {
+        sm[4 + w] = wcnt;
+        sm[8 + w] = wlast;
+    }
+    __syncthreads();
+
+    // 3. publish the aggregate, look back over the unit's earlier tiles (wave 0)
+    if (w == 0) {
+        uint32_t C = 0, L = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            C += sm[4 + i];
+            L = sm[8 + i] > L ? sm[8 + i] : L;
+        }
+        const uint32_t L1 = L ? start + L : 0u;  // unit-relative last kept + 1
+        uint32_t ecnt = 0, elast = 0;            // exclusive: pairs before, last kept + 1 before
+        if (ft.index == 0) {
+            if (l == 0) st_rlx(P.status + et, kFlagIncl | ((unsigned long long)C << 31) | L1);
+        } else {
+            if (l == 0) st_rlx(P.status + et, kFlagAgg | ((unsigned long long)C << 31) | L1);
+            const unsigned long long t0 = (RING && P.stats) ? now_ticks() : 0;
+            int64_t pos = (int64_t)et - 1;
+            const int64_t first = U.et_begin;
+            // Window of the 64 nearest predecessors (lane l = tile et-1-l; tiles
+            // before the unit read as an inclusive 0).  Lanes up to the nearest
+            // inclusive one are summed once every one of them has published;
+            // a run of published aggregates before the first unpublished tile
+            // is summed and the window slides past it.
+            for (uint32_t spins = 0;;) {
+                const int64_t idx = pos - l;
+                const unsigned long long v = idx >= first ? ld_rlx(P.status + idx) : kFlagIncl;
+                const unsigned long long incl = __ballot((v >> 62) == 2);
+                const unsigned long long zero = __ballot((v >> 62) == 0);
+                const int kI = incl ? __ffsll((long long)incl) - 1 : 64;
+                const int kZ = zero ? __ffsll((long long)zero) - 1 : 64;
+                const int take = kI < kZ ? kI + 1 : kZ;  // lanes [0, take) are summed
+                if (take > 0) {
+                    const bool in = l < take;
+                    ecnt += wave_sum(in ? (uint32_t)((v >> 31) & kMask31) : 0u);
+                    const unsigned long long hasl = __ballot(in && (v & kMask31) != 0);
+                    const uint32_t hl = __shfl((uint32_t)(v & kMask31), hasl ? __ffsll((long long)hasl) - 1 : 0);
+                    if (elast == 0 && hasl) elast = hl;
+                }
+                if (kI < kZ) break;
+                pos -= take;
+                if (take == 0 && spin_fail(spins, P.err)) break;
+            }
+            if (l == 0)
+                st_rlx(P.status + et, kFlagIncl | ((unsigned long long)(ecnt + C) << 31) | (L1 ? L1 : elast));
+            if (RING && P.stats && l == 0) st[kStELook] += now_ticks() - t0;
+        }
+        if (l == 0) {
+            sm[0] = ecnt;
+            sm[1] = elast;
+            // ring reads of this tile are done (all waves passed the barrier above)
+            if constexpr (RING) add_rlx(P.edone + u, 1u);
+            if (ft.index + 1 == U.net) {  // last tile: header + kept + slot offset
+                const uint32_t total = ecnt + C;
+                int32_t* hd = reinterpret_cast<int32_t*>(P.payload + U.pay_off);
+                hd[0] = U.nx;
+                hd[1] = U.ny;
+                hd[2] = U.nz;
+                hd[3] = (int32_t)U.ncells;
+                hd[4] = (int32_t)total;
+                P.kept[u] = total;
+                P.offsets[u] = U.pay_off;
+                if ((int)u == P.n - 1) P.offsets[P.n] = U.pay_off + 20 + 8ull * total;
+            }
+        }
+    }
+    __syncthreads();
+
+    // 4. emit (run, value) pairs: ranks from wave ballots, run = f - prev - 1.
+    // Flat indices are unit-relative and < 2^31: 32-bit arithmetic, with
+    // "no previous kept" = 0xffffffff so that run = f - prev - 1 = f.
+    uint32_t rank = sm[0];
+    uint32_t prev = sm[1] - 1u;
+    for (int i = 0; i < w; ++i) {
+        rank += sm[4 + i];
+        if (sm[8 + i]) prev = start + sm[8 + i] - 1u;
+    }
+    uint2* __restrict__ pairs = reinterpret_cast<uint2*>(P.payload + U.pay_off + 20);
+    const unsigned long long lt = (1ull << l) - 1ull;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const uint32_t nib = (kb >> (it * 4)) & 0xfu;
+        const unsigned long long any = __ballot(nib != 0);
+        if (!any) continue;
+        const uint32_t cnt = (uint32_t)__popc(nib);
+        // exclusive prefix of kept counts over lanes (wave scan of 0..4)
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o);
+            if (l >= o) incl += t;
+        }
+        const uint32_t ebase = start + (uint32_t)(w * 2048 + it * 256 + l * 4);
+        const uint32_t lane_last = ebase + (nib ? 31u - (uint32_t)__clz(nib) : 0u);
+        const unsigned long long below = any & lt;
+        const uint32_t from_lane = __shfl(lane_last, below ? 63 - __clzll(below) : l);
+        uint32_t p = below ? from_lane : prev;
+        uint32_t r = rank + incl - cnt;
+        if (nib) {
+            const float vv[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (nib & (1u << j)) {
+                    const uint32_t f = ebase + (uint32_t)j;
+                    pairs[r] = make_uint2(f - p - 1u, __float_as_uint(vv[j]));
+                    p = f;
+                    ++r;
+                }
+            }
+        }
+        rank += __shfl(incl, 63);
+        prev = __shfl(lane_last, 63 - __clzll(any));
+    }
+}
+
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kThreads, 4) void k_forward_pipe(PipeParams P) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    uint32_t* ctl = reinterpret_cast<uint32_t*>(lds);   // [0]: next batch; [2..17]: stats (tid 0)
+    uint32_t* sm = ctl + 18;                             // emit scratch (16 words)
+    float* tl = lds + 48;                                // transform tile rows (192-B offset)
+    const int tid = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t ring = __builtin_amdgcn_make_buffer_rsrc(P.ring, 0, (int)P.ring_bytes, 0x00020000);
+    // stats accumulators (tid 0 only) live in LDS words ctl[2..]
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(ctl + 2);
+    if (tid == 0) {
+        for (int i = 0; i < kPipeStats; ++i) st[i] = 0;
+        ctl[0] = atomicAdd(P.ticket, 1u);
+    }
+    __syncthreads();
+    const uint32_t K = P.claim;
+    uint32_t batch = __builtin_amdgcn_readfirstlane(ctl[0]);
+    while (batch * K < P.nitems) {
+        uint32_t next = 0;
+        const uint32_t first = batch * K, last = min(first + K, P.nitems);
+        for (uint32_t item = first; item < last; ++item) {
+            if (tid == 0 && P.prefetch && item + 1 == last) next = atomicAdd(P.ticket, 1u);
+            const unsigned long long t0 = (P.stats && tid == 0) ? now_ticks() : 0;
+            const uint32_t code = P.items[item];
+            if (code & 0x80000000u) {
+                pipe_emit<true>(P, ring, nullptr, code & 0x7fffffffu, sm, tid, st);
+                if (P.stats && tid == 0) {
+                    st[kStE] += now_ticks() - t0;
+                    st[kStNE] += 1;
+                }
+            } else {
+                pipe_transform<T>(P, ring, code, tl, tid, st);
+                if (P.stats && tid == 0) {
+                    st[kStT] += now_ticks() - t0;
+                    st[kStNT] += 1;
+                }
+            }
+        }
+        if (tid == 0) {
+            const unsigned long long t0 = P.stats ? now_ticks() : 0;
+            if (!P.prefetch) next = atomicAdd(P.ticket, 1u);
+            ctl[0] = next;
+            if (P.stats) st[kStClaim] += now_ticks() - t0;
+        }
+        __syncthreads();
+        batch = __builtin_amdgcn_readfirstlane(ctl[0]);
+    }
+    if (P.stats && tid == 0)
+        for (int i = 0; i < kPipeStats; ++i) atomicAdd(P.stats + i, st[i]);
+}
+
+// Staged-path emit: one launch over every emit tile of the batch.  Block b
+// belongs to unit etiles[b].unit, but takes its tile index within the unit
+// from that unit's ticket (P.tdone[u], unused by the staged path), so a
+// tile's look-back predecessors have always started (forward progress
+// without assuming dispatch order), and the ticket atomics spread over one
+// address per unit instead of one for the whole grid.
+__global__ __launch_bounds__(kThreads) void k_emit_lb(PipeParams P, const float* __restrict__ coef) {
+    __shared__ __attribute__((aligned(16))) uint32_t sm[32];
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        const uint32_t u = P.etiles[blockIdx.x].unit;
+        sm[16] = P.units[u].et_begin + atomicAdd(P.tdone + u, 1u);
+    }
+    __syncthreads();
+    const uint32_t et = __builtin_amdgcn_readfirstlane(sm[16]);
+    __syncthreads();
+    __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(nullptr, 0, 0, 0x00020000);
+    pipe_emit<false>(P, none, coef, et, sm, tid, nullptr);
+}
+
+}  // namespace
+
+hipError_t launch_emit_lb(hipStream_t st, const PipeParams& p, const float* coef, uint32_t netiles) {
+    if (netiles) k_emit_lb<<<netiles, kThreads, 0, st>>>(p, coef);
+    return hipGetLastError();
+}
+
+size_t pipe_lds_bytes(size_t tile_lds) { return 192 + tile_lds; }
+
+hipError_t launch_forward_pipe(hipStream_t st, int dtype, size_t lds, uint32_t grid, const PipeParams& p) {
+    if (p.nitems == 0) return hipSuccess;
+    if (dtype == 1)
+        k_forward_pipe<double><<<grid, kThreads, lds, st>>>(p);
+    else
+        k_forward_pipe<float><<<grid, kThreads, lds, st>>>(p);
+    return hipGetLastError();
+}
+
+// Workgroups that fit on the device at once (more would only find the
+// ticket counter exhausted).  Residency is not needed for correctness.
+uint32_t pipe_grid(int dtype, size_t lds, int max_per_cu) {
+    int per_cu = 0, ncu = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    const void* fn = dtype == 1 ? (const void*)k_forward_pipe<double> : (const void*)k_forward_pipe<float>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kThreads, lds) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 ||
+        ncu < 1)
+        return 1024;
+    if (max_per_cu > 0 && per_cu > max_per_cu) per_cu = max_per_cu;
+    return (uint32_t)per_cu * (uint32_t)ncu;
+}
+
+}  // namespace wc

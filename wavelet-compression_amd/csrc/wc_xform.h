@@ -1,0 +1,276 @@
+// wc_xform.h — the two transform-tile bodies (K1) shared by the staged
+// kernels (wc_transform.hip) and the pipelined forward kernel (wc_pipe.hip).
+//
+// One-level 3-D Haar, src/compressor.cpp:85-185: a coefficient (I, J, K)
+// depends only on the 2x2x2 input block (I mod hx, J mod hy, K mod hz), so a
+// tile of blocks is transformed in registers (Z, then Y, then X pairs — the
+// reference's sweep order) and its outputs land in LDS rows keyed by flat row
+// (I, J) (flat order is x-slowest / z-fastest, :178-181).  Phase 2 streams
+// the rows out along K through a caller-supplied store functor.
+//
+// Max key (src/compressor.cpp:212-215, std::max_element by |c|):
+//   bits 62..32 |c| bits, 31..1 (0x7fffffff - flat index), bit 0 sign.
+// Larger key = larger magnitude, then SMALLER flat index (first wins); the
+// sign rides along so thresh needs no second lookup.  A NaN at flat index 0
+// (max_element then returns flat[0]: every comparison with NaN is false)
+// is the sentinel ~0 -> thresh NaN -> nothing kept; later NaNs never win.
+#pragma once
+
+#include "wc_device.h"
+
+namespace wc {
+
+__device__ __forceinline__ unsigned long long coef_key(float c, uint32_t f) {
+    const uint32_t bits = __float_as_uint(c);
+    const uint32_t ab = bits & 0x7fffffffu;
+    if (ab > 0x7f800000u) return f == 0 ? kKeyNaNFirst : 0ull;
+    return ((unsigned long long)ab << 32) | ((unsigned long long)(0x7fffffffu - f) << 1) | (bits >> 31);
+}
+
+// thresh = (signed max) * (1 - keep), src/compressor.cpp:216.  key 0 (no
+// coefficients or all NaN) gives max 0 -> thresh 0, as max_element on an
+// all-NaN range returns flat[0] only when it is the sentinel case.
+__device__ __forceinline__ double key_thresh(unsigned long long key, double keep) {
+    if (key == kKeyNaNFirst) return __longlong_as_double(0x7ff8000000000000ll);
+    const uint32_t ab = (uint32_t)(key >> 32) & 0x7fffffffu;
+    const float maxv = __uint_as_float(ab | ((uint32_t)(key & 1ull) << 31));
+    return (double)maxv * (1.0 - keep);
+}
+
+__device__ __forceinline__ void row_of(int row, int lbx, int lby, int& bxl, int& ssx, int& byl, int& ssy) {
+    bxl = row & ((1 << lbx) - 1);
+    int r2 = row >> lbx;
+    ssx = r2 & 1;
+    r2 >>= 1;
+    byl = r2 & ((1 << lby) - 1);
+    ssy = r2 >> lby;
+}
+
+// ---------------------------------------------------------------------------
+// Generic tile: any dims (odd tails pass through on that axis).  LDS row
+// stride 2*TZ + 1 floats.
+template <typename T>
+__device__ __forceinline__ void xform_generic_p1(const T* __restrict__ src, const UnitDev& U,
+                                                               const XTile& td, float* lds, int tid) {
+    const int H = U.ny, W = U.nx;
+    const int hx = U.hx, hy = U.hy, hz = U.hz;
+    const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
+    const int TX = 1 << lbx, TY = 1 << lby, TZ = 1 << lbz;
+    const int rstride = 2 * TZ + 1;
+    const int nblk = TX * TY * TZ;
+    const int64_t sy = W, sz = (int64_t)W * H;
+    const bool vec = ((U.cell_off & 1) == 0) && ((W & 1) == 0);
+    for (int b = tid; b < nblk; b += kThreads) {
+        const int bxl = b & (TX - 1);
+        const int byl = (b >> lbx) & (TY - 1);
+        const int bzl = b >> (lbx + lby);
+        const int bx = td.bx0 + bxl, by = td.by0 + byl, bz = td.bz0 + bzl;
+        if (bx >= U.nbx || by >= U.nby || bz >= U.nbz) continue;
+        const bool px = bx < hx, py = by < hy, pz = bz < hz;
+        float v[2][2][2];  // [dz][dy][dx]
+#pragma unroll
+        for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+            for (int dy = 0; dy < 2; ++dy) {
+                if ((dz == 0 || pz) && (dy == 0 || py)) {
+                    const T* p = src + 2 * (int64_t)bx + sy * (2 * by + dy) + sz * (2 * bz + dz);
+                    load_xpair<T>(p, px, vec, v[dz][dy][0], v[dz][dy][1]);
+                } else {
+                    v[dz][dy][0] = 0.0f;
+                    v[dz][dy][1] = 0.0f;
+                }
+            }
+        float a[2][2][2];  // Z sweep (src/compressor.cpp:98-125): a[sz][dy][dx]
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx) {
+                a[0][dy][dx] = pz ? haar_lo(v[0][dy][dx], v[1][dy][dx]) : v[0][dy][dx];
+                a[1][dy][dx] = pz ? haar_hi(v[0][dy][dx], v[1][dy][dx]) : 0.0f;
+            }
+        float c2[2][2][2];  // Y sweep (:128-150): c2[sz][sy][dx]
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx) {
+                c2[s][0][dx] = py ? haar_lo(a[s][0][dx], a[s][1][dx]) : a[s][0][dx];
+                c2[s][1][dx] = py ? haar_hi(a[s][0][dx], a[s][1][dx]) : 0.0f;
+            }
+        float c[2][2][2];  // X sweep (:153-175): c[sz][sy][sx]
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                c[s][t][0] = px ? haar_lo(c2[s][t][0], c2[s][t][1]) : c2[s][t][0];
+                c[s][t][1] = px ? haar_hi(c2[s][t][0], c2[s][t][1]) : 0.0f;
+            }
+#pragma unroll
+        for (int ssz = 0; ssz < 2; ++ssz)
+#pragma unroll
+            for (int ssy = 0; ssy < 2; ++ssy)
+#pragma unroll
+                for (int ssx = 0; ssx < 2; ++ssx) {
+                    if ((ssx && !px) || (ssy && !py) || (ssz && !pz)) continue;
+                    const float cv = c[ssz][ssy][ssx];
+                    const int row = ((((ssy << lby) + byl) * 2 + ssx) << lbx) + bxl;
+                    lds[row * rstride + (ssz << lbz) + bzl] = cv;
+                }
+    }
+}
+
+// Phase 2 of a generic tile: st(flat index within the unit, value).  With
+// KEYS, also returns this thread's max key over the values it stores (keys
+// are computed here rather than in phase 1, where every coefficient of the
+// thread's blocks is live in registers).
+template <bool KEYS, class Store1>
+__device__ __forceinline__ unsigned long long xform_generic_p2(const UnitDev& U, const XTile& td, const float* lds,
+                                                               int tid, Store1 st) {
+    unsigned long long kmax = 0;
+    const int W = U.nx, H = U.ny, D = U.nz;
+    const int hx = U.hx, hy = U.hy, hz = U.hz;
+    const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
+    const int TX = 1 << lbx, TY = 1 << lby, TZ = 1 << lbz;
+    const int rowlen = 2 * TZ, rstride = rowlen + 1;
+    const int nrows = 4 * TX * TY;
+    const int total = nrows * rowlen;
+    const int lrow = lbz + 1;
+    for (int e = tid; e < total; e += kThreads) {
+        const int row = e >> lrow;
+        const int col = e & (rowlen - 1);
+        const int ssz = col >> lbz, bzl = col & (TZ - 1);
+        int bxl, ssx, byl, ssy;
+        row_of(row, lbx, lby, bxl, ssx, byl, ssy);
+        const int bx = td.bx0 + bxl, by = td.by0 + byl, bz = td.bz0 + bzl;
+        if (bx >= U.nbx || by >= U.nby || bz >= U.nbz) continue;
+        if ((ssx && bx >= hx) || (ssy && by >= hy) || (ssz && bz >= hz)) continue;
+        const int I = out_index(bx, ssx, hx, W), J = out_index(by, ssy, hy, H), K = out_index(bz, ssz, hz, D);
+        const int64_t f = ((int64_t)I * H + J) * D + K;
+        const float v = lds[row * rstride + col];
+        st(f, v);
+        if constexpr (KEYS) {
+            const unsigned long long k = coef_key(v, (uint32_t)f);
+            kmax = k > kmax ? k : kmax;
+        }
+    }
+    return kmax;
+}
+
+// ---------------------------------------------------------------------------
+// Fast tile: even W, H, D with D % 8 == 0 (no tails).  A thread owns a column
+// of 4 consecutive z-blocks (bx, by, bz..bz+3): 16 independent x-pair loads in
+// flight, and each of its 8 output rows gets 4 consecutive K -> one 16-B LDS
+// write.  LDS row stride 2*TZ + 4 floats (16-B rows; b128 writes of 8 lanes
+// hit 32 banks).  Keys come from phase 2.
+template <typename T, bool SPLIT = false>
+__device__ __forceinline__ void xform_fast_p1(const T* __restrict__ src, const UnitDev& U,
+                                                            const XTile& td, float* lds, int tid) {
+    const int W = U.nx, H = U.ny;
+    const int hx = U.hx, hy = U.hy, hz = U.hz;
+    const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
+    const int TX = 1 << lbx, TY = 1 << lby, TZ = 1 << lbz;
+    const int rstride = 2 * TZ + 4;
+    const int ncol = (TX * TY * TZ) >> 2;
+    const int64_t sy = W, sz = (int64_t)W * H;
+    const bool vec = (U.cell_off & 1) == 0;
+    for (int ci = tid; ci < ncol; ci += kThreads) {
+        const int bxl = ci & (TX - 1);
+        const int byl = (ci >> lbx) & (TY - 1);
+        const int bzq = ci >> (lbx + lby);  // quad of z-blocks within the tile
+        const int bx = td.bx0 + bxl, by = td.by0 + byl, bzb = td.bz0 + 4 * bzq;
+        if (bx >= hx || by >= hy || bzb >= hz) continue;
+        const T* p0 = src + 2 * (int64_t)bx + sy * (2 * by) + sz * (2 * (int64_t)bzb);
+        float c[4][2][2][2];  // [q][sz][sy][sx]
+        // Two halves of 4 z-planes (8 x-pair loads in flight each): bounds the
+        // raw fp64 registers so 4 workgroups fit per CU.
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            float v[4][2][2];  // [z plane 4h..4h+3][dy][dx]
+#pragma unroll
+            for (int zp = 0; zp < 4; ++zp)
+#pragma unroll
+                for (int dy = 0; dy < 2; ++dy)
+                    load_xpair<T>(p0 + sz * (4 * h + zp) + sy * dy, true, vec, v[zp][dy][0], v[zp][dy][1]);
+#pragma unroll
+            for (int qq = 0; qq < 2; ++qq) {
+                const int q = 2 * h + qq;
+                float a[2][2][2];
+#pragma unroll
+                for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+                    for (int dx = 0; dx < 2; ++dx) {
+                        a[0][dy][dx] = haar_lo(v[2 * qq][dy][dx], v[2 * qq + 1][dy][dx]);
+                        a[1][dy][dx] = haar_hi(v[2 * qq][dy][dx], v[2 * qq + 1][dy][dx]);
+                    }
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    float b[2][2];
+#pragma unroll
+                    for (int dx = 0; dx < 2; ++dx) {
+                        b[0][dx] = haar_lo(a[s][0][dx], a[s][1][dx]);
+                        b[1][dx] = haar_hi(a[s][0][dx], a[s][1][dx]);
+                    }
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        c[q][s][t][0] = haar_lo(b[t][0], b[t][1]);
+                        c[q][s][t][1] = haar_hi(b[t][0], b[t][1]);
+                    }
+                }
+            }
+            if (SPLIT && h == 0) __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int ssz = 0; ssz < 2; ++ssz)
+#pragma unroll
+            for (int ssy = 0; ssy < 2; ++ssy)
+#pragma unroll
+                for (int ssx = 0; ssx < 2; ++ssx) {
+                    const int row = ((((ssy << lby) + byl) * 2 + ssx) << lbx) + bxl;
+                    *reinterpret_cast<float4*>(lds + row * rstride + (ssz << lbz) + 4 * bzq) =
+                        make_float4(c[0][ssz][ssy][ssx], c[1][ssz][ssy][ssx], c[2][ssz][ssy][ssx],
+                                    c[3][ssz][ssy][ssx]);
+                }
+    }
+}
+
+// Phase 2 of a fast tile: st(flat index within the unit (multiple of 4), float4);
+// with KEYS, returns this thread's max key.
+template <bool KEYS, class Store4>
+__device__ __forceinline__ unsigned long long xform_fast_p2(const UnitDev& U, const XTile& td, const float* lds,
+                                                            int tid, Store4 st) {
+    unsigned long long kmax = 0;
+    const int H = U.ny, D = U.nz;
+    const int hx = U.hx, hy = U.hy, hz = U.hz;
+    const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
+    const int TX = 1 << lbx, TY = 1 << lby, TZ = 1 << lbz;
+    const int rstride = 2 * TZ + 4;
+    const int nrows = 4 * TX * TY;
+    const int q4 = lbz - 1;  // log2(rowlen / 4)
+    const int total4 = nrows << q4;
+    for (int e = tid; e < total4; e += kThreads) {
+        const int row = e >> q4;
+        const int col = (e & ((1 << q4) - 1)) << 2;
+        const int ssz = col >> lbz, bzl = col & (TZ - 1);
+        int bxl, ssx, byl, ssy;
+        row_of(row, lbx, lby, bxl, ssx, byl, ssy);
+        const int bx = td.bx0 + bxl, by = td.by0 + byl, bz = td.bz0 + bzl;
+        if (bx >= hx || by >= hy || bz >= hz) continue;
+        const int I = bx + ssx * hx, J = by + ssy * hy, K = bz + ssz * hz;
+        const int64_t f = ((int64_t)I * H + J) * D + K;
+        const float4 v = *reinterpret_cast<const float4*>(lds + row * rstride + col);
+        st(f, v);
+        if constexpr (KEYS) {
+            const uint32_t f0 = (uint32_t)f;
+            unsigned long long k = coef_key(v.x, f0);
+            kmax = k > kmax ? k : kmax;
+            k = coef_key(v.y, f0 + 1);
+            kmax = k > kmax ? k : kmax;
+            k = coef_key(v.z, f0 + 2);
+            kmax = k > kmax ? k : kmax;
+            k = coef_key(v.w, f0 + 3);
+            kmax = k > kmax ? k : kmax;
+        }
+    }
+    return kmax;
+}
+
+}  // namespace wc
