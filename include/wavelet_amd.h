@@ -89,7 +89,7 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports kernel-side errors of earlier 
  *   the Infinity Cache) with emit tiles.  Results are byte-identical either
  *   way (DESIGN.md has the timings of both).
  * WC_OPT_PIPE_LAG: cells of transform work listed between a unit's last
- *   transform tile and its first emit tile (0 = default, 4 Mi cells).
+ *   transform tile and its emit work (0 = default, 16 Mi cells).
  * WC_OPT_PIPE_RING: coefficient ring size in floats (0 = default: lag + 8 Mi
  *   + 2 x the largest unit; never more than the batch needs). */
 #define WC_OPT_PIPE 1
@@ -99,6 +99,9 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports kernel-side errors of earlier 
 #define WC_OPT_PIPE_PREFETCH 5  /* 1: claim the next ticket while working (default 0) */
 #define WC_OPT_PIPE_WGS 6       /* workgroups per CU (0 = occupancy limit) */
 #define WC_OPT_PIPE_STATS 7     /* 1: collect wait-time counters (wc_pipe_stats) */
+#define WC_OPT_CHUNK 8          /* staged forward over chunks of this many cells, transform of
+                                   chunk c+1 overlapping emit of chunk c (0 = whole batch) */
+#define WC_OPT_CHUNK_SLOTS 9    /* coefficient slots of the chunked forward (default 3) */
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 
 /* Diagnostics of the pipelined kernel (WC_OPT_PIPE_STATS on): summed over
@@ -165,7 +168,8 @@ int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* 
 #define WC_STAGE_INVERSE 6    /* K6  */
 #define WC_STAGE_RMSE 7       /* K7  */
 #define WC_STAGE_PIPE 8       /* pipelined forward kernel (whole wc_forward) */
-#define WC_NUM_STAGES 9
+#define WC_STAGE_CHUNKED 9    /* chunked forward, first to last launch (whole wc_forward) */
+#define WC_NUM_STAGES 10
 int wc_profile_enable(wc_ctx* ctx, int on);
 int wc_profile_read(wc_ctx* ctx, double* total_ms, uint32_t* launches, int nstages);
 

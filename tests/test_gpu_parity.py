@@ -337,7 +337,7 @@ def test_pipe_stats_counters(wc, ctx, oracle):
         ctx.set_option(wc.capi.WC_OPT_PIPE_STATS, 0)
         ctx.set_pipe(False)
     assert st[6] == 8 * 32 + 4 * 1   # transform tiles: 64^3 -> 32 tiles of 64x2x64, 16^3 -> 1
-    assert st[7] == 8 * 32 + 4 * 1   # emit tiles of 8192 coefficients
+    assert st[7] == 8 + 4            # emit items: one whole-unit item per unit
     for i, b in enumerate(boxes):
         assert wc.capi.unit_payload(payload, offs, kept, i) == oracle_payload(oracle, b, KEEPS[1])
 

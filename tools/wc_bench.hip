@@ -6,6 +6,7 @@
 //
 // usage: wc_bench [boxes=1024] [dim=64] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1]
 //                 [pipe=1|0] [check=0|1] [lag=0] [ring=0] [claim=1] [prefetch=0] [wgs=0] [stats=0]
+//                 [chunk=0] [slots=3]
 // check=1: also run the staged path once and compare every unit's payload
 // bytes with the pipelined path's ("paths_identical" in the JSON line).
 // lag / ring: WC_OPT_PIPE_LAG / WC_OPT_PIPE_RING (0 = library defaults).
@@ -69,6 +70,8 @@ int main(int argc, char** argv) {
     const int prefetch = argc > 13 ? std::atoi(argv[13]) : 0;
     const int wgs = argc > 14 ? std::atoi(argv[14]) : 0;
     const int stats = argc > 15 ? std::atoi(argv[15]) : 0;
+    const long long chunk = argc > 16 ? std::atoll(argv[16]) : 0;
+    const int slots = argc > 17 ? std::atoi(argv[17]) : 3;
 
     std::vector<wc_unit> units(boxes);
     const unsigned long long per = (unsigned long long)dim * dim * dim;
@@ -103,6 +106,8 @@ int main(int argc, char** argv) {
     wc_set_option(ctx, WC_OPT_PIPE_CLAIM, claim);
     wc_set_option(ctx, WC_OPT_PIPE_PREFETCH, prefetch);
     wc_set_option(ctx, WC_OPT_PIPE_WGS, wgs);
+    wc_set_option(ctx, WC_OPT_CHUNK, chunk);
+    wc_set_option(ctx, WC_OPT_CHUNK_SLOTS, slots);
     auto fwd = [&]() {
         int rc = wc_forward(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, keep, payload, cap, offsets, kept);
         if (rc != WC_OK) {
@@ -150,11 +155,10 @@ int main(int argc, char** argv) {
     }
     int identical = -1;
     if (check) {
-        // Pipelined vs staged: every unit's serialized bytes must match.
+        // Configured path vs the plain staged path: every unit's serialized bytes must match.
         std::vector<uint64_t> off_a(boxes + 1), off_b(boxes + 1);
         std::vector<uint32_t> k_a(boxes), k_b(boxes);
         std::vector<uint8_t> pa(cap), pb(cap);
-        wc_set_option(ctx, WC_OPT_PIPE, 1);
         fwd();
         wc_synchronize(ctx);
         CK(hipMemcpy(off_a.data(), offsets, 8 * (boxes + 1), hipMemcpyDeviceToHost));
@@ -162,6 +166,7 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(pa.data(), payload, cap, hipMemcpyDeviceToHost));
         CK(hipMemset(payload, 0xA5, cap));
         wc_set_option(ctx, WC_OPT_PIPE, 0);
+        wc_set_option(ctx, WC_OPT_CHUNK, 0);
         fwd();
         wc_synchronize(ctx);
         CK(hipMemcpy(off_b.data(), offsets, 8 * (boxes + 1), hipMemcpyDeviceToHost));
@@ -173,6 +178,7 @@ int main(int argc, char** argv) {
             else if (std::memcmp(pa.data() + off_a[i], pb.data() + off_b[i], 20 + 8ull * k_a[i]) != 0) identical = 0;
         }
         wc_set_option(ctx, WC_OPT_PIPE, pipe ? 1 : 0);
+        wc_set_option(ctx, WC_OPT_CHUNK, chunk);
     }
     uint64_t total = 0;
     CK(hipMemcpy(&total, offsets + boxes, 8, hipMemcpyDeviceToHost));
@@ -181,7 +187,7 @@ int main(int argc, char** argv) {
     double ksum = 0;
     for (uint32_t k : hk) ksum += k;
     const char* names[WC_NUM_STAGES] = {"transform", "flat_count", "unit_scan", "unit_offsets",
-                                        "flat_emit", "decode", "inverse", "rmse", "pipe"};
+                                        "flat_emit", "decode", "inverse", "rmse", "pipe", "chunked"};
     std::printf("{\"boxes\": %d, \"dim\": %d, \"dtype\": \"%s\", \"keep\": %.17g, \"steps\": %d, "
                 "\"ms_per_step\": %.4f, \"cells_per_s\": %.6e, \"kept_fraction\": %.6f, \"payload_bytes\": %llu, "
                 "\"pipe\": %d, \"lag\": %lld, \"ring\": %lld, \"paths_identical\": %d, \"stage_ms\": {",

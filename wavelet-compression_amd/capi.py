@@ -31,10 +31,11 @@ EXPORTED = (
 )
 WC_OPT_PIPE, WC_OPT_PIPE_LAG, WC_OPT_PIPE_RING = 1, 2, 3
 WC_OPT_PIPE_CLAIM, WC_OPT_PIPE_PREFETCH, WC_OPT_PIPE_WGS, WC_OPT_PIPE_STATS = 4, 5, 6, 7
+WC_OPT_CHUNK, WC_OPT_CHUNK_SLOTS = 8, 9
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*), kernel names as rocprof shows them.
 STAGES = ("transform", "flat_count", "unit_scan", "unit_offsets", "flat_emit", "decode", "inverse", "rmse",
-          "pipe")
+          "pipe", "chunked")
 
 
 class WcUnit(ctypes.Structure):

@@ -73,6 +73,17 @@ struct Plan {
     uint64_t ring_floats = 0;  // pipe coefficient ring
     size_t lds_gen = 0, lds_fast = 0, lds_inverse = 0, lds_pipe = 0;
     size_t state_bytes = 0;    // pipe per-call state: ticket | key[n] | tdone[n] | edone[n] | status[netiles]
+    // chunked forward (WC_OPT_CHUNK): unit ranges whose coefficients fit one slot
+    struct Chunk {
+        uint32_t u0, u1;            // units [u0, u1)
+        uint32_t gen_b, gen_n;      // generic transform tiles
+        uint32_t fast_b, fast_n;    // fast transform tiles
+        uint32_t et_b, et_n;        // emit tiles
+    };
+    int64_t chunk_req = 0;
+    std::vector<Chunk> chunks;
+    uint64_t slot_floats = 0;
+    int nslots = 0;
     DevBuf d_units, d_xtiles, d_ftiles, d_etiles, d_items, d_waits;
 };
 
@@ -98,6 +109,10 @@ struct wc_ctx {
     bool opt_prefetch = false;  // WC_OPT_PIPE_PREFETCH
     int opt_wgs = 0;         // WC_OPT_PIPE_WGS (0 = occupancy limit)
     bool opt_stats = false;  // WC_OPT_PIPE_STATS
+    int64_t opt_chunk = 0;   // WC_OPT_CHUNK: cells per chunk (0 = whole batch at once)
+    int opt_slots = 3;       // WC_OPT_CHUNK_SLOTS
+    hipStream_t side = nullptr;        // second stream of the chunked forward (emit launches)
+    std::vector<hipEvent_t> chunk_ev;  // 2 per chunk + 1
     bool err_check_pending = false;
     // scratch (grow-only)
     DevBuf coef, tsum, tbase, part, errflag, ring, state, stats;
@@ -210,7 +225,7 @@ void push_tiles(std::vector<XTile>& v, const UnitDev& d, uint32_t u) {
             for (int bx = 0; bx < d.nbx; bx += TX) v.push_back(XTile{u, (uint32_t)bx, (uint32_t)by, (uint32_t)bz});
 }
 
-constexpr int64_t kDefaultLag = int64_t(4) << 20;    // cells of transform work between a unit and its emit tiles
+constexpr int64_t kDefaultLag = int64_t(16) << 20;   // cells of transform work between a unit and its emit work
 constexpr int64_t kDefaultRingExtra = int64_t(8) << 20;  // ring floats beyond the lag (tiles in flight)
 
 uint64_t round_up(uint64_t v, uint64_t m) { return (v + m - 1) / m * m; }
@@ -271,47 +286,94 @@ void build_pipe(Plan& P, int n) {
         d.wl_len = (uint32_t)w.size();
         cur += a;
     }
-    // Work list: transform tiles in unit order; a unit's emit tiles once
-    // `lag` more cells of transform work have been listed after its last
-    // transform tile; all emit tiles of the units a transform waits for come
-    // before it.  Every wait is therefore on an earlier item.
+    // Work list: transform tiles in unit order; a unit's emit work once `lag`
+    // more cells of transform work have been listed after its last transform
+    // tile, as ONE whole-unit item (no look-back); units whose emit work
+    // comes after the last transform tile (the drain) are split into emit
+    // tiles with look-back instead, so the tail runs wide.  All emit work of
+    // the units a transform waits for comes before it.  Every wait is
+    // therefore on an earlier item.
     std::vector<int64_t> tend(n);
-    const uint32_t NE = (uint32_t)P.etiles.size();
-    uint32_t ep = 0;
+    int eu = 0;  // next unit whose emit work is not listed yet
     int64_t tc = 0;
-    auto emit_until = [&](uint32_t target) {
-        for (; ep < target; ++ep) P.items.push_back(0x80000000u | ep);
+    bool t_left = true;
+    auto emit_unit = [&](int v) {
+        UnitDev& d = P.units[v];
+        d.ewant = 1;
+        P.items.push_back(0xC0000000u | (uint32_t)v);
+        (void)t_left;
+    };
+    auto emit_until = [&](int target) {
+        for (; eu < target; ++eu) emit_unit(eu);
     };
     auto emit_eligible = [&](int upto_unit) {
-        while (ep < NE) {
-            const uint32_t v = P.etiles[ep].unit;
-            if ((int)v > upto_unit || tend[v] + lag > tc) break;
-            P.items.push_back(0x80000000u | ep++);
-        }
+        while (eu <= upto_unit && tend[eu] + lag <= tc) emit_unit(eu++);
     };
+    int last_t = -1;
+    for (int u = 0; u < n; ++u)
+        if (P.units[u].ntx) last_t = u;
     for (int u = 0; u < n; ++u) {
         const UnitDev& d = P.units[u];
-        for (uint32_t k = 0; k < d.wl_len; ++k) {
-            const UnitDev& v = P.units[P.waits[d.wl_off + k]];
-            emit_until(std::max(ep, v.et_begin + v.net));
-        }
+        for (uint32_t k = 0; k < d.wl_len; ++k) emit_until(std::max(eu, (int)P.waits[d.wl_off + k] + 1));
         const int64_t tcells = (int64_t)8 << (d.lbx + d.lby + d.lbz);
         for (uint32_t g = 0; g < d.ntx; ++g) {
             P.items.push_back(d.xt_begin + g);
             tc += tcells;
             if (g + 1 == d.ntx) tend[u] = tc;
+            if (u == last_t && g + 1 == d.ntx) t_left = false;
             emit_eligible(u - 1);
         }
         if (d.ntx == 0) tend[u] = tc;
         emit_eligible(u);
     }
-    emit_until(NE);
+    t_left = false;
+    emit_until(n);
+}
+
+// Chunked forward: consecutive units grouped until their coefficients reach
+// chunk_req floats (a larger unit is a chunk of its own); chunk c's
+// coefficients live in slot c % nslots (ring_off), so a slot is rewritten
+// only after the emit launch that read it has finished.
+void build_chunks(Plan& P, int n) {
+    uint32_t gcur = 0, fcur = P.ngen;
+    uint64_t slot = 0;
+    int u = 0;
+    while (u < n) {
+        Plan::Chunk ch{};
+        ch.u0 = (uint32_t)u;
+        ch.gen_b = gcur;
+        ch.fast_b = fcur;
+        ch.et_b = P.units[u].et_begin;
+        uint64_t fl = 0;
+        do {
+            UnitDev& d = P.units[u];
+            d.ring_off = fl;  // relative to the slot for now
+            fl = round_up(fl + d.ncells, 4);
+            if (d.fast)
+                fcur += d.ntx;
+            else
+                gcur += d.ntx;
+            ch.et_n += d.net;
+            ++u;
+        } while (u < n && fl + P.units[u].ncells <= (uint64_t)P.chunk_req);
+        ch.u1 = (uint32_t)u;
+        ch.gen_n = gcur - ch.gen_b;
+        ch.fast_n = fcur - ch.fast_b;
+        slot = std::max(slot, fl);
+        P.chunks.push_back(ch);
+    }
+    P.slot_floats = round_up(std::max<uint64_t>(slot, 4), 4);
+    for (size_t c = 0; c < P.chunks.size(); ++c)
+        for (uint32_t v = P.chunks[c].u0; v < P.chunks[c].u1; ++v)
+            P.units[v].ring_off += (c % P.nslots) * P.slot_floats;
+    P.ring_floats = P.slot_floats * P.nslots + kEmitTile;
 }
 
 // Build (or reuse) the plan for this batch and upload it.
 int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     Plan& P = c->plan;
     if (c->plan_valid && P.pipe == c->opt_pipe && P.lag == c->opt_lag && P.ring_req == c->opt_ring &&
+        P.chunk_req == c->opt_chunk && P.nslots == (c->opt_chunk ? c->opt_slots : 0) &&
         (int)P.key.size() == n && (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0))
         return WC_OK;
     c->plan_valid = false;
@@ -321,6 +383,9 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     P.waits.clear();
     P.lag = c->opt_lag;
     P.ring_req = c->opt_ring;
+    P.chunk_req = c->opt_chunk;
+    P.nslots = c->opt_chunk ? c->opt_slots : 0;
+    P.chunks.clear();
     P.units.assign(n, UnitDev{});
     P.xtiles.clear();
     P.ftiles.clear();
@@ -375,6 +440,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     }
     P.coef_extent = coef_cursor ? coef_cursor + kFlatTile : 0;  // slack: flat tiles read whole float4 groups
     build_etiles(P, n);
+    if (!P.pipe && P.chunk_req > 0) build_chunks(P, n);
     if (P.pipe) {
         build_pipe(P, n);
         P.lds_pipe = pipe_lds_bytes(std::max(P.lds_gen, P.lds_fast));
@@ -464,6 +530,8 @@ PipeParams pipe_params(wc_ctx* c, const void* d_cells, int n, double keep, uint8
     p.err = (uint32_t*)c->errflag.p;
     p.keep = keep;
     p.claim = 1;
+    const char* dbg = std::getenv("WCAMD_DBG");
+    p.dbg = dbg ? (uint32_t)std::atoi(dbg) : 0u;
     return p;
 }
 
@@ -517,6 +585,55 @@ int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep
         e = launch_emit_lb(c->stream, p, coef, (uint32_t)P.etiles.size());
     }
     if (e != hipSuccess) return hip_fail(c, e, "emit launch");
+    return WC_OK;
+}
+
+// Chunked forward: transform of chunk c+1 (context stream) overlaps the emit
+// of chunk c (side stream); events order each emit after its transform and
+// each slot's rewrite after the emit that read it.
+int forward_chunked(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
+                    uint64_t* d_offsets, uint32_t* d_kept) {
+    Plan& P = c->plan;
+    const UnitDev* du = (const UnitDev*)P.d_units.p;
+    const XTile* dxt = (const XTile*)P.d_xtiles.p;
+    hipError_t e;
+    if (!c->side && (e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) != hipSuccess)
+        return hip_fail(c, e, "side stream");
+    const size_t nev = 2 * P.chunks.size() + 1;
+    while (c->chunk_ev.size() < nev) {
+        hipEvent_t ev = nullptr;
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(c, e, "event");
+        c->chunk_ev.push_back(ev);
+    }
+    hipEvent_t* ev_t = c->chunk_ev.data();
+    hipEvent_t* ev_e = ev_t + P.chunks.size();
+    hipEvent_t ev0 = ev_t[2 * P.chunks.size()];
+    StageTimer timer(c, WC_STAGE_CHUNKED);
+    if ((e = hipMemsetAsync(c->state.p, 0, P.state_bytes, c->stream)) != hipSuccess)
+        return hip_fail(c, e, "memset state");
+    PipeParams p = pipe_params(c, d_cells, n, keep, d_payload, d_offsets, d_kept);
+    p.ring_coefs = 1;
+    float* ring = (float*)c->ring.p;
+    if ((e = hipEventRecord(ev0, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(c->side, ev0, 0)) != hipSuccess)
+        return hip_fail(c, e, "chunk start");
+    for (size_t k = 0; k < P.chunks.size(); ++k) {
+        const Plan::Chunk& ch = P.chunks[k];
+        if (k >= (size_t)P.nslots && (e = hipStreamWaitEvent(c->stream, ev_e[k - P.nslots], 0)) != hipSuccess)
+            return hip_fail(c, e, "slot wait");
+        e = launch_transform(c->stream, d_cells, dtype, du, dxt + ch.gen_b, ch.gen_n, P.lds_gen, ring, 2, p.key);
+        if (e == hipSuccess)
+            e = launch_transform_fast(c->stream, d_cells, dtype, du, dxt + ch.fast_b, ch.fast_n, P.lds_fast, ring, 2,
+                                      p.key);
+        if (e != hipSuccess) return hip_fail(c, e, "transform launch");
+        if ((e = hipEventRecord(ev_t[k], c->stream)) != hipSuccess ||
+            (e = hipStreamWaitEvent(c->side, ev_t[k], 0)) != hipSuccess)
+            return hip_fail(c, e, "chunk event");
+        p.etile_base = ch.et_b;
+        if ((e = launch_emit_lb(c->side, p, ring, ch.et_n)) != hipSuccess) return hip_fail(c, e, "emit launch");
+        if ((e = hipEventRecord(ev_e[k], c->side)) != hipSuccess) return hip_fail(c, e, "chunk event");
+    }
+    if ((e = hipStreamWaitEvent(c->stream, ev_e[P.chunks.size() - 1], 0)) != hipSuccess)
+        return hip_fail(c, e, "chunk join");
     return WC_OK;
 }
 
@@ -579,6 +696,11 @@ void wc_ctx_destroy(wc_ctx* c) {
         c->ev_pool.push_back(m.b);
     }
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->chunk_ev) (void)hipEventDestroy(e);
+    if (c->side) {
+        (void)hipStreamSynchronize(c->side);
+        (void)hipStreamDestroy(c->side);
+    }
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -615,6 +737,14 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
         case WC_OPT_PIPE_WGS:
             if (value < 0 || value > 64) return fail(c, WC_ERR_INVALID, "workgroups per CU must be 0..64");
             c->opt_wgs = (int)value;
+            return WC_OK;
+        case WC_OPT_CHUNK:
+            if (value < 0) return fail(c, WC_ERR_INVALID, "chunk cells < 0");
+            c->opt_chunk = value;
+            return WC_OK;
+        case WC_OPT_CHUNK_SLOTS:
+            if (value < 2 || value > 16) return fail(c, WC_ERR_INVALID, "chunk slots must be 2..16");
+            c->opt_slots = (int)value;
             return WC_OK;
         case WC_OPT_PIPE_STATS:
             c->opt_stats = value != 0;
@@ -662,6 +792,10 @@ int wc_forward(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, 
     if (c->plan.pipe) {
         if ((rc = ensure_pipe_scratch(c))) return rc;
         return forward_pipe(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
+    }
+    if (!c->plan.chunks.empty()) {
+        if ((rc = ensure_scratch(c)) || (rc = ensure_pipe_scratch(c))) return rc;
+        return forward_chunked(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
     }
     if ((rc = ensure_scratch(c))) return rc;
     return forward_staged(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);

@@ -39,6 +39,8 @@ struct UnitDev {
     uint32_t wl_off;        // ring wait list: units whose emit tiles must finish before
     uint32_t wl_len;        //   this unit's transform tiles overwrite their ring chunks
     uint32_t xt_begin;      // first transform tile of the unit in the plan's tile list
+    uint32_t ewant;         // pipe: emit items of the unit (1 = one whole-unit item, else net tiles)
+    uint32_t pad_;
 };
 
 // A transform tile: a (1<<lbx) x (1<<lby) x (1<<lbz) box of 2x2x2 blocks.
@@ -106,6 +108,9 @@ struct PipeParams {
     uint32_t* kept;                // [n]
     uint32_t* err;
     double keep;
+    uint32_t dbg;                  // experiment switches (WCAMD_DBG), 0 in production
+    uint32_t etile_base;           // k_emit_lb: first emit tile of this launch
+    uint32_t ring_coefs;           // k_emit_lb: 1 = coefficients at ring_off (chunk slots), 0 = coef_off
 };
 
 }  // namespace wc

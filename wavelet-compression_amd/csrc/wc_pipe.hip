@@ -39,7 +39,7 @@ namespace wc {
 
 namespace {
 
-constexpr uint32_t kSpinLimit = 1u << 22;
+constexpr uint32_t kSpinLimit = 1u << 20;  // x ~1.7 us: ~2 s before a wait is declared hung
 constexpr unsigned long long kFlagAgg = 1ull << 62;
 constexpr unsigned long long kFlagIncl = 2ull << 62;
 constexpr unsigned long long kMask31 = 0x7fffffffull;
@@ -78,12 +78,20 @@ __device__ __forceinline__ float4 ring_ld4(__amdgpu_buffer_rsrc_t r, uint32_t by
     return make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
 }
 
+// Bounded spin with backoff: pollers share the memory system with the
+// streaming loads (MI355X_MICROARCH.md: 255 pollers cut chip bandwidth
+// 37-71 %), so re-polls slow down from ~0.2 us to ~1.7 us.
 __device__ __forceinline__ bool spin_fail(uint32_t& spins, uint32_t* err) {
     if (++spins > kSpinLimit) {
         atomicOr(err, kErrTimeout);
         return true;
     }
-    __builtin_amdgcn_s_sleep(2);
+    if (spins < 4)
+        __builtin_amdgcn_s_sleep(8);
+    else if (spins < 16)
+        __builtin_amdgcn_s_sleep(24);
+    else
+        __builtin_amdgcn_s_sleep(64);
     return false;
 }
 
@@ -93,7 +101,8 @@ __device__ __forceinline__ unsigned long long now_ticks() { return __builtin_amd
 // T item: transform tile `xt` into the ring.
 template <typename T>
 __device__ __forceinline__ void pipe_transform(const PipeParams& P, __amdgpu_buffer_rsrc_t ring, uint32_t xt,
-                                               float* lds, int tid, unsigned long long* st) {
+                                               float* lds, int tid, unsigned long long* st, bool claim,
+                                               uint32_t& next) {
     const XTile td = P.xtiles[xt];
     const UnitDev& U = P.units[td.unit];
     const T* src = static_cast<const T*>(P.cells) + U.cell_off;
@@ -110,7 +119,7 @@ __device__ __forceinline__ void pipe_transform(const PipeParams& P, __amdgpu_buf
             const uint32_t i = i0 + lane;
             const bool need = i < U.wl_len;
             const uint32_t v = need ? P.waits[U.wl_off + i] : 0u;
-            const uint32_t want = need ? P.units[v].net : 0u;
+            const uint32_t want = need ? P.units[v].ewant : 0u;
             for (uint32_t spins = 0;;) {
                 const bool ok = !need || ld_rlx(P.edone + v) >= want;
                 if (__all(ok)) break;
@@ -131,9 +140,85 @@ __device__ __forceinline__ void pipe_transform(const PipeParams& P, __amdgpu_buf
     kmax = wave_max_u64(kmax);
     if (lane == 0 && kmax != 0)
         __hip_atomic_fetch_max(P.key + td.unit, kmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // claim the next item now: its round trip overlaps the store drain
+    if (claim && tid == 0) next = atomicAdd(P.ticket, 1u);
     drain();  // every storing wave: ring stores and the key atomic are complete
     __syncthreads();
     if (tid == 0) add_rlx(P.tdone + td.unit, 1u);
+}
+
+// Emit the kept coefficients of one 8192-coefficient chunk held in q (thread
+// (w, l) owns elements w*2048 + it*256 + 4l + j; kb bit it*4 + j = kept) as
+// (run, value) pairs: ranks from per-column ballots, run =
+// f - prev - 1.  rank / prev: this wave's first pair index and the unit-
+// relative flat index of the last kept coefficient before this wave's
+// elements (0xffffffff = none, so that run = f).  32-bit arithmetic: flat
+// indices are < 2^31.
+// Set bits of a 64-lane mask below this lane.
+__device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+template <class Val>
+__device__ __forceinline__ void emit_pairs(Val val, uint32_t kb, uint32_t start, int w, int l, uint32_t rank,
+                                           uint32_t prev, uint2* __restrict__ pairs) {
+    const unsigned long long lt = (1ull << l) - 1ull;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const uint32_t nib = (kb >> (it * 4)) & 0xfu;
+        const unsigned long long any = __ballot(nib != 0);
+        if (!any) continue;
+        // exclusive prefix of kept counts over lanes: one ballot per column j,
+        // counted below this lane with mbcnt (ballots live in SGPRs)
+        const unsigned long long b0 = __ballot(nib & 1u), b1 = __ballot(nib & 2u), b2 = __ballot(nib & 4u),
+                                 b3 = __ballot(nib & 8u);
+        const uint32_t pre = mbcnt64(b0) + mbcnt64(b1) + mbcnt64(b2) + mbcnt64(b3);
+        const uint32_t itot = (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+        const uint32_t ebase = start + (uint32_t)(w * 2048 + it * 256 + l * 4);
+        const uint32_t lane_last = ebase + (nib ? 31u - (uint32_t)__clz(nib) : 0u);
+        const unsigned long long below = any & lt;
+        const uint32_t from_lane = __shfl(lane_last, below ? 63 - __clzll(below) : l);
+        uint32_t p = below ? from_lane : prev;
+        uint32_t r = rank + pre;
+        if (nib) {
+            const float4 v4 = val(it);
+            const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (nib & (1u << j)) {
+                    const uint32_t f = ebase + (uint32_t)j;
+                    pairs[r] = make_uint2(f - p - 1u, __float_as_uint(vv[j]));
+                    p = f;
+                    ++r;
+                }
+            }
+        }
+        rank += itot;
+        prev = __shfl(lane_last, 63 - __clzll(any));
+    }
+}
+
+// Keep bits of a chunk: bit it*4 + j of element w*2048 + it*256 + 4l + j,
+// |c| > tf for elements below len (src/compressor.cpp:225-226).
+__device__ __forceinline__ uint32_t keep_bits(const float4 (&q)[8], float tf, uint32_t len, int w, int l) {
+    uint32_t kb = 0;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const float e[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t idx = (uint32_t)(w * 2048 + it * 256 + l * 4 + j);
+            kb |= (uint32_t)(idx < len && fabsf(e[j]) > tf) << (it * 4 + j);
+        }
+    }
+    return kb;
+}
+
+// Per-wave kept count and last kept (chunk-relative index + 1, 0 = none).
+__device__ __forceinline__ void wave_totals(uint32_t kb, int w, int l, uint32_t& cnt, uint32_t& last) {
+    cnt = wave_sum((uint32_t)__popc(kb));
+    const int hb = kb ? 31 - __clz(kb) : 0;
+    last = wave_max_u32(kb ? (uint32_t)(w * 2048 + (hb >> 2) * 256 + l * 4 + (hb & 3) + 1) : 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -180,26 +265,15 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
         for (int it = 0; it < 8; ++it) q[it] = ring_ld4(ring, base + 16u * (uint32_t)(w * 512 + it * 64 + l));
     } else {
         // flat scratch: 16-B aligned per unit, kFlatTile slack past the last unit
-        const float4* __restrict__ p4 = reinterpret_cast<const float4*>(coef + U.coef_off + start);
+        const float4* __restrict__ p4 =
+            reinterpret_cast<const float4*>(coef + (P.ring_coefs ? U.ring_off : U.coef_off) + start);
 #pragma unroll
         for (int it = 0; it < 8; ++it) q[it] = (uint32_t)(w * 2048 + it * 256 + 4 * l) < len ? p4[w * 512 + it * 64 + l]
                                                                                               : make_float4(0, 0, 0, 0);
     }
-    uint32_t kb = 0;
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        const float e[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t idx = (uint32_t)(w * 2048 + it * 256 + l * 4 + j);
-            kb |= (uint32_t)(idx < len && fabsf(e[j]) > tf) << (it * 4 + j);
-        }
-    }
-    // per-wave count and last kept (tile-relative index + 1)
-    const uint32_t wcnt = wave_sum((uint32_t)__popc(kb));
-    const int hb = kb ? 31 - __clz(kb) : 0;
-    const uint32_t mylast = kb ? (uint32_t)(w * 2048 + (hb >> 2) * 256 + l * 4 + (hb & 3) + 1) : 0u;
-    const uint32_t wlast = wave_max_u32(mylast);
+    const uint32_t kb = keep_bits(q, tf, len, w, l);
+    uint32_t wcnt, wlast;
+    wave_totals(kb, w, l, wcnt, wlast);
     if (l == 0) {
         sm[4 + w] = wcnt;
         sm[8 + w] = wlast;
@@ -216,7 +290,7 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
         }
         const uint32_t L1 = L ? start + L : 0u;  // unit-relative last kept + 1
         uint32_t ecnt = 0, elast = 0;            // exclusive: pairs before, last kept + 1 before
-        if (ft.index == 0) {
+        if (ft.index == 0 || (P.dbg & 2)) {
             if (l == 0) st_rlx(P.status + et, kFlagIncl | ((unsigned long long)C << 31) | L1);
         } else {
             if (l == 0) st_rlx(P.status + et, kFlagAgg | ((unsigned long long)C << 31) | L1);
@@ -282,40 +356,91 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
         if (sm[8 + i]) prev = start + sm[8 + i] - 1u;
     }
     uint2* __restrict__ pairs = reinterpret_cast<uint2*>(P.payload + U.pay_off + 20);
-    const unsigned long long lt = (1ull << l) - 1ull;
+    emit_pairs([&](int it) { return q[it]; }, kb, start, w, l, rank, prev, pairs);
+}
+
+// ---------------------------------------------------------------------------
+// E item, unit granularity: one workgroup thresholds and packs a whole unit,
+// streaming its ring region in kEmitTile chunks: a chunk's values are parked
+// in LDS (each thread its own elements) so the next chunk's loads are in
+// flight while this one is packed.  Pair offsets are a running sum (no
+// look-back); one dependency wait per unit.
+// sm: [0..1] key, [4..19] per-wave counts / lasts of two chunks (alternating,
+// so one barrier per chunk suffices); stash: 32 KB of LDS.
+__device__ __forceinline__ void ring_chunk(__amdgpu_buffer_rsrc_t ring, uint32_t rbase, uint32_t c, int w, int l,
+                                           float4 (&q)[8]) {
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-        const uint32_t nib = (kb >> (it * 4)) & 0xfu;
-        const unsigned long long any = __ballot(nib != 0);
-        if (!any) continue;
-        const uint32_t cnt = (uint32_t)__popc(nib);
-        // exclusive prefix of kept counts over lanes (wave scan of 0..4)
-        uint32_t incl = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(incl, o);
-            if (l >= o) incl += t;
+    for (int it = 0; it < 8; ++it)
+        q[it] = ring_ld4(ring, rbase + 4u * c * (uint32_t)kEmitTile + 16u * (uint32_t)(w * 512 + it * 64 + l));
+}
+
+__device__ __forceinline__ void pipe_emit_unit(const PipeParams& P, __amdgpu_buffer_rsrc_t ring, uint32_t u,
+                                               uint32_t* sm, float* stash, int tid, unsigned long long* st) {
+    const UnitDev& U = P.units[u];
+    const int w = tid >> 6, l = tid & 63;
+    unsigned long long* smk = reinterpret_cast<unsigned long long*>(sm);
+    if (tid == 0) {
+        const unsigned long long t0 = P.stats ? now_ticks() : 0;
+        for (uint32_t spins = 0;;) {
+            if (ld_rlx(P.tdone + u) >= U.ntx) break;
+            if (spin_fail(spins, P.err)) break;
         }
-        const uint32_t ebase = start + (uint32_t)(w * 2048 + it * 256 + l * 4);
-        const uint32_t lane_last = ebase + (nib ? 31u - (uint32_t)__clz(nib) : 0u);
-        const unsigned long long below = any & lt;
-        const uint32_t from_lane = __shfl(lane_last, below ? 63 - __clzll(below) : l);
-        uint32_t p = below ? from_lane : prev;
-        uint32_t r = rank + incl - cnt;
-        if (nib) {
-            const float vv[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
+        smk[0] = ld_rlx(P.key + u);
+        if (P.stats) st[kStEWait] += now_ticks() - t0;
+    }
+    __syncthreads();
+    const float tf = thresh_as_float(key_thresh(smk[0], P.keep));
+    const uint32_t nc = (uint32_t)U.ncells;
+    const uint32_t nch = (nc + kEmitTile - 1) / kEmitTile;
+    const uint32_t rbase = 4u * (uint32_t)U.ring_off;
+    uint2* __restrict__ pairs = reinterpret_cast<uint2*>(P.payload + U.pay_off + 20);
+    uint32_t rank = 0, prev = 0xffffffffu;
+    // This thread's stash slots (its own elements: no barrier needed).
+    float4* mine = reinterpret_cast<float4*>(stash) + w * 512 + l;
+    float4 q[8];
+    if (nch) ring_chunk(ring, rbase, 0, w, l, q);
+    for (uint32_t c = 0; c < nch; ++c) {
+        uint32_t* cs = sm + 4 + 8 * (c & 1u);  // alternating: one barrier per chunk
+        const uint32_t start = c * (uint32_t)kEmitTile;
+        const uint32_t len = min((uint32_t)kEmitTile, nc - start);
+        const uint32_t kb = keep_bits(q, tf, len, w, l);
+        uint32_t wc, wl;
+        wave_totals(kb, w, l, wc, wl);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (nib & (1u << j)) {
-                    const uint32_t f = ebase + (uint32_t)j;
-                    pairs[r] = make_uint2(f - p - 1u, __float_as_uint(vv[j]));
-                    p = f;
-                    ++r;
-                }
+        for (int it = 0; it < 8; ++it) mine[it * 64] = q[it];
+        if (c + 1 < nch) ring_chunk(ring, rbase, c + 1, w, l, q);  // in flight while this chunk is packed
+        if (l == 0) {
+            cs[w] = wc;
+            cs[4 + w] = wl;
+        }
+        __syncthreads();
+        uint32_t r = rank, pv = prev, tot = 0, cl = prev;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t ci = cs[i], li = cs[4 + i];
+            if (i < w) {
+                r += ci;
+                if (li) pv = start + li - 1u;
             }
+            tot += ci;
+            if (li) cl = start + li - 1u;
         }
-        rank += __shfl(incl, 63);
-        prev = __shfl(lane_last, 63 - __clzll(any));
+        emit_pairs([&](int it) { return mine[it * 64]; }, kb, start, w, l, r, pv, pairs);
+        rank += tot;
+        prev = cl;
+    }
+    __syncthreads();  // every ring load of the unit has been consumed
+    if (tid == 0) {
+        add_rlx(P.edone + u, 1u);
+        int32_t* hd = reinterpret_cast<int32_t*>(P.payload + U.pay_off);
+        hd[0] = U.nx;
+        hd[1] = U.ny;
+        hd[2] = U.nz;
+        hd[3] = (int32_t)U.ncells;
+        hd[4] = (int32_t)rank;
+        P.kept[u] = rank;
+        P.offsets[u] = U.pay_off;
+        if ((int)u == P.n - 1) P.offsets[P.n] = U.pay_off + 20 + 8ull * rank;
     }
 }
 
@@ -324,7 +449,7 @@ template <typename T>
 __global__ __launch_bounds__(kThreads, 4) void k_forward_pipe(PipeParams P) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     uint32_t* ctl = reinterpret_cast<uint32_t*>(lds);   // [0]: next batch; [2..17]: stats (tid 0)
-    uint32_t* sm = ctl + 18;                             // emit scratch (16 words)
+    uint32_t* sm = ctl + 18;                             // emit scratch (24 words)
     float* tl = lds + 48;                                // transform tile rows (192-B offset)
     const int tid = threadIdx.x;
     const __amdgpu_buffer_rsrc_t ring = __builtin_amdgcn_make_buffer_rsrc(P.ring, 0, (int)P.ring_bytes, 0x00020000);
@@ -340,18 +465,20 @@ __global__ __launch_bounds__(kThreads, 4) void k_forward_pipe(PipeParams P) {
     while (batch * K < P.nitems) {
         uint32_t next = 0;
         const uint32_t first = batch * K, last = min(first + K, P.nitems);
+        bool claimed = false;
         for (uint32_t item = first; item < last; ++item) {
             if (tid == 0 && P.prefetch && item + 1 == last) next = atomicAdd(P.ticket, 1u);
             const unsigned long long t0 = (P.stats && tid == 0) ? now_ticks() : 0;
             const uint32_t code = P.items[item];
             if (code & 0x80000000u) {
-                pipe_emit<true>(P, ring, nullptr, code & 0x7fffffffu, sm, tid, st);
+                pipe_emit_unit(P, ring, code & 0x3fffffffu, sm, tl, tid, st);
                 if (P.stats && tid == 0) {
                     st[kStE] += now_ticks() - t0;
                     st[kStNE] += 1;
                 }
             } else {
-                pipe_transform<T>(P, ring, code, tl, tid, st);
+                claimed = !P.prefetch && item + 1 == last;
+                pipe_transform<T>(P, ring, code, tl, tid, st, claimed, next);
                 if (P.stats && tid == 0) {
                     st[kStT] += now_ticks() - t0;
                     st[kStNT] += 1;
@@ -360,7 +487,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_forward_pipe(PipeParams P) {
         }
         if (tid == 0) {
             const unsigned long long t0 = P.stats ? now_ticks() : 0;
-            if (!P.prefetch) next = atomicAdd(P.ticket, 1u);
+            if (!P.prefetch && !claimed) next = atomicAdd(P.ticket, 1u);
             ctl[0] = next;
             if (P.stats) st[kStClaim] += now_ticks() - t0;
         }
@@ -381,8 +508,8 @@ __global__ __launch_bounds__(kThreads) void k_emit_lb(PipeParams P, const float*
     __shared__ __attribute__((aligned(16))) uint32_t sm[32];
     const int tid = threadIdx.x;
     if (tid == 0) {
-        const uint32_t u = P.etiles[blockIdx.x].unit;
-        sm[16] = P.units[u].et_begin + atomicAdd(P.tdone + u, 1u);
+        const uint32_t u = P.etiles[P.etile_base + blockIdx.x].unit;
+        sm[16] = (P.dbg & 1) ? blockIdx.x : P.units[u].et_begin + atomicAdd(P.tdone + u, 1u);
     }
     __syncthreads();
     const uint32_t et = __builtin_amdgcn_readfirstlane(sm[16]);
@@ -398,7 +525,7 @@ hipError_t launch_emit_lb(hipStream_t st, const PipeParams& p, const float* coef
     return hipGetLastError();
 }
 
-size_t pipe_lds_bytes(size_t tile_lds) { return 192 + tile_lds; }
+size_t pipe_lds_bytes(size_t tile_lds) { return 192 + (tile_lds > 4u * kEmitTile ? tile_lds : 4u * kEmitTile); }
 
 hipError_t launch_forward_pipe(hipStream_t st, int dtype, size_t lds, uint32_t grid, const PipeParams& p) {
     if (p.nitems == 0) return hipSuccess;
