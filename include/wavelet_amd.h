@@ -102,6 +102,9 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports kernel-side errors of earlier 
 #define WC_OPT_CHUNK 8          /* staged forward over chunks of this many cells, transform of
                                    chunk c+1 overlapping emit of chunk c (0 = whole batch) */
 #define WC_OPT_CHUNK_SLOTS 9    /* coefficient slots of the chunked forward (default 3) */
+#define WC_OPT_EMIT_SEG_MAX 10  /* staged emit: units of at most this many 8192-coefficient tiles are packed
+                                   whole by one workgroup each, no look-back (default 64; 0 = never) */
+#define WC_OPT_EMIT_SEG_MIN_UNITS 11 /* ... when the batch holds at least this many of them (default 256) */
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 
 /* Diagnostics of the pipelined kernel (WC_OPT_PIPE_STATS on): summed over
@@ -163,7 +166,7 @@ int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* 
 #define WC_STAGE_COUNT 1      /* unused since the look-back emit (kept for numbering) */
 #define WC_STAGE_SCAN 2       /* unused */
 #define WC_STAGE_OFFSETS 3    /* unused */
-#define WC_STAGE_EMIT 4       /* K2  threshold + look-back + pack (k_emit_lb) */
+#define WC_STAGE_EMIT 4       /* K2  threshold + ordered pack (k_emit) */
 #define WC_STAGE_DECODE 5     /* K5a-c */
 #define WC_STAGE_INVERSE 6    /* K6  */
 #define WC_STAGE_RMSE 7       /* K7  */

@@ -35,13 +35,20 @@ def pack(wc, boxes, dtype=np.float64, offsets=None):
     return units, n, extent, cells
 
 
-def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None, pipe=True, lag=0, ring=0):
+def set_path(ctx, path, lag=0, ring=0):
+    """Forward-path options (library defaults: staged, whole-unit emit when >= 256 units)."""
+    ctx.set_pipe(path == "pipe", lag=lag, ring=ring)
+    ctx.set_chunk(16384 if path == "chunked" else 0, slots=2)
+    ctx.set_emit_seg(0 if path == "lookback" else 64, 1 if path == "seg" else 256)
+
+
+def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None, path="staged", lag=0, ring=0):
     units, n, extent, cells = pack(wc, boxes, dtype, offsets)
-    ctx.set_pipe(pipe, lag=lag, ring=ring)
+    set_path(ctx, path, lag, ring)
     try:
         payload, offs, kept = ctx.forward_host(cells, units, n, keep)
     finally:
-        ctx.set_pipe(False)  # library default
+        set_path(ctx, "staged")  # library defaults
     return [wc.capi.unit_payload(payload, offs, kept, i) for i in range(n)], kept
 
 
@@ -50,36 +57,40 @@ def oracle_payload(O, b, keep):
     return O.compress_payload(b32, keep)[0]
 
 
-PATHS = [pytest.param(True, id="pipe"), pytest.param(False, id="staged")]
+# Forward paths, all byte-identical: the library default; every unit through
+# look-back emit tiles; whole-unit emit forced (units of <= 64 tiles) beside
+# look-back tiles for larger units in the same launch; chunked two-stream
+# (16 Ki-cell chunks, 2 coefficient slots); the pipelined single launch.
+PATHS = ["staged", "lookback", "seg", "chunked", "pipe"]
 
 
-@pytest.mark.parametrize("pipe", PATHS)
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("keep", KEEPS)
-def test_forward_payload_bit_exact_fp64(wc, ctx, oracle, keep, pipe):
+def test_forward_payload_bit_exact_fp64(wc, ctx, oracle, keep, path):
     boxes = synth(oracle, DIMS)
-    got, kept = gpu_payloads(wc, ctx, boxes, keep, pipe=pipe)
+    got, kept = gpu_payloads(wc, ctx, boxes, keep, path=path)
     for i, b in enumerate(boxes):
         want = oracle_payload(oracle, b, keep)
         assert got[i] == want, f"unit {i} dims {DIMS[i]} keep {keep}"
 
 
-@pytest.mark.parametrize("pipe", PATHS)
-def test_forward_payload_bit_exact_fp32_input(wc, ctx, oracle, pipe):
+@pytest.mark.parametrize("path", PATHS)
+def test_forward_payload_bit_exact_fp32_input(wc, ctx, oracle, path):
     keep = KEEPS[1]
     boxes = [oracle.narrow(b) for b in synth(oracle, DIMS, seed0=1)]
-    got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, pipe=pipe)
+    got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, path=path)
     for i, b in enumerate(boxes):
         assert got[i] == oracle.compress_payload(b, keep)[0], f"unit {i} dims {DIMS[i]}"
 
 
-@pytest.mark.parametrize("pipe", PATHS)
-def test_unaligned_offsets(wc, ctx, oracle, pipe):
+@pytest.mark.parametrize("path", PATHS)
+def test_unaligned_offsets(wc, ctx, oracle, path):
     """Odd cell offsets disable the vector loads; results must not change."""
     keep = KEEPS[1]
     dims = [(8, 8, 8), (6, 4, 2), (16, 2, 4), (4, 4, 16)]
     boxes = synth(oracle, dims, seed0=2)
     offs = [1, 1 + 512 + 3, 1 + 512 + 3 + 48 + 5, 1 + 512 + 3 + 48 + 5 + 128 + 7]
-    got, _ = gpu_payloads(wc, ctx, boxes, keep, offsets=offs, pipe=pipe)
+    got, _ = gpu_payloads(wc, ctx, boxes, keep, offsets=offs, path=path)
     for i, b in enumerate(boxes):
         assert got[i] == oracle_payload(oracle, b, keep)
 
@@ -168,12 +179,12 @@ def special_boxes():
     return out
 
 
-@pytest.mark.parametrize("pipe", PATHS)
-def test_special_boxes(wc, ctx, oracle, pipe):
+@pytest.mark.parametrize("path", PATHS)
+def test_special_boxes(wc, ctx, oracle, path):
     keep = KEEPS[1]
     sp = special_boxes()
     names = list(sp)
-    got, kept = gpu_payloads(wc, ctx, [sp[k][0] for k in names], keep, dtype=np.float32, pipe=pipe)
+    got, kept = gpu_payloads(wc, ctx, [sp[k][0] for k in names], keep, dtype=np.float32, path=path)
     for i, k in enumerate(names):
         b, expect_kept = sp[k]
         want, wk = oracle.compress_payload(b, keep)
@@ -281,28 +292,28 @@ def test_rle_decode_out_of_range_pairs_dropped(wc, ctx, oracle):
     assert out.tobytes() == want.tobytes()
 
 
-@pytest.mark.parametrize("pipe", PATHS)
-def test_large_batch_64cubed_fp64(wc, ctx, oracle, pipe):
+@pytest.mark.parametrize("path", PATHS)
+def test_large_batch_64cubed_fp64(wc, ctx, oracle, path):
     """64 boxes of the headline shape (64^3 fp64, keep 0.999f): every payload byte."""
     keep = KEEPS[1]
     dims = [(64, 64, 64)] * 64
     boxes = [oracle.synth_box_f64(oracle.unit_seed(0, 0, i, 0), (64 * (i % 8), 64 * (i // 8), 0), 64, 64, 64)
              for i in range(64)]
-    got, kept = gpu_payloads(wc, ctx, boxes, keep, pipe=pipe)
+    got, kept = gpu_payloads(wc, ctx, boxes, keep, path=path)
     frac = kept.sum() / (64 * 64 ** 3)
     assert 0.05 < frac < 0.95
     for i, b in enumerate(boxes):
         assert got[i] == oracle_payload(oracle, b, keep), i
 
 
-@pytest.mark.parametrize("pipe", PATHS)
-def test_128cubed_fp32_and_mixed_sizes(wc, ctx, oracle, pipe):
+@pytest.mark.parametrize("path", PATHS)
+def test_128cubed_fp32_and_mixed_sizes(wc, ctx, oracle, path):
     """C5 shape (128^3 fp32, keep 0.9999f: z split over tiles) beside fast-transform and
     other AMR-style mixed boxes in one batch."""
     keep = KEEPS[2]
     dims = [(128, 128, 128), (32, 32, 32), (16, 16, 16), (48, 32, 16), (64, 64, 64), (128, 64, 32)]
     boxes = [oracle.narrow(b) for b in synth(oracle, dims, seed0=8)]
-    got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, pipe=pipe)
+    got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, path=path)
     for i, b in enumerate(boxes):
         assert got[i] == oracle.compress_payload(b, keep)[0], dims[i]
 
@@ -318,9 +329,44 @@ def test_pipe_ring_reuse_and_waits(wc, ctx, oracle, lag, ring):
     dims = [(16, 16, 16), (32, 32, 32), (3, 5, 7), (64, 64, 64), (0, 4, 4), (48, 32, 16), (16, 16, 16),
             (33, 17, 9), (64, 64, 64), (8, 4, 2), (32, 32, 32), (2, 200, 3)] * 3
     boxes = synth(oracle, dims, seed0=11)
-    got, kept = gpu_payloads(wc, ctx, boxes, keep, pipe=True, lag=lag, ring=ring)
+    got, kept = gpu_payloads(wc, ctx, boxes, keep, path="pipe", lag=lag, ring=ring)
     for i, b in enumerate(boxes):
         assert got[i] == oracle_payload(oracle, b, keep), (i, dims[i])
+
+
+@pytest.mark.parametrize("chunk,slots", [(4096, 2), (100_000, 3), (1 << 20, 2)])
+def test_chunked_slot_reuse(wc, ctx, oracle, chunk, slots):
+    """Chunked forward: a coefficient slot is rewritten only after the emit that read it;
+    chunks smaller than one unit, mixed shapes, odd dims and an empty unit."""
+    keep = KEEPS[1]
+    dims = [(16, 16, 16), (32, 32, 32), (3, 5, 7), (64, 64, 64), (0, 4, 4), (48, 32, 16), (33, 17, 9),
+            (64, 64, 64), (8, 4, 2), (2, 200, 3)] * 2
+    boxes = synth(oracle, dims, seed0=13)
+    units, n, extent, cells = pack(wc, boxes)
+    ctx.set_chunk(chunk, slots)
+    try:
+        payload, offs, kept = ctx.forward_host(cells, units, n, keep)
+    finally:
+        ctx.set_chunk(0)
+    for i, b in enumerate(boxes):
+        assert wc.capi.unit_payload(payload, offs, kept, i) == oracle_payload(oracle, b, keep), (i, dims[i])
+
+
+def test_whole_unit_emit_beside_lookback_tiles(wc, ctx, oracle):
+    """One k_emit launch: units of <= 2 emit tiles packed whole by one workgroup, the larger
+    ones through look-back tiles; empty and single-cell units among them."""
+    keep = KEEPS[0]
+    dims = [(16, 16, 16), (32, 32, 32), (0, 3, 3), (40, 40, 70), (1, 1, 1), (64, 64, 64), (6, 10, 14),
+            (128, 16, 8), (2, 2, 2)]
+    boxes = synth(oracle, dims, seed0=14)
+    units, n, extent, cells = pack(wc, boxes)
+    ctx.set_emit_seg(2, 1)
+    try:
+        payload, offs, kept = ctx.forward_host(cells, units, n, keep)
+    finally:
+        ctx.set_emit_seg()
+    for i, b in enumerate(boxes):
+        assert wc.capi.unit_payload(payload, offs, kept, i) == oracle_payload(oracle, b, keep), (i, dims[i])
 
 
 def test_pipe_stats_counters(wc, ctx, oracle):
@@ -368,8 +414,8 @@ def test_reference_calc_rmse_case(wc):
     assert wc.calc_rmse_per_box(a, p, 2) == [3.5, 3.5]
 
 
-@pytest.mark.parametrize("pipe", PATHS)
-def test_gpu_matches_committed_golden_fixtures(wc, ctx, pipe):
+@pytest.mark.parametrize("path", PATHS)
+def test_gpu_matches_committed_golden_fixtures(wc, ctx, path):
     """Stored vectors (tests/golden/codec_golden.npz): payload bytes and reconstructions."""
     import json
     from pathlib import Path
@@ -381,7 +427,7 @@ def test_gpu_matches_committed_golden_fixtures(wc, ctx, pipe):
         by_keep.setdefault(case["keep"], []).append(case)
     for keep, cases in by_keep.items():
         boxes = [z[c["box"]] for c in cases]
-        got, kept = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, pipe=pipe)
+        got, kept = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, path=path)
         for i, c in enumerate(cases):
             assert got[i] == z[c["name"] + "/payload"].tobytes(), c["name"]
             assert int(kept[i]) == c["kept"], c["name"]

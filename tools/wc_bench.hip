@@ -6,9 +6,10 @@
 //
 // usage: wc_bench [boxes=1024] [dim=64] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1]
 //                 [pipe=1|0] [check=0|1] [lag=0] [ring=0] [claim=1] [prefetch=0] [wgs=0] [stats=0]
-//                 [chunk=0] [slots=3]
-// check=1: also run the staged path once and compare every unit's payload
-// bytes with the pipelined path's ("paths_identical" in the JSON line).
+//                 [chunk=0] [slots=3] [seg=64] [segmin=256]
+// check=1: also run the plain staged path (look-back emit only) once and
+// compare every unit's payload bytes with the configured path's
+// ("paths_identical" in the JSON line).
 // lag / ring: WC_OPT_PIPE_LAG / WC_OPT_PIPE_RING (0 = library defaults).
 #include <hip/hip_runtime.h>
 
@@ -62,7 +63,7 @@ int main(int argc, char** argv) {
     const int steps = argc > 5 ? std::atoi(argv[5]) : 10;
     const int warmup = argc > 6 ? std::atoi(argv[6]) : 2;
     const bool inverse = argc > 7 ? std::atoi(argv[7]) != 0 : false;
-    const bool pipe = argc > 8 ? std::atoi(argv[8]) != 0 : true;  // library default
+    const bool pipe = argc > 8 ? std::atoi(argv[8]) != 0 : false;  // library default: staged
     const bool check = argc > 9 ? std::atoi(argv[9]) != 0 : false;
     const long long lag = argc > 10 ? std::atoll(argv[10]) : 0;
     const long long ring = argc > 11 ? std::atoll(argv[11]) : 0;
@@ -72,6 +73,8 @@ int main(int argc, char** argv) {
     const int stats = argc > 15 ? std::atoi(argv[15]) : 0;
     const long long chunk = argc > 16 ? std::atoll(argv[16]) : 0;
     const int slots = argc > 17 ? std::atoi(argv[17]) : 3;
+    const int seg = argc > 18 ? std::atoi(argv[18]) : 64;
+    const int segmin = argc > 19 ? std::atoi(argv[19]) : 256;
 
     std::vector<wc_unit> units(boxes);
     const unsigned long long per = (unsigned long long)dim * dim * dim;
@@ -108,6 +111,8 @@ int main(int argc, char** argv) {
     wc_set_option(ctx, WC_OPT_PIPE_WGS, wgs);
     wc_set_option(ctx, WC_OPT_CHUNK, chunk);
     wc_set_option(ctx, WC_OPT_CHUNK_SLOTS, slots);
+    wc_set_option(ctx, WC_OPT_EMIT_SEG_MAX, seg);
+    wc_set_option(ctx, WC_OPT_EMIT_SEG_MIN_UNITS, segmin);
     auto fwd = [&]() {
         int rc = wc_forward(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, keep, payload, cap, offsets, kept);
         if (rc != WC_OK) {
@@ -167,6 +172,7 @@ int main(int argc, char** argv) {
         CK(hipMemset(payload, 0xA5, cap));
         wc_set_option(ctx, WC_OPT_PIPE, 0);
         wc_set_option(ctx, WC_OPT_CHUNK, 0);
+        wc_set_option(ctx, WC_OPT_EMIT_SEG_MAX, 0);
         fwd();
         wc_synchronize(ctx);
         CK(hipMemcpy(off_b.data(), offsets, 8 * (boxes + 1), hipMemcpyDeviceToHost));
@@ -179,6 +185,7 @@ int main(int argc, char** argv) {
         }
         wc_set_option(ctx, WC_OPT_PIPE, pipe ? 1 : 0);
         wc_set_option(ctx, WC_OPT_CHUNK, chunk);
+        wc_set_option(ctx, WC_OPT_EMIT_SEG_MAX, seg);
     }
     uint64_t total = 0;
     CK(hipMemcpy(&total, offsets + boxes, 8, hipMemcpyDeviceToHost));
@@ -190,9 +197,10 @@ int main(int argc, char** argv) {
                                         "flat_emit", "decode", "inverse", "rmse", "pipe", "chunked"};
     std::printf("{\"boxes\": %d, \"dim\": %d, \"dtype\": \"%s\", \"keep\": %.17g, \"steps\": %d, "
                 "\"ms_per_step\": %.4f, \"cells_per_s\": %.6e, \"kept_fraction\": %.6f, \"payload_bytes\": %llu, "
-                "\"pipe\": %d, \"lag\": %lld, \"ring\": %lld, \"paths_identical\": %d, \"stage_ms\": {",
+                "\"pipe\": %d, \"lag\": %lld, \"ring\": %lld, \"chunk\": %lld, \"slots\": %d, \"seg\": %d, "
+                "\"paths_identical\": %d, \"stage_ms\": {",
                 boxes, dim, f64 ? "f64" : "f32", keep, steps, step_ms, per * boxes / (step_ms * 1e-3),
-                ksum / (double)(per * boxes), (unsigned long long)total, pipe ? 1 : 0, lag, ring, identical);
+                ksum / (double)(per * boxes), (unsigned long long)total, pipe ? 1 : 0, lag, ring, chunk, slots, seg, identical);
     bool first = true;
     for (int s = 0; s < WC_NUM_STAGES; ++s)
         if (cnt[s]) {

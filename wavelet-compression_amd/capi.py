@@ -32,6 +32,7 @@ EXPORTED = (
 WC_OPT_PIPE, WC_OPT_PIPE_LAG, WC_OPT_PIPE_RING = 1, 2, 3
 WC_OPT_PIPE_CLAIM, WC_OPT_PIPE_PREFETCH, WC_OPT_PIPE_WGS, WC_OPT_PIPE_STATS = 4, 5, 6, 7
 WC_OPT_CHUNK, WC_OPT_CHUNK_SLOTS = 8, 9
+WC_OPT_EMIT_SEG_MAX, WC_OPT_EMIT_SEG_MIN_UNITS = 10, 11
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*), kernel names as rocprof shows them.
 STAGES = ("transform", "flat_count", "unit_scan", "unit_offsets", "flat_emit", "decode", "inverse", "rmse",
@@ -188,6 +189,18 @@ class Context:
         self.set_option(WC_OPT_PIPE, 1 if on else 0)
         self.set_option(WC_OPT_PIPE_LAG, lag)
         self.set_option(WC_OPT_PIPE_RING, ring)
+
+    def set_chunk(self, cells: int, slots: int = 3):
+        """Chunked forward: the transform of chunk c+1 overlaps the emit of chunk c on a
+        second stream (cells per chunk; 0 = the whole batch at once)."""
+        self.set_option(WC_OPT_CHUNK, cells)
+        self.set_option(WC_OPT_CHUNK_SLOTS, slots)
+
+    def set_emit_seg(self, max_tiles: int = 64, min_units: int = 256):
+        """Staged emit: units of <= max_tiles 8192-coefficient tiles packed whole by one
+        workgroup when the batch holds >= min_units of them (max_tiles 0: never)."""
+        self.set_option(WC_OPT_EMIT_SEG_MAX, max_tiles)
+        self.set_option(WC_OPT_EMIT_SEG_MIN_UNITS, min_units)
 
     def pipe_stats(self) -> list:
         """wc_pipe_stats: pipelined-kernel diagnostics since the last read (8 counters)."""

@@ -7,8 +7,10 @@
 //
 // Forward path per batch (wc_forward), every unit shape:
 //   WC_OPT_PIPE = 0 (default): staged kernels: k_transform{,_fast} -> flat
-//       coefficients in HBM scratch -> k_emit_lb (threshold + decoupled
-//       look-back + pack)
+//       coefficients in HBM scratch -> k_emit (threshold + ordered pack:
+//       whole units per workgroup, or emit tiles with decoupled look-back);
+//       WC_OPT_CHUNK > 0 cuts the batch into chunks whose transform and emit
+//       launches overlap on two streams
 //   WC_OPT_PIPE = 1: k_forward_pipe, one persistent launch: transform
 //       tiles -> coefficient ring (Infinity-Cache resident) -> emit tiles
 //       (threshold + decoupled look-back + pack), interleaved by a host-built
@@ -41,7 +43,7 @@ hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const 
 hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDev*, int, const FTile*,
                        uint32_t, double*, double*);
 hipError_t launch_forward_pipe(hipStream_t, int, size_t, uint32_t, const PipeParams&);
-hipError_t launch_emit_lb(hipStream_t, const PipeParams&, const float*, uint32_t);
+hipError_t launch_emit(hipStream_t, const PipeParams&, const float*, uint32_t, uint32_t);
 }  // namespace wc
 
 using namespace wc;
@@ -67,7 +69,8 @@ struct Plan {
     std::vector<UnitDev> units;
     std::vector<XTile> xtiles;
     std::vector<FTile> ftiles, etiles;
-    std::vector<uint32_t> items, waits;
+    std::vector<uint32_t> items, waits, segs;
+    int seg_max = 0, seg_min = 0;  // whole-unit emit: WC_OPT_EMIT_SEG_MAX / _MIN_UNITS
     uint32_t ngen = 0, nfast = 0;
     uint64_t coef_extent = 0;  // floats of staged coefficient scratch
     uint64_t ring_floats = 0;  // pipe coefficient ring
@@ -78,13 +81,14 @@ struct Plan {
         uint32_t u0, u1;            // units [u0, u1)
         uint32_t gen_b, gen_n;      // generic transform tiles
         uint32_t fast_b, fast_n;    // fast transform tiles
-        uint32_t et_b, et_n;        // emit tiles
+        uint32_t et_b, et_n;        // look-back emit tiles
+        uint32_t seg_b, seg_n;      // whole-unit emit entries
     };
     int64_t chunk_req = 0;
     std::vector<Chunk> chunks;
     uint64_t slot_floats = 0;
     int nslots = 0;
-    DevBuf d_units, d_xtiles, d_ftiles, d_etiles, d_items, d_waits;
+    DevBuf d_units, d_xtiles, d_ftiles, d_etiles, d_items, d_waits, d_segs;
 };
 
 int ceil_log2(int64_t v) {
@@ -111,6 +115,8 @@ struct wc_ctx {
     bool opt_stats = false;  // WC_OPT_PIPE_STATS
     int64_t opt_chunk = 0;   // WC_OPT_CHUNK: cells per chunk (0 = whole batch at once)
     int opt_slots = 3;       // WC_OPT_CHUNK_SLOTS
+    int opt_seg_max = 64;    // WC_OPT_EMIT_SEG_MAX
+    int opt_seg_min = 256;   // WC_OPT_EMIT_SEG_MIN_UNITS
     hipStream_t side = nullptr;        // second stream of the chunked forward (emit launches)
     std::vector<hipEvent_t> chunk_ev;  // 2 per chunk + 1
     bool err_check_pending = false;
@@ -230,15 +236,31 @@ constexpr int64_t kDefaultRingExtra = int64_t(8) << 20;  // ring floats beyond t
 
 uint64_t round_up(uint64_t v, uint64_t m) { return (v + m - 1) / m * m; }
 
-// Pipelined forward: emit tiles, coefficient ring with wait lists, work list.
-// Emit tiles (both forward paths): kEmitTile flat coefficients each, at
-// least one per unit (an empty unit's tile writes its header).
+// Emit work of the staged paths.  Units of at most seg_max emit tiles are
+// packed whole, one workgroup each (segs), when the batch holds at least
+// seg_min of them (enough workgroups to fill the device) and is not cut into
+// chunks; every other unit is split into emit tiles of kEmitTile flat
+// coefficients packed with decoupled look-back (at least one per unit: an
+// empty unit's tile writes its header).
 void build_etiles(Plan& P, int n) {
     P.etiles.clear();
+    P.segs.clear();
+    auto tiles_of = [](const UnitDev& d) {
+        return (uint32_t)std::max<uint64_t>(1, (d.ncells + kEmitTile - 1) / kEmitTile);
+    };
+    int eligible = 0;
+    if (P.seg_max > 0 && !P.pipe && P.chunk_req == 0)
+        for (int i = 0; i < n; ++i) eligible += tiles_of(P.units[i]) <= (uint32_t)P.seg_max;
+    const bool seg = eligible > 0 && eligible >= P.seg_min;
     for (int i = 0; i < n; ++i) {
         UnitDev& d = P.units[i];
         d.et_begin = (uint32_t)P.etiles.size();
-        d.net = (uint32_t)std::max<uint64_t>(1, (d.ncells + kEmitTile - 1) / kEmitTile);
+        d.net = tiles_of(d);
+        if (seg && d.net <= (uint32_t)P.seg_max) {
+            d.net = 0;
+            P.segs.push_back((uint32_t)i);
+            continue;
+        }
         for (uint32_t t = 0; t < d.net; ++t) P.etiles.push_back(FTile{(uint32_t)i, t});
     }
     P.state_bytes = round_up(16 + 16ull * n + 8ull * P.etiles.size(), 16);
@@ -357,6 +379,8 @@ void build_chunks(Plan& P, int n) {
             ++u;
         } while (u < n && fl + P.units[u].ncells <= (uint64_t)P.chunk_req);
         ch.u1 = (uint32_t)u;
+        ch.seg_b = (uint32_t)(std::lower_bound(P.segs.begin(), P.segs.end(), ch.u0) - P.segs.begin());
+        ch.seg_n = (uint32_t)(std::lower_bound(P.segs.begin(), P.segs.end(), ch.u1) - P.segs.begin()) - ch.seg_b;
         ch.gen_n = gcur - ch.gen_b;
         ch.fast_n = fcur - ch.fast_b;
         slot = std::max(slot, fl);
@@ -374,6 +398,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     Plan& P = c->plan;
     if (c->plan_valid && P.pipe == c->opt_pipe && P.lag == c->opt_lag && P.ring_req == c->opt_ring &&
         P.chunk_req == c->opt_chunk && P.nslots == (c->opt_chunk ? c->opt_slots : 0) &&
+        P.seg_max == c->opt_seg_max && P.seg_min == c->opt_seg_min &&
         (int)P.key.size() == n && (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0))
         return WC_OK;
     c->plan_valid = false;
@@ -385,6 +410,8 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     P.ring_req = c->opt_ring;
     P.chunk_req = c->opt_chunk;
     P.nslots = c->opt_chunk ? c->opt_slots : 0;
+    P.seg_max = c->opt_seg_max;
+    P.seg_min = c->opt_seg_min;
     P.chunks.clear();
     P.units.assign(n, UnitDev{});
     P.xtiles.clear();
@@ -451,7 +478,8 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         (rc = upload(c, P.d_ftiles, P.ftiles.data(), sizeof(FTile) * P.ftiles.size(), "upload ftiles")) ||
         (rc = upload(c, P.d_etiles, P.etiles.data(), sizeof(FTile) * P.etiles.size(), "upload etiles")) ||
         (rc = upload(c, P.d_items, P.items.data(), sizeof(uint32_t) * P.items.size(), "upload items")) ||
-        (rc = upload(c, P.d_waits, P.waits.data(), sizeof(uint32_t) * P.waits.size(), "upload waits")))
+        (rc = upload(c, P.d_waits, P.waits.data(), sizeof(uint32_t) * P.waits.size(), "upload waits")) ||
+        (rc = upload(c, P.d_segs, P.segs.data(), sizeof(uint32_t) * P.segs.size(), "upload segs")))
         return rc;
     // The host vectors back the async copies: finish them before returning.
     hipError_t e = hipStreamSynchronize(c->stream);
@@ -530,8 +558,7 @@ PipeParams pipe_params(wc_ctx* c, const void* d_cells, int n, double keep, uint8
     p.err = (uint32_t*)c->errflag.p;
     p.keep = keep;
     p.claim = 1;
-    const char* dbg = std::getenv("WCAMD_DBG");
-    p.dbg = dbg ? (uint32_t)std::atoi(dbg) : 0u;
+    p.segs = (const uint32_t*)P.d_segs.p;
     return p;
 }
 
@@ -582,7 +609,7 @@ int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep
     if (e != hipSuccess) return hip_fail(c, e, "transform launch");
     {
         StageTimer t(c, WC_STAGE_EMIT);
-        e = launch_emit_lb(c->stream, p, coef, (uint32_t)P.etiles.size());
+        e = launch_emit(c->stream, p, coef, (uint32_t)P.segs.size(), (uint32_t)P.etiles.size());
     }
     if (e != hipSuccess) return hip_fail(c, e, "emit launch");
     return WC_OK;
@@ -628,8 +655,9 @@ int forward_chunked(wc_ctx* c, const void* d_cells, int dtype, int n, double kee
         if ((e = hipEventRecord(ev_t[k], c->stream)) != hipSuccess ||
             (e = hipStreamWaitEvent(c->side, ev_t[k], 0)) != hipSuccess)
             return hip_fail(c, e, "chunk event");
+        p.seg_base = ch.seg_b;
         p.etile_base = ch.et_b;
-        if ((e = launch_emit_lb(c->side, p, ring, ch.et_n)) != hipSuccess) return hip_fail(c, e, "emit launch");
+        if ((e = launch_emit(c->side, p, ring, ch.seg_n, ch.et_n)) != hipSuccess) return hip_fail(c, e, "emit launch");
         if ((e = hipEventRecord(ev_e[k], c->side)) != hipSuccess) return hip_fail(c, e, "chunk event");
     }
     if ((e = hipStreamWaitEvent(c->stream, ev_e[P.chunks.size() - 1], 0)) != hipSuccess)
@@ -688,7 +716,7 @@ void wc_ctx_destroy(wc_ctx* c) {
                       &c->ring,      &c->state,     &c->stats,      &c->h_cells,    &c->h_payload,
                       &c->h_packed,  &c->h_offsets, &c->h_poff,    &c->h_kept,     &c->h_out,
                       &c->plan.d_units, &c->plan.d_xtiles, &c->plan.d_ftiles, &c->plan.d_etiles,
-                      &c->plan.d_items, &c->plan.d_waits};
+                      &c->plan.d_items, &c->plan.d_waits, &c->plan.d_segs};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& m : c->marks) {
@@ -745,6 +773,14 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
         case WC_OPT_CHUNK_SLOTS:
             if (value < 2 || value > 16) return fail(c, WC_ERR_INVALID, "chunk slots must be 2..16");
             c->opt_slots = (int)value;
+            return WC_OK;
+        case WC_OPT_EMIT_SEG_MAX:
+            if (value < 0 || value > 65536) return fail(c, WC_ERR_INVALID, "seg max tiles must be 0..65536");
+            c->opt_seg_max = (int)value;
+            return WC_OK;
+        case WC_OPT_EMIT_SEG_MIN_UNITS:
+            if (value < 1 || value > (int64_t(1) << 30)) return fail(c, WC_ERR_INVALID, "seg min units must be >= 1");
+            c->opt_seg_min = (int)value;
             return WC_OK;
         case WC_OPT_PIPE_STATS:
             c->opt_stats = value != 0;

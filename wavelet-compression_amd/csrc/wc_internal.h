@@ -35,7 +35,7 @@ struct UnitDev {
     uint64_t ring_off;      // element offset of the unit's coefficients in the ring (chunk aligned)
     uint32_t ntx;           // transform tiles of the unit
     uint32_t et_begin;      // first emit tile (kEmitTile coefficients) of the unit
-    uint32_t net;           // emit tiles = max(1, ceil(ncells / kEmitTile))
+    uint32_t net;           // look-back emit tiles = max(1, ceil(ncells / kEmitTile)); 0 = packed whole
     uint32_t wl_off;        // ring wait list: units whose emit tiles must finish before
     uint32_t wl_len;        //   this unit's transform tiles overwrite their ring chunks
     uint32_t xt_begin;      // first transform tile of the unit in the plan's tile list
@@ -108,9 +108,10 @@ struct PipeParams {
     uint32_t* kept;                // [n]
     uint32_t* err;
     double keep;
-    uint32_t dbg;                  // experiment switches (WCAMD_DBG), 0 in production
-    uint32_t etile_base;           // k_emit_lb: first emit tile of this launch
-    uint32_t ring_coefs;           // k_emit_lb: 1 = coefficients at ring_off (chunk slots), 0 = coef_off
+    const uint32_t* segs;          // k_emit: units packed whole, one workgroup each
+    uint32_t seg_base;             // k_emit: first entry of segs in this launch
+    uint32_t etile_base;           // k_emit: first look-back emit tile of this launch
+    uint32_t ring_coefs;           // k_emit: 1 = coefficients at ring_off (chunk slots), 0 = coef_off
 };
 
 }  // namespace wc

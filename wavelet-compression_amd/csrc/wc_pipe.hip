@@ -221,6 +221,20 @@ __device__ __forceinline__ void wave_totals(uint32_t kb, int w, int l, uint32_t&
     last = wave_max_u32(kb ? (uint32_t)(w * 2048 + (hb >> 2) * 256 + l * 4 + (hb & 3) + 1) : 0u);
 }
 
+// Unit u's header (src/compressor.cpp:55-80: int32 W, H, D, ncoeff, nrle),
+// kept count and payload offset, once its pair count is known.
+__device__ __forceinline__ void finish_unit(const PipeParams& P, const UnitDev& U, uint32_t u, uint32_t total) {
+    int32_t* hd = reinterpret_cast<int32_t*>(P.payload + U.pay_off);
+    hd[0] = U.nx;
+    hd[1] = U.ny;
+    hd[2] = U.nz;
+    hd[3] = (int32_t)U.ncells;
+    hd[4] = (int32_t)total;
+    P.kept[u] = total;
+    P.offsets[u] = U.pay_off;
+    if ((int)u == P.n - 1) P.offsets[P.n] = U.pay_off + 20 + 8ull * total;
+}
+
 // ---------------------------------------------------------------------------
 // E item: threshold + ordered pack of emit tile `et`.
 // Thread t = (wave w, lane l) owns elements w*2048 + it*256 + 4l + j, it 0..7.
@@ -290,7 +304,7 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
         }
         const uint32_t L1 = L ? start + L : 0u;  // unit-relative last kept + 1
         uint32_t ecnt = 0, elast = 0;            // exclusive: pairs before, last kept + 1 before
-        if (ft.index == 0 || (P.dbg & 2)) {
+        if (ft.index == 0) {
             if (l == 0) st_rlx(P.status + et, kFlagIncl | ((unsigned long long)C << 31) | L1);
         } else {
             if (l == 0) st_rlx(P.status + et, kFlagAgg | ((unsigned long long)C << 31) | L1);
@@ -330,18 +344,7 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
             sm[1] = elast;
             // ring reads of this tile are done (all waves passed the barrier above)
             if constexpr (RING) add_rlx(P.edone + u, 1u);
-            if (ft.index + 1 == U.net) {  // last tile: header + kept + slot offset
-                const uint32_t total = ecnt + C;
-                int32_t* hd = reinterpret_cast<int32_t*>(P.payload + U.pay_off);
-                hd[0] = U.nx;
-                hd[1] = U.ny;
-                hd[2] = U.nz;
-                hd[3] = (int32_t)U.ncells;
-                hd[4] = (int32_t)total;
-                P.kept[u] = total;
-                P.offsets[u] = U.pay_off;
-                if ((int)u == P.n - 1) P.offsets[P.n] = U.pay_off + 20 + 8ull * total;
-            }
+            if (ft.index + 1 == U.net) finish_unit(P, U, u, ecnt + C);  // last tile
         }
     }
     __syncthreads();
@@ -432,15 +435,7 @@ __device__ __forceinline__ void pipe_emit_unit(const PipeParams& P, __amdgpu_buf
     __syncthreads();  // every ring load of the unit has been consumed
     if (tid == 0) {
         add_rlx(P.edone + u, 1u);
-        int32_t* hd = reinterpret_cast<int32_t*>(P.payload + U.pay_off);
-        hd[0] = U.nx;
-        hd[1] = U.ny;
-        hd[2] = U.nz;
-        hd[3] = (int32_t)U.ncells;
-        hd[4] = (int32_t)rank;
-        P.kept[u] = rank;
-        P.offsets[u] = U.pay_off;
-        if ((int)u == P.n - 1) P.offsets[P.n] = U.pay_off + 20 + 8ull * rank;
+        finish_unit(P, U, u, rank);
     }
 }
 
@@ -498,18 +493,94 @@ __global__ __launch_bounds__(kThreads, 4) void k_forward_pipe(PipeParams P) {
         for (int i = 0; i < kPipeStats; ++i) atomicAdd(P.stats + i, st[i]);
 }
 
-// Staged-path emit: one launch over every emit tile of the batch.  Block b
-// belongs to unit etiles[b].unit, but takes its tile index within the unit
-// from that unit's ticket (P.tdone[u], unused by the staged path), so a
-// tile's look-back predecessors have always started (forward progress
-// without assuming dispatch order), and the ticket atomics spread over one
-// address per unit instead of one for the whole grid.
-__global__ __launch_bounds__(kThreads) void k_emit_lb(PipeParams P, const float* __restrict__ coef) {
+// ---------------------------------------------------------------------------
+// Staged-path emit, whole units (k_emit blocks [0, nseg)): one workgroup
+// thresholds and packs a unit of at most WC_OPT_EMIT_SEG_MAX emit tiles,
+// streaming its coefficients in kEmitTile chunks with the next chunk's loads
+// in flight while the current one is packed.  Pair ranks and the previous
+// kept index are running values: no look-back, no tickets, no traffic
+// between workgroups.  sm[4..11] / sm[12..19]: per-wave counts and lasts of
+// even / odd chunks (alternating, so one barrier per chunk suffices).
+__device__ __forceinline__ void seg_load(const float4* __restrict__ p4, uint32_t c, uint32_t nc, int w, int l,
+                                         float4 (&q)[8]) {
+    const uint32_t start = c * (uint32_t)kEmitTile;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const uint32_t e = start + (uint32_t)(w * 2048 + it * 256 + 4 * l);
+        q[it] = e < nc ? p4[e >> 2] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+__device__ __forceinline__ void seg_pack(const float4 (&q)[8], float tf, uint32_t c, uint32_t nc, int w, int l,
+                                         uint32_t* cs, uint32_t& rank, uint32_t& prev, uint2* __restrict__ pairs) {
+    const uint32_t start = c * (uint32_t)kEmitTile;
+    const uint32_t kb = keep_bits(q, tf, min((uint32_t)kEmitTile, nc - start), w, l);
+    uint32_t wc, wl;
+    wave_totals(kb, w, l, wc, wl);
+    if (l == 0) {
+        cs[w] = wc;
+        cs[4 + w] = wl;
+    }
+    __syncthreads();
+    uint32_t r = rank, pv = prev, tot = 0, cl = prev;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t ci = cs[i], li = cs[4 + i];
+        if (i < w) {
+            r += ci;
+            if (li) pv = start + li - 1u;
+        }
+        tot += ci;
+        if (li) cl = start + li - 1u;
+    }
+    emit_pairs([&](int it) { return q[it]; }, kb, start, w, l, r, pv, pairs);
+    rank += tot;
+    prev = cl;
+}
+
+__device__ __forceinline__ void emit_seg(const PipeParams& P, const float* __restrict__ coef, uint32_t u,
+                                         uint32_t* sm, int tid) {
+    const UnitDev& U = P.units[u];
+    const int w = tid >> 6, l = tid & 63;
+    const float tf = thresh_as_float(key_thresh(P.key[u], P.keep));
+    const uint32_t nc = (uint32_t)U.ncells;
+    const uint32_t nch = (nc + kEmitTile - 1) / kEmitTile;
+    const float4* __restrict__ p4 = reinterpret_cast<const float4*>(coef + (P.ring_coefs ? U.ring_off : U.coef_off));
+    uint2* __restrict__ pairs = reinterpret_cast<uint2*>(P.payload + U.pay_off + 20);
+    uint32_t rank = 0, prev = 0xffffffffu;
+    float4 a[8], b[8];
+    if (nch) seg_load(p4, 0, nc, w, l, a);
+    for (uint32_t c = 0; c < nch; c += 2) {
+        if (c + 1 < nch) seg_load(p4, c + 1, nc, w, l, b);
+        seg_pack(a, tf, c, nc, w, l, sm + 4, rank, prev, pairs);
+        if (c + 1 == nch) break;
+        if (c + 2 < nch) seg_load(p4, c + 2, nc, w, l, a);
+        seg_pack(b, tf, c + 1, nc, w, l, sm + 12, rank, prev, pairs);
+    }
+    if (tid == 0) finish_unit(P, U, u, rank);
+}
+
+// Staged-path emit, one launch: blocks [0, nseg) pack whole units
+// (emit_seg); the rest pack the emit tiles of the other units with decoupled
+// look-back (pipe_emit).  A look-back block takes its tile index within the
+// unit from that unit's ticket (P.tdone[u], unused by the staged path), so a
+// tile's predecessors have always started (forward progress without
+// assuming dispatch order), and the ticket atomics spread over one address
+// per unit.  SEG = false compiles the look-back path alone (its register
+// budget is not raised by the whole-unit path's double buffer).
+template <bool SEG>
+__global__ __launch_bounds__(kThreads, 4) void k_emit(PipeParams P, const float* __restrict__ coef, uint32_t nseg) {
     __shared__ __attribute__((aligned(16))) uint32_t sm[32];
     const int tid = threadIdx.x;
+    if constexpr (SEG) {
+        if (blockIdx.x < nseg) {
+            emit_seg(P, coef, P.segs[P.seg_base + blockIdx.x], sm, tid);
+            return;
+        }
+    }
     if (tid == 0) {
-        const uint32_t u = P.etiles[P.etile_base + blockIdx.x].unit;
-        sm[16] = (P.dbg & 1) ? blockIdx.x : P.units[u].et_begin + atomicAdd(P.tdone + u, 1u);
+        const uint32_t u = P.etiles[P.etile_base + (blockIdx.x - nseg)].unit;
+        sm[16] = P.units[u].et_begin + atomicAdd(P.tdone + u, 1u);
     }
     __syncthreads();
     const uint32_t et = __builtin_amdgcn_readfirstlane(sm[16]);
@@ -520,8 +591,11 @@ __global__ __launch_bounds__(kThreads) void k_emit_lb(PipeParams P, const float*
 
 }  // namespace
 
-hipError_t launch_emit_lb(hipStream_t st, const PipeParams& p, const float* coef, uint32_t netiles) {
-    if (netiles) k_emit_lb<<<netiles, kThreads, 0, st>>>(p, coef);
+hipError_t launch_emit(hipStream_t st, const PipeParams& p, const float* coef, uint32_t nseg, uint32_t netiles) {
+    if (nseg)
+        k_emit<true><<<nseg + netiles, kThreads, 0, st>>>(p, coef, nseg);
+    else if (netiles)
+        k_emit<false><<<netiles, kThreads, 0, st>>>(p, coef, 0u);
     return hipGetLastError();
 }
 
