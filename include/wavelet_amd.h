@@ -103,7 +103,8 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports kernel-side errors of earlier 
                                    chunk c+1 overlapping emit of chunk c (0 = whole batch) */
 #define WC_OPT_CHUNK_SLOTS 9    /* coefficient slots of the chunked forward (default 3) */
 #define WC_OPT_EMIT_SEG_MAX 10  /* staged emit: units of at most this many 8192-coefficient tiles are packed
-                                   whole by one workgroup each, no look-back (default 64; 0 = never) */
+                                   whole by one workgroup each, no look-back (default 0 = never: the
+                                   look-back tiles measured faster) */
 #define WC_OPT_EMIT_SEG_MIN_UNITS 11 /* ... when the batch holds at least this many of them (default 256) */
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 

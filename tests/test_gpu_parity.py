@@ -36,10 +36,10 @@ def pack(wc, boxes, dtype=np.float64, offsets=None):
 
 
 def set_path(ctx, path, lag=0, ring=0):
-    """Forward-path options (library defaults: staged, whole-unit emit when >= 256 units)."""
+    """Forward-path options (library defaults: staged, look-back emit tiles)."""
     ctx.set_pipe(path == "pipe", lag=lag, ring=ring)
     ctx.set_chunk(16384 if path == "chunked" else 0, slots=2)
-    ctx.set_emit_seg(0 if path == "lookback" else 64, 1 if path == "seg" else 256)
+    ctx.set_emit_seg(64 if path == "seg" else 0, 1)
 
 
 def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None, path="staged", lag=0, ring=0):
@@ -57,11 +57,11 @@ def oracle_payload(O, b, keep):
     return O.compress_payload(b32, keep)[0]
 
 
-# Forward paths, all byte-identical: the library default; every unit through
-# look-back emit tiles; whole-unit emit forced (units of <= 64 tiles) beside
-# look-back tiles for larger units in the same launch; chunked two-stream
-# (16 Ki-cell chunks, 2 coefficient slots); the pipelined single launch.
-PATHS = ["staged", "lookback", "seg", "chunked", "pipe"]
+# Forward paths, all byte-identical: the library default (look-back emit
+# tiles); whole-unit emit forced for units of <= 64 tiles, beside look-back
+# tiles for larger units in the same launch; chunked two-stream (16 Ki-cell
+# chunks, 2 coefficient slots); the pipelined single launch.
+PATHS = ["staged", "seg", "chunked", "pipe"]
 
 
 @pytest.mark.parametrize("path", PATHS)

@@ -196,9 +196,9 @@ class Context:
         self.set_option(WC_OPT_CHUNK, cells)
         self.set_option(WC_OPT_CHUNK_SLOTS, slots)
 
-    def set_emit_seg(self, max_tiles: int = 64, min_units: int = 256):
+    def set_emit_seg(self, max_tiles: int = 0, min_units: int = 256):
         """Staged emit: units of <= max_tiles 8192-coefficient tiles packed whole by one
-        workgroup when the batch holds >= min_units of them (max_tiles 0: never)."""
+        workgroup when the batch holds >= min_units of them (max_tiles 0: never, the default)."""
         self.set_option(WC_OPT_EMIT_SEG_MAX, max_tiles)
         self.set_option(WC_OPT_EMIT_SEG_MIN_UNITS, min_units)
 

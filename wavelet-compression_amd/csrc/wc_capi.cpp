@@ -115,7 +115,7 @@ struct wc_ctx {
     bool opt_stats = false;  // WC_OPT_PIPE_STATS
     int64_t opt_chunk = 0;   // WC_OPT_CHUNK: cells per chunk (0 = whole batch at once)
     int opt_slots = 3;       // WC_OPT_CHUNK_SLOTS
-    int opt_seg_max = 64;    // WC_OPT_EMIT_SEG_MAX
+    int opt_seg_max = 0;     // WC_OPT_EMIT_SEG_MAX (0: look-back tiles only, the faster layout measured)
     int opt_seg_min = 256;   // WC_OPT_EMIT_SEG_MIN_UNITS
     hipStream_t side = nullptr;        // second stream of the chunked forward (emit launches)
     std::vector<hipEvent_t> chunk_ev;  // 2 per chunk + 1
@@ -559,6 +559,7 @@ PipeParams pipe_params(wc_ctx* c, const void* d_cells, int n, double keep, uint8
     p.keep = keep;
     p.claim = 1;
     p.segs = (const uint32_t*)P.d_segs.p;
+    { const char* d = std::getenv("WCAMD_DBG"); p.dbg = d ? (uint32_t)std::atoi(d) : 0u; }
     return p;
 }
 

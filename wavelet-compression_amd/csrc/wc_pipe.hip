@@ -159,9 +159,14 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-template <class Val>
+// STAGE: the pairs of each 256-element block are first placed in this wave's
+// 256-entry LDS stage in rank order, then copied out with contiguous 8-B
+// stores (one full 512-B row per instruction instead of up to four sparse,
+// partial-line scatters: the pair stores, not the bytes, bounded the emit).
+// A wave's LDS operations execute in order, so the stage needs no barrier.
+template <bool STAGE, class Val>
 __device__ __forceinline__ void emit_pairs(Val val, uint32_t kb, uint32_t start, int w, int l, uint32_t rank,
-                                           uint32_t prev, uint2* __restrict__ pairs) {
+                                           uint32_t prev, uint2* __restrict__ pairs, uint2* stage) {
     const unsigned long long lt = (1ull << l) - 1ull;
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
@@ -179,7 +184,7 @@ __device__ __forceinline__ void emit_pairs(Val val, uint32_t kb, uint32_t start,
         const unsigned long long below = any & lt;
         const uint32_t from_lane = __shfl(lane_last, below ? 63 - __clzll(below) : l);
         uint32_t p = below ? from_lane : prev;
-        uint32_t r = rank + pre;
+        uint32_t r = STAGE ? pre : rank + pre;
         if (nib) {
             const float4 v4 = val(it);
             const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
@@ -187,11 +192,20 @@ __device__ __forceinline__ void emit_pairs(Val val, uint32_t kb, uint32_t start,
             for (int j = 0; j < 4; ++j) {
                 if (nib & (1u << j)) {
                     const uint32_t f = ebase + (uint32_t)j;
-                    pairs[r] = make_uint2(f - p - 1u, __float_as_uint(vv[j]));
+                    const uint2 pr = make_uint2(f - p - 1u, __float_as_uint(vv[j]));
+                    if constexpr (STAGE)
+                        stage[r] = pr;
+                    else
+                        pairs[r] = pr;
                     p = f;
                     ++r;
                 }
             }
+        }
+        if constexpr (STAGE) {
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t k = (uint32_t)l; k < itot; k += 64) pairs[rank + k] = stage[k];
+            __builtin_amdgcn_wave_barrier();
         }
         rank += itot;
         prev = __shfl(lane_last, 63 - __clzll(any));
@@ -244,8 +258,8 @@ __device__ __forceinline__ void finish_unit(const PipeParams& P, const UnitDev& 
 // an earlier launch).
 template <bool RING>
 __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_rsrc_t ring,
-                                          const float* __restrict__ coef, uint32_t et, uint32_t* sm, int tid,
-                                          unsigned long long* st) {
+                                          const float* __restrict__ coef, uint32_t et, uint32_t* sm, uint2* stage,
+                                          int tid, unsigned long long* st) {
     const FTile ft = P.etiles[et];
     const uint32_t u = ft.unit;
     const UnitDev& U = P.units[u];
@@ -359,7 +373,7 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
         if (sm[8 + i]) prev = start + sm[8 + i] - 1u;
     }
     uint2* __restrict__ pairs = reinterpret_cast<uint2*>(P.payload + U.pay_off + 20);
-    emit_pairs([&](int it) { return q[it]; }, kb, start, w, l, rank, prev, pairs);
+    emit_pairs<!RING>([&](int it) { return q[it]; }, kb, start, w, l, rank, prev, pairs, stage);
 }
 
 // ---------------------------------------------------------------------------
@@ -428,7 +442,7 @@ __device__ __forceinline__ void pipe_emit_unit(const PipeParams& P, __amdgpu_buf
             tot += ci;
             if (li) cl = start + li - 1u;
         }
-        emit_pairs([&](int it) { return mine[it * 64]; }, kb, start, w, l, r, pv, pairs);
+        emit_pairs<false>([&](int it) { return mine[it * 64]; }, kb, start, w, l, r, pv, pairs, nullptr);
         rank += tot;
         prev = cl;
     }
@@ -512,7 +526,8 @@ __device__ __forceinline__ void seg_load(const float4* __restrict__ p4, uint32_t
 }
 
 __device__ __forceinline__ void seg_pack(const float4 (&q)[8], float tf, uint32_t c, uint32_t nc, int w, int l,
-                                         uint32_t* cs, uint32_t& rank, uint32_t& prev, uint2* __restrict__ pairs) {
+                                         uint32_t* cs, uint32_t& rank, uint32_t& prev, uint2* __restrict__ pairs,
+                                         uint2* stage, uint32_t dbg) {
     const uint32_t start = c * (uint32_t)kEmitTile;
     const uint32_t kb = keep_bits(q, tf, min((uint32_t)kEmitTile, nc - start), w, l);
     uint32_t wc, wl;
@@ -533,13 +548,13 @@ __device__ __forceinline__ void seg_pack(const float4 (&q)[8], float tf, uint32_
         tot += ci;
         if (li) cl = start + li - 1u;
     }
-    emit_pairs([&](int it) { return q[it]; }, kb, start, w, l, r, pv, pairs);
+    if (!(dbg & 2)) emit_pairs<true>([&](int it) { return q[it]; }, (dbg & 1) ? 0u : kb, start, w, l, r, pv, pairs, stage);
     rank += tot;
     prev = cl;
 }
 
 __device__ __forceinline__ void emit_seg(const PipeParams& P, const float* __restrict__ coef, uint32_t u,
-                                         uint32_t* sm, int tid) {
+                                         uint32_t* sm, uint2* stage, int tid) {
     const UnitDev& U = P.units[u];
     const int w = tid >> 6, l = tid & 63;
     const float tf = thresh_as_float(key_thresh(P.key[u], P.keep));
@@ -552,10 +567,10 @@ __device__ __forceinline__ void emit_seg(const PipeParams& P, const float* __res
     if (nch) seg_load(p4, 0, nc, w, l, a);
     for (uint32_t c = 0; c < nch; c += 2) {
         if (c + 1 < nch) seg_load(p4, c + 1, nc, w, l, b);
-        seg_pack(a, tf, c, nc, w, l, sm + 4, rank, prev, pairs);
+        seg_pack(a, tf, c, nc, w, l, sm + 4, rank, prev, pairs, stage, P.dbg);
         if (c + 1 == nch) break;
         if (c + 2 < nch) seg_load(p4, c + 2, nc, w, l, a);
-        seg_pack(b, tf, c + 1, nc, w, l, sm + 12, rank, prev, pairs);
+        seg_pack(b, tf, c + 1, nc, w, l, sm + 12, rank, prev, pairs, stage, P.dbg);
     }
     if (tid == 0) finish_unit(P, U, u, rank);
 }
@@ -571,10 +586,12 @@ __device__ __forceinline__ void emit_seg(const PipeParams& P, const float* __res
 template <bool SEG>
 __global__ __launch_bounds__(kThreads, 4) void k_emit(PipeParams P, const float* __restrict__ coef, uint32_t nseg) {
     __shared__ __attribute__((aligned(16))) uint32_t sm[32];
+    __shared__ uint2 stage_all[kThreads / kWave][256];  // per-wave pair stage (emit_pairs)
     const int tid = threadIdx.x;
+    uint2* stage = stage_all[tid >> 6];
     if constexpr (SEG) {
         if (blockIdx.x < nseg) {
-            emit_seg(P, coef, P.segs[P.seg_base + blockIdx.x], sm, tid);
+            emit_seg(P, coef, P.segs[P.seg_base + blockIdx.x], sm, stage, tid);
             return;
         }
     }
@@ -586,7 +603,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_emit(PipeParams P, const float*
     const uint32_t et = __builtin_amdgcn_readfirstlane(sm[16]);
     __syncthreads();
     __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(nullptr, 0, 0, 0x00020000);
-    pipe_emit<false>(P, none, coef, et, sm, tid, nullptr);
+    pipe_emit<false>(P, none, coef, et, sm, stage, tid, nullptr);
 }
 
 }  // namespace
