@@ -137,7 +137,10 @@ int wc_decompose(wc_ctx* ctx, const void* d_cells, int dtype, const wc_unit* uni
                  float* d_flat);
 
 /* Inverse path for a batch: payloads -> fp32 Box3D cells at units[u].cell_offset.
- * Each payload header must match its unit (W,H,D, ncoeff) or WC_ERR_FORMAT. */
+ * Asynchronous on the context's stream.  Each payload header must match its unit
+ * (W,H,D, ncoeff) and no run may be negative, else the next wc_synchronize (or the
+ * _host variant itself) returns WC_ERR_FORMAT (the reference exits,
+ * src/decompressor.cpp:228-231). */
 int wc_inverse(wc_ctx* ctx, const uint8_t* d_payload, const uint64_t* d_offsets,
                const wc_unit* units, int n, float* d_out);
 

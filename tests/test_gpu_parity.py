@@ -219,6 +219,28 @@ def test_inverse_bit_exact(wc, ctx, oracle, keep):
         assert regen[o:o + b.size].tobytes() == want.tobytes(), f"dims {DIMS[i]}"
 
 
+def test_inverse_writes_every_coefficient(wc, ctx, oracle):
+    """The decode writes zeros between pairs instead of clearing its scratch first: an
+    inverse right after a dense one, over sparse, empty-payload (all-zero, NaN-first) and
+    sign-quirk units, must equal the oracle's decompress exactly."""
+    dense = synth(oracle, [(32, 32, 32)] * 4 + [(64, 16, 8)], seed0=15)
+    units, n, extent, cells = pack(wc, dense)
+    payload, offs, kept = ctx.forward_host(cells, units, n, KEEPS[0])
+    ctx.inverse_host(payload, offs[:n], units, n, extent)
+    sp = special_boxes()
+    boxes = [sp[k][0] for k in ("zeros_f", "nan_first_f", "plus5_spike_f", "const_3902", "minus5_sign_quirk_f",
+                                "zeros", "tie_pm")]
+    boxes.append(np.zeros((32, 32, 32), np.float32))
+    boxes.append(oracle.narrow(synth(oracle, [(64, 64, 64)], seed0=16)[0]))
+    units, n, extent, cells = pack(wc, boxes, np.float32)
+    payload, offs, kept = ctx.forward_host(cells, units, n, KEEPS[2])
+    regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
+    for i, b in enumerate(boxes):
+        o = units[i].cell_offset
+        want = oracle.decompress_payload(wc.capi.unit_payload(payload, offs, kept, i)).ravel()
+        assert regen[o:o + b.size].tobytes() == want.tobytes(), i
+
+
 def test_inverse_flat_random(wc, ctx, oracle):
     import torch
     rng = np.random.default_rng(11)

@@ -148,6 +148,7 @@ int main(int argc, char** argv) {
     if (inverse) {
         auto a = std::chrono::steady_clock::now();
         for (int i = 0; i < steps; ++i) inv();
+        wc_synchronize(ctx);
         auto b = std::chrono::steady_clock::now();
         inv_ms = std::chrono::duration<double, std::milli>(b - a).count() / steps;
         wc_profile_read(ctx, ims, icnt, WC_NUM_STAGES);

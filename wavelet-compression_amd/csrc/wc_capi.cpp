@@ -36,10 +36,10 @@ hipError_t launch_transform(hipStream_t, const void*, int, const UnitDev*, const
 hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
                                  float*, int, unsigned long long*);
 hipError_t launch_pack(hipStream_t, const UnitDev*, int, const uint32_t*, const uint8_t*, uint64_t*, uint8_t*);
-hipError_t launch_decode(hipStream_t, const UnitDev*, int, const FTile*, uint32_t, const uint8_t*,
-                         const uint64_t*, uint64_t*, uint64_t*, float*, uint32_t*);
-hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const XTile*, uint32_t, size_t,
-                          float*);
+hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, const uint8_t*, const uint64_t*,
+                         uint32_t*, unsigned long long*, float*, uint32_t*);
+hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const XTile*, uint32_t, size_t, uint32_t,
+                          size_t, float*);
 hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDev*, int, const FTile*,
                        uint32_t, double*, double*);
 hipError_t launch_forward_pipe(hipStream_t, int, size_t, uint32_t, const PipeParams&);
@@ -121,7 +121,7 @@ struct wc_ctx {
     std::vector<hipEvent_t> chunk_ev;  // 2 per chunk + 1
     bool err_check_pending = false;
     // scratch (grow-only)
-    DevBuf coef, tsum, tbase, part, errflag, ring, state, stats;
+    DevBuf coef, part, errflag, ring, state, stats;
     // host-path staging
     DevBuf h_cells, h_payload, h_packed, h_offsets, h_poff, h_kept, h_out;
     // per-kernel event timing (wc_profile_enable / wc_profile_read)
@@ -488,15 +488,17 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     return WC_OK;
 }
 
+// Per-call state of the decode: ticket[n] (8-B aligned) | status[flat tiles].
+size_t decode_state_bytes(const Plan& P) { return round_up(4ull * P.units.size(), 8) + 8ull * P.ftiles.size(); }
+
 // Scratch of the staged forward, the inverse and the RMSE (grow-only).
 int ensure_scratch(wc_ctx* c) {
     const Plan& P = c->plan;
     const size_t nft = P.ftiles.size();
     int rc;
     if ((rc = ensure(c, c->coef, sizeof(float) * std::max<uint64_t>(P.coef_extent, 1))) ||
-        (rc = ensure(c, c->tsum, sizeof(uint64_t) * nft)) || (rc = ensure(c, c->tbase, sizeof(uint64_t) * nft)) ||
         (rc = ensure(c, c->part, sizeof(double) * nft)) || (rc = ensure(c, c->errflag, 16)) ||
-        (rc = ensure(c, c->state, P.state_bytes)))
+        (rc = ensure(c, c->state, std::max<size_t>(P.state_bytes, decode_state_bytes(P)))))
         return rc;
     return WC_OK;
 }
@@ -516,8 +518,10 @@ int set_device(wc_ctx* c) {
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "hipSetDevice");
 }
 
-// Surface an error bit a kernel raised (pipe dependency timeout) at the next
-// synchronisation point.
+// Surface an error bit a kernel raised (malformed payload in the decode, a
+// dependency wait that timed out) at the next synchronisation point.  The
+// reference exits on a malformed payload (src/decompressor.cpp:228-231);
+// here it is WC_ERR_FORMAT.
 int check_kernel_errors(wc_ctx* c) {
     if (!c->err_check_pending) return WC_OK;
     c->err_check_pending = false;
@@ -525,7 +529,12 @@ int check_kernel_errors(wc_ctx* c) {
     hipError_t e = hipMemcpyAsync(&flag, c->errflag.p, 4, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "error flag readback");
-    if (flag & kErrTimeout) return fail(c, WC_ERR_HIP, "pipelined forward: a dependency wait timed out");
+    if (flag & (kErrHeader | kErrNegativeRun)) {
+        char buf[128];
+        std::snprintf(buf, sizeof buf, "malformed payload (flags 0x%x: 1 header, 2 negative run)", flag);
+        return fail(c, WC_ERR_FORMAT, buf);
+    }
+    if (flag & kErrTimeout) return fail(c, WC_ERR_HIP, "a dependency wait between workgroups timed out");
     return WC_OK;
 }
 
@@ -559,7 +568,6 @@ PipeParams pipe_params(wc_ctx* c, const void* d_cells, int n, double keep, uint8
     p.keep = keep;
     p.claim = 1;
     p.segs = (const uint32_t*)P.d_segs.p;
-    { const char* d = std::getenv("WCAMD_DBG"); p.dbg = d ? (uint32_t)std::atoi(d) : 0u; }
     return p;
 }
 
@@ -713,7 +721,7 @@ void wc_ctx_destroy(wc_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->coef,      &c->tsum,      &c->tbase,     &c->part,       &c->errflag,
+    DevBuf* bufs[] = {&c->coef,      &c->part,       &c->errflag,
                       &c->ring,      &c->state,     &c->stats,      &c->h_cells,    &c->h_payload,
                       &c->h_packed,  &c->h_offsets, &c->h_poff,    &c->h_kept,     &c->h_out,
                       &c->plan.d_units, &c->plan.d_xtiles, &c->plan.d_ftiles, &c->plan.d_etiles,
@@ -867,33 +875,28 @@ int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, c
     if ((rc = set_device(c)) || (rc = get_plan_staged(c, units, n)) || (rc = ensure_scratch(c))) return rc;
     Plan& P = c->plan;
     hipError_t e;
-    if ((e = hipMemsetAsync(c->coef.p, 0, sizeof(float) * P.coef_extent, c->stream)) != hipSuccess ||
+    // per-call decode state: ticket[n] | status[flat tiles]; the dense
+    // coefficient scratch itself is fully written by the decode (no memset)
+    uint8_t* st = (uint8_t*)c->state.p;
+    if ((e = hipMemsetAsync(st, 0, decode_state_bytes(P), c->stream)) != hipSuccess ||
         (e = hipMemsetAsync(c->errflag.p, 0, 4, c->stream)) != hipSuccess)
         return hip_fail(c, e, "memset");
     {
         StageTimer t(c, WC_STAGE_DECODE);
-        e = launch_decode(c->stream, (const UnitDev*)P.d_units.p, n, (const FTile*)P.d_ftiles.p,
-                          (uint32_t)P.ftiles.size(), d_payload, d_offsets, (uint64_t*)c->tsum.p,
-                          (uint64_t*)c->tbase.p, (float*)c->coef.p, (uint32_t*)c->errflag.p);
+        e = launch_decode(c->stream, (const UnitDev*)P.d_units.p, (const FTile*)P.d_ftiles.p,
+                          (uint32_t)P.ftiles.size(), d_payload, d_offsets, (uint32_t*)st,
+                          (unsigned long long*)(st + round_up(4ull * n, 8)), (float*)c->coef.p,
+                          (uint32_t*)c->errflag.p);
     }
     if (e != hipSuccess) return hip_fail(c, e, "decode launch");
     {
         StageTimer t(c, WC_STAGE_INVERSE);
         e = launch_inverse(c->stream, (const float*)c->coef.p, 0, (const UnitDev*)P.d_units.p,
-                           (const XTile*)P.d_xtiles.p, (uint32_t)P.xtiles.size(), P.lds_inverse, d_out);
+                           (const XTile*)P.d_xtiles.p, P.ngen, P.lds_inverse, P.nfast, P.lds_fast, d_out);
     }
     if (e != hipSuccess) return hip_fail(c, e, "inverse launch");
-    // Malformed payloads end the reference with exit(EXIT_FAILURE)
-    // (src/decompressor.cpp:228-231); here they return WC_ERR_FORMAT.
-    uint32_t flag = 0;
-    if ((e = hipMemcpyAsync(&flag, c->errflag.p, sizeof(flag), hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
-        return hip_fail(c, e, "error flag readback");
-    if (flag) {
-        char buf[128];
-        std::snprintf(buf, sizeof buf, "malformed payload (flags 0x%x: 1 header, 2 negative run)", flag);
-        return fail(c, WC_ERR_FORMAT, buf);
-    }
+    // Malformed payloads surface at the next wc_synchronize (WC_ERR_FORMAT).
+    c->err_check_pending = true;
     return WC_OK;
 }
 
@@ -907,7 +910,7 @@ int wc_inverse_flat(wc_ctx* c, const float* d_flat, const wc_unit* units, int n,
     Plan& P = c->plan;
     StageTimer t(c, WC_STAGE_INVERSE);
     hipError_t e = launch_inverse(c->stream, d_flat, 1, (const UnitDev*)P.d_units.p, (const XTile*)P.d_xtiles.p,
-                                  (uint32_t)P.xtiles.size(), P.lds_inverse, d_out);
+                                  P.ngen, P.lds_inverse, P.nfast, P.lds_fast, d_out);
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "inverse launch");
 }
 
@@ -1049,7 +1052,7 @@ int wc_inverse_host(wc_ctx* c, const uint8_t* payload, const uint64_t* offsets, 
             return hip_fail(c, e, "box readback");
     }
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(c, e, "sync");
-    return WC_OK;
+    return check_kernel_errors(c);
 }
 
 // Stage host arrays through the context's staging buffers for the

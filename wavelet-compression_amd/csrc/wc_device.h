@@ -125,4 +125,89 @@ __device__ __forceinline__ ScanOut block_scan_sum_max(S v, uint32_t m, S* s_sum,
 }
 
 
+// ---------------------------------------------------------------------------
+// Hand-offs between workgroups of one launch (MI355X_MICROARCH.md, Valid
+// forms): relaxed agent-scope atomics on self-validating 8-B granules (the
+// word carries its own data, so no fence is needed), bounded spins.
+constexpr uint32_t kSpinLimit = 1u << 20;  // x ~1.7 us: ~2 s before a wait is declared hung
+constexpr unsigned long long kFlagAgg = 1ull << 62;   // granule holds this tile's aggregate
+constexpr unsigned long long kFlagIncl = 2ull << 62;  // granule holds the inclusive prefix
+constexpr unsigned long long kMask62 = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint32_t ld_rlx(const uint32_t* p) {
+    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_rlx(const unsigned long long* p) {
+    return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rlx(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void add_rlx(uint32_t* p, uint32_t v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Bounded spin with backoff: pollers share the memory system with the
+// streaming loads (MI355X_MICROARCH.md: 255 pollers cut chip bandwidth
+// 37-71 %), so re-polls slow down from ~0.2 us to ~1.7 us.
+__device__ __forceinline__ bool spin_fail(uint32_t& spins, uint32_t* err) {
+    if (++spins > kSpinLimit) {
+        atomicOr(err, kErrTimeout);
+        return true;
+    }
+    if (spins < 4)
+        __builtin_amdgcn_s_sleep(8);
+    else if (spins < 16)
+        __builtin_amdgcn_s_sleep(24);
+    else
+        __builtin_amdgcn_s_sleep(64);
+    return false;
+}
+
+// Decoupled look-back (one wave): exclusive prefix of tile t from granules
+// st[0..t) of 62-bit sums.  A window of the 64 nearest predecessors (lane l =
+// tile pos - l; indices below 0 read as an inclusive 0) is summed up to the
+// nearest inclusive granule once every lane before it has published; a run
+// of published aggregates before the first unpublished tile is summed and
+// the window slides past it.
+__device__ __forceinline__ unsigned long long lookback_sum62(const unsigned long long* st, int64_t t, int l,
+                                                             uint32_t* err) {
+    unsigned long long excl = 0;
+    int64_t pos = t - 1;
+    for (uint32_t spins = 0;;) {
+        const int64_t idx = pos - l;
+        const unsigned long long v = idx >= 0 ? ld_rlx(st + idx) : kFlagIncl;
+        const unsigned long long incl = __ballot((v >> 62) == 2);
+        const unsigned long long zero = __ballot((v >> 62) == 0);
+        const int kI = incl ? __ffsll((long long)incl) - 1 : 64;
+        const int kZ = zero ? __ffsll((long long)zero) - 1 : 64;
+        const int take = kI < kZ ? kI + 1 : kZ;  // lanes [0, take) are summed
+        if (take > 0) excl += wave_sum(l < take ? (v & kMask62) : 0ull);
+        if (kI < kZ) break;
+        pos -= take;
+        if (take == 0 && spin_fail(spins, err)) break;
+    }
+    return excl & kMask62;
+}
+
+// Wave-wide inclusive sum (64 lanes) on DPP lane moves, GFX9 pattern:
+// row_shr 1/2/4/8 within 16-lane rows, then row_bcast:15 and row_bcast:31
+// carry into the next rows.  Lanes whose source is out of range read 0.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)v, CTRL, ROW_MASK, 0xf, false);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(v >> 32), CTRL, ROW_MASK, 0xf, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_incl_sum(uint64_t v) {
+    v += dpp_u64<0x111, 0xf>(v);  // row_shr:1
+    v += dpp_u64<0x112, 0xf>(v);  // row_shr:2
+    v += dpp_u64<0x114, 0xf>(v);  // row_shr:4
+    v += dpp_u64<0x118, 0xf>(v);  // row_shr:8
+    v += dpp_u64<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+    v += dpp_u64<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 }  // namespace wc

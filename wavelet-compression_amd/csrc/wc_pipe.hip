@@ -39,25 +39,10 @@ namespace wc {
 
 namespace {
 
-constexpr uint32_t kSpinLimit = 1u << 20;  // x ~1.7 us: ~2 s before a wait is declared hung
-constexpr unsigned long long kFlagAgg = 1ull << 62;
-constexpr unsigned long long kFlagIncl = 2ull << 62;
 constexpr unsigned long long kMask31 = 0x7fffffffull;
 
 using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint32_t ld_rlx(const uint32_t* p) {
-    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_rlx(const unsigned long long* p) {
-    return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_rlx(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void add_rlx(uint32_t* p, uint32_t v) {
-    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Ring access: buffer instructions with aux = 16 (sc1): stores write through
@@ -76,23 +61,6 @@ __device__ __forceinline__ void ring_st1(__amdgpu_buffer_rsrc_t r, uint32_t byte
 __device__ __forceinline__ float4 ring_ld4(__amdgpu_buffer_rsrc_t r, uint32_t byte) {
     const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte, 0, 16);
     return make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
-}
-
-// Bounded spin with backoff: pollers share the memory system with the
-// streaming loads (MI355X_MICROARCH.md: 255 pollers cut chip bandwidth
-// 37-71 %), so re-polls slow down from ~0.2 us to ~1.7 us.
-__device__ __forceinline__ bool spin_fail(uint32_t& spins, uint32_t* err) {
-    if (++spins > kSpinLimit) {
-        atomicOr(err, kErrTimeout);
-        return true;
-    }
-    if (spins < 4)
-        __builtin_amdgcn_s_sleep(8);
-    else if (spins < 16)
-        __builtin_amdgcn_s_sleep(24);
-    else
-        __builtin_amdgcn_s_sleep(64);
-    return false;
 }
 
 __device__ __forceinline__ unsigned long long now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
@@ -527,7 +495,7 @@ __device__ __forceinline__ void seg_load(const float4* __restrict__ p4, uint32_t
 
 __device__ __forceinline__ void seg_pack(const float4 (&q)[8], float tf, uint32_t c, uint32_t nc, int w, int l,
                                          uint32_t* cs, uint32_t& rank, uint32_t& prev, uint2* __restrict__ pairs,
-                                         uint2* stage, uint32_t dbg) {
+                                         uint2* stage) {
     const uint32_t start = c * (uint32_t)kEmitTile;
     const uint32_t kb = keep_bits(q, tf, min((uint32_t)kEmitTile, nc - start), w, l);
     uint32_t wc, wl;
@@ -548,7 +516,7 @@ __device__ __forceinline__ void seg_pack(const float4 (&q)[8], float tf, uint32_
         tot += ci;
         if (li) cl = start + li - 1u;
     }
-    if (!(dbg & 2)) emit_pairs<true>([&](int it) { return q[it]; }, (dbg & 1) ? 0u : kb, start, w, l, r, pv, pairs, stage);
+    emit_pairs<true>([&](int it) { return q[it]; }, kb, start, w, l, r, pv, pairs, stage);
     rank += tot;
     prev = cl;
 }
@@ -567,10 +535,10 @@ __device__ __forceinline__ void emit_seg(const PipeParams& P, const float* __res
     if (nch) seg_load(p4, 0, nc, w, l, a);
     for (uint32_t c = 0; c < nch; c += 2) {
         if (c + 1 < nch) seg_load(p4, c + 1, nc, w, l, b);
-        seg_pack(a, tf, c, nc, w, l, sm + 4, rank, prev, pairs, stage, P.dbg);
+        seg_pack(a, tf, c, nc, w, l, sm + 4, rank, prev, pairs, stage);
         if (c + 1 == nch) break;
         if (c + 2 < nch) seg_load(p4, c + 2, nc, w, l, a);
-        seg_pack(b, tf, c + 1, nc, w, l, sm + 12, rank, prev, pairs, stage, P.dbg);
+        seg_pack(b, tf, c + 1, nc, w, l, sm + 12, rank, prev, pairs, stage);
     }
     if (tid == 0) finish_unit(P, U, u, rank);
 }
