@@ -1,5 +1,6 @@
 set -o pipefail
-export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/t4.log 2>&1; echo "tests rc=$?"
-for d in 0 1; do echo "== dbg=$d"; WCAMD_DBG=$d timeout -k 10 60 tools/bin/wc_bench 1024 64 f64 0.999 10 2 1 || exit 1; done > gpurun_out/inv4.log 2>&1 && echo DONE
+exec tools/gpu_run.sh \
+  "kt_wcb:200:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_wcb -o wcb -- tools/bin/wc_bench 1024 64 f64 0.999 10 2 1" \
+  "pmc_fetch:200:rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch -o fetch -- tools/bin/wc_bench 1024 64 f64 0.999 3 1 1" \
+  "pmc_write:200:rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write -o write -- tools/bin/wc_bench 1024 64 f64 0.999 3 1 1" \
+  "wcb_f32:120:tools/bin/wc_bench 64 128 f32 0.9999 10 2 1 0 1"
