@@ -99,9 +99,9 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports kernel-side errors of earlier 
 #define WC_OPT_PIPE_PREFETCH 5  /* 1: claim the next ticket while working (default 0) */
 #define WC_OPT_PIPE_WGS 6       /* workgroups per CU (0 = occupancy limit) */
 #define WC_OPT_PIPE_STATS 7     /* 1: collect wait-time counters (wc_pipe_stats) */
-#define WC_OPT_CHUNK 8          /* staged forward over chunks of this many cells, transform of
-                                   chunk c+1 overlapping emit of chunk c (0 = whole batch) */
-#define WC_OPT_CHUNK_SLOTS 9    /* coefficient slots of the chunked forward (default 3) */
+#define WC_OPT_CHUNK 8          /* forward over chunks of this many cells: one launch per chunk
+                                   transforms it and packs the previous chunk (0 = whole batch) */
+#define WC_OPT_CHUNK_SLOTS 9    /* coefficient slots of the chunked forward (default 2) */
 #define WC_OPT_EMIT_SEG_MAX 10  /* staged emit: units of at most this many 8192-coefficient tiles are packed
                                    whole by one workgroup each, no look-back (default 0 = never: the
                                    look-back tiles measured faster) */

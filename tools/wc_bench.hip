@@ -6,7 +6,7 @@
 //
 // usage: wc_bench [boxes=1024] [dim=64] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1]
 //                 [pipe=1|0] [check=0|1] [lag=0] [ring=0] [claim=1] [prefetch=0] [wgs=0] [stats=0]
-//                 [chunk=0] [slots=3] [seg=0] [segmin=256]
+//                 [chunk=0] [slots=2] [seg=0] [segmin=256]
 // check=1: also run the plain staged path (look-back emit only) once and
 // compare every unit's payload bytes with the configured path's
 // ("paths_identical" in the JSON line).
@@ -72,7 +72,7 @@ int main(int argc, char** argv) {
     const int wgs = argc > 14 ? std::atoi(argv[14]) : 0;
     const int stats = argc > 15 ? std::atoi(argv[15]) : 0;
     const long long chunk = argc > 16 ? std::atoll(argv[16]) : 0;
-    const int slots = argc > 17 ? std::atoi(argv[17]) : 3;
+    const int slots = argc > 17 ? std::atoi(argv[17]) : 2;
     const int seg = argc > 18 ? std::atoi(argv[18]) : 0;  // library default
     const int segmin = argc > 19 ? std::atoi(argv[19]) : 256;
 

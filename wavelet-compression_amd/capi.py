@@ -190,9 +190,9 @@ class Context:
         self.set_option(WC_OPT_PIPE_LAG, lag)
         self.set_option(WC_OPT_PIPE_RING, ring)
 
-    def set_chunk(self, cells: int, slots: int = 3):
-        """Chunked forward: the transform of chunk c+1 overlaps the emit of chunk c on a
-        second stream (cells per chunk; 0 = the whole batch at once)."""
+    def set_chunk(self, cells: int, slots: int = 2):
+        """Chunked forward: one launch per chunk transforms it and packs the previous chunk
+        (cells per chunk; 0 = the whole batch at once)."""
         self.set_option(WC_OPT_CHUNK, cells)
         self.set_option(WC_OPT_CHUNK_SLOTS, slots)
 

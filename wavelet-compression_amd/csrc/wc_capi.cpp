@@ -9,8 +9,8 @@
 //   WC_OPT_PIPE = 0 (default): staged kernels: k_transform{,_fast} -> flat
 //       coefficients in HBM scratch -> k_emit (threshold + ordered pack:
 //       whole units per workgroup, or emit tiles with decoupled look-back);
-//       WC_OPT_CHUNK > 0 cuts the batch into chunks whose transform and emit
-//       launches overlap on two streams
+//       WC_OPT_CHUNK > 0 cuts the batch into chunks: one launch per chunk
+//       transforms it and packs the previous one (k_chunk)
 //   WC_OPT_PIPE = 1: k_forward_pipe, one persistent launch: transform
 //       tiles -> coefficient ring (Infinity-Cache resident) -> emit tiles
 //       (threshold + decoupled look-back + pack), interleaved by a host-built
@@ -44,6 +44,9 @@ hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDe
                        uint32_t, double*, double*);
 hipError_t launch_forward_pipe(hipStream_t, int, size_t, uint32_t, const PipeParams&);
 hipError_t launch_emit(hipStream_t, const PipeParams&, const float*, uint32_t, uint32_t);
+size_t chunk_lds_bytes(size_t tile_lds);
+hipError_t launch_chunk(hipStream_t, int, size_t, const PipeParams&, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
+                        uint32_t);
 }  // namespace wc
 
 using namespace wc;
@@ -114,11 +117,9 @@ struct wc_ctx {
     int opt_wgs = 0;         // WC_OPT_PIPE_WGS (0 = occupancy limit)
     bool opt_stats = false;  // WC_OPT_PIPE_STATS
     int64_t opt_chunk = 0;   // WC_OPT_CHUNK: cells per chunk (0 = whole batch at once)
-    int opt_slots = 3;       // WC_OPT_CHUNK_SLOTS
+    int opt_slots = 2;       // WC_OPT_CHUNK_SLOTS
     int opt_seg_max = 0;     // WC_OPT_EMIT_SEG_MAX (0: look-back tiles only, the faster layout measured)
     int opt_seg_min = 256;   // WC_OPT_EMIT_SEG_MIN_UNITS
-    hipStream_t side = nullptr;        // second stream of the chunked forward (emit launches)
-    std::vector<hipEvent_t> chunk_ev;  // 2 per chunk + 1
     bool err_check_pending = false;
     // scratch (grow-only)
     DevBuf coef, part, errflag, ring, state, stats;
@@ -624,53 +625,26 @@ int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep
     return WC_OK;
 }
 
-// Chunked forward: transform of chunk c+1 (context stream) overlaps the emit
-// of chunk c (side stream); events order each emit after its transform and
-// each slot's rewrite after the emit that read it.
+// Chunked forward: launch k transforms chunk k into slot k % nslots and packs
+// chunk k - 1 (wc_pipe.hip k_chunk), all on the context stream.
 int forward_chunked(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
                     uint64_t* d_offsets, uint32_t* d_kept) {
     Plan& P = c->plan;
-    const UnitDev* du = (const UnitDev*)P.d_units.p;
-    const XTile* dxt = (const XTile*)P.d_xtiles.p;
     hipError_t e;
-    if (!c->side && (e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) != hipSuccess)
-        return hip_fail(c, e, "side stream");
-    const size_t nev = 2 * P.chunks.size() + 1;
-    while (c->chunk_ev.size() < nev) {
-        hipEvent_t ev = nullptr;
-        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(c, e, "event");
-        c->chunk_ev.push_back(ev);
-    }
-    hipEvent_t* ev_t = c->chunk_ev.data();
-    hipEvent_t* ev_e = ev_t + P.chunks.size();
-    hipEvent_t ev0 = ev_t[2 * P.chunks.size()];
     StageTimer timer(c, WC_STAGE_CHUNKED);
     if ((e = hipMemsetAsync(c->state.p, 0, P.state_bytes, c->stream)) != hipSuccess)
         return hip_fail(c, e, "memset state");
     PipeParams p = pipe_params(c, d_cells, n, keep, d_payload, d_offsets, d_kept);
     p.ring_coefs = 1;
-    float* ring = (float*)c->ring.p;
-    if ((e = hipEventRecord(ev0, c->stream)) != hipSuccess || (e = hipStreamWaitEvent(c->side, ev0, 0)) != hipSuccess)
-        return hip_fail(c, e, "chunk start");
-    for (size_t k = 0; k < P.chunks.size(); ++k) {
-        const Plan::Chunk& ch = P.chunks[k];
-        if (k >= (size_t)P.nslots && (e = hipStreamWaitEvent(c->stream, ev_e[k - P.nslots], 0)) != hipSuccess)
-            return hip_fail(c, e, "slot wait");
-        e = launch_transform(c->stream, d_cells, dtype, du, dxt + ch.gen_b, ch.gen_n, P.lds_gen, ring, 2, p.key);
-        if (e == hipSuccess)
-            e = launch_transform_fast(c->stream, d_cells, dtype, du, dxt + ch.fast_b, ch.fast_n, P.lds_fast, ring, 2,
-                                      p.key);
-        if (e != hipSuccess) return hip_fail(c, e, "transform launch");
-        if ((e = hipEventRecord(ev_t[k], c->stream)) != hipSuccess ||
-            (e = hipStreamWaitEvent(c->side, ev_t[k], 0)) != hipSuccess)
-            return hip_fail(c, e, "chunk event");
-        p.seg_base = ch.seg_b;
-        p.etile_base = ch.et_b;
-        if ((e = launch_emit(c->side, p, ring, ch.seg_n, ch.et_n)) != hipSuccess) return hip_fail(c, e, "emit launch");
-        if ((e = hipEventRecord(ev_e[k], c->side)) != hipSuccess) return hip_fail(c, e, "chunk event");
+    const size_t lds = chunk_lds_bytes(std::max(P.lds_gen, P.lds_fast));
+    const size_t nch = P.chunks.size();
+    for (size_t k = 0; k <= nch; ++k) {
+        const Plan::Chunk* t = k < nch ? &P.chunks[k] : nullptr;
+        const Plan::Chunk* m = k > 0 ? &P.chunks[k - 1] : nullptr;
+        e = launch_chunk(c->stream, dtype, lds, p, t ? t->gen_b : 0, t ? t->gen_n : 0, t ? t->fast_b : 0,
+                         t ? t->fast_n : 0, m ? m->et_b : 0, m ? m->et_n : 0);
+        if (e != hipSuccess) return hip_fail(c, e, "chunk launch");
     }
-    if ((e = hipStreamWaitEvent(c->stream, ev_e[P.chunks.size() - 1], 0)) != hipSuccess)
-        return hip_fail(c, e, "chunk join");
     return WC_OK;
 }
 
@@ -733,11 +707,6 @@ void wc_ctx_destroy(wc_ctx* c) {
         c->ev_pool.push_back(m.b);
     }
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : c->chunk_ev) (void)hipEventDestroy(e);
-    if (c->side) {
-        (void)hipStreamSynchronize(c->side);
-        (void)hipStreamDestroy(c->side);
-    }
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }

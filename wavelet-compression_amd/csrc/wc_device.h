@@ -46,17 +46,29 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 
 // Load the x-pair (x, x+1) of a row as fp32 (fp64 cells narrowed RNE,
 // src/preprocess.cpp:78).  `vec`: both elements in one aligned vector load.
-template <typename T>
+// NT: non-temporal (streaming) vector load: the cells are read exactly once.
+using f64x2 = double __attribute__((ext_vector_type(2)));
+using f32x2 = float __attribute__((ext_vector_type(2)));
+
+template <typename T, bool NT = false>
 __device__ __forceinline__ void load_xpair(const T* __restrict__ p, bool two, bool vec,
                                            float& a, float& b) {
     if (two) {
         if (vec) {
             if constexpr (sizeof(T) == 8) {
-                const double2 d = *reinterpret_cast<const double2*>(p);
+                f64x2 d;
+                if constexpr (NT)
+                    d = __builtin_nontemporal_load(reinterpret_cast<const f64x2*>(p));
+                else
+                    d = *reinterpret_cast<const f64x2*>(p);
                 a = (float)d.x;
                 b = (float)d.y;
             } else {
-                const float2 d = *reinterpret_cast<const float2*>(p);
+                f32x2 d;
+                if constexpr (NT)
+                    d = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(p));
+                else
+                    d = *reinterpret_cast<const f32x2*>(p);
                 a = d.x;
                 b = d.y;
             }

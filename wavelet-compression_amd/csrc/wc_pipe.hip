@@ -574,6 +574,58 @@ __global__ __launch_bounds__(kThreads, 4) void k_emit(PipeParams P, const float*
     pipe_emit<false>(P, none, coef, et, sm, stage, tid, nullptr);
 }
 
+// ---------------------------------------------------------------------------
+// Chunked forward (WC_OPT_CHUNK): one launch per chunk on ONE stream.  Blocks
+// [0, nE) pack the emit tiles of the previous chunk (look-back, as k_emit),
+// blocks after them transform the tiles of this chunk into its coefficient
+// slot.  The launch boundary orders every hand-off: chunk k's coefficients
+// (slot k % 2) are complete when launch k + 1 reads them, and slot k % 2 is
+// rewritten by launch k + 2 only after launch k + 1 has read it.  A slot is a
+// few tens of MB, so the coefficients should stay in the 256 MiB Infinity
+// Cache between their write and their read.
+struct ChunkLaunch {
+    uint32_t gen_b, gen_n, fast_b, fast_n;  // transform tiles of this chunk (xtiles ranges)
+    uint32_t et_b, et_n;                    // emit tiles of the previous chunk
+};
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void k_chunk(PipeParams P, ChunkLaunch C) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int tid = threadIdx.x;
+    if (blockIdx.x < C.et_n) {
+        uint32_t* sm = reinterpret_cast<uint32_t*>(lds);                   // 32 words
+        uint2* stage = reinterpret_cast<uint2*>(lds + 32) + (tid >> 6) * 256;  // per-wave pair stage
+        if (tid == 0) {
+            const uint32_t u = P.etiles[C.et_b + blockIdx.x].unit;
+            sm[16] = P.units[u].et_begin + atomicAdd(P.tdone + u, 1u);
+        }
+        __syncthreads();
+        const uint32_t et = __builtin_amdgcn_readfirstlane(sm[16]);
+        __syncthreads();
+        __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(nullptr, 0, 0, 0x00020000);
+        pipe_emit<false>(P, none, P.ring, et, sm, stage, tid, nullptr);
+        return;
+    }
+    const uint32_t b = blockIdx.x - C.et_n;
+    const XTile td = P.xtiles[b < C.gen_n ? C.gen_b + b : C.fast_b + (b - C.gen_n)];
+    const UnitDev& U = P.units[td.unit];
+    const T* src = static_cast<const T*>(P.cells) + U.cell_off;
+    float* __restrict__ dst = P.ring + U.ring_off;
+    unsigned long long kmax;
+    if (U.fast) {
+        xform_fast_p1<T>(src, U, td, lds, tid);
+        __syncthreads();
+        kmax = xform_fast_p2<true>(U, td, lds, tid,
+                                   [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
+    } else {
+        xform_generic_p1<T>(src, U, td, lds, tid);
+        __syncthreads();
+        kmax = xform_generic_p2<true>(U, td, lds, tid, [&](int64_t f, float v) { dst[f] = v; });
+    }
+    kmax = wave_max_u64(kmax);
+    if ((tid & 63) == 0 && kmax != 0) atomicMax(P.key + td.unit, kmax);
+}
+
 }  // namespace
 
 hipError_t launch_emit(hipStream_t st, const PipeParams& p, const float* coef, uint32_t nseg, uint32_t netiles) {
@@ -607,6 +659,23 @@ uint32_t pipe_grid(int dtype, size_t lds, int max_per_cu) {
         return 1024;
     if (max_per_cu > 0 && per_cu > max_per_cu) per_cu = max_per_cu;
     return (uint32_t)per_cu * (uint32_t)ncu;
+}
+
+size_t chunk_lds_bytes(size_t tile_lds) {
+    const size_t emit = 4 * 32 + 8 * 256 * (kThreads / kWave);
+    return tile_lds > emit ? tile_lds : emit;
+}
+
+hipError_t launch_chunk(hipStream_t st, int dtype, size_t lds, const PipeParams& p, uint32_t gen_b, uint32_t gen_n,
+                        uint32_t fast_b, uint32_t fast_n, uint32_t et_b, uint32_t et_n) {
+    const ChunkLaunch c{gen_b, gen_n, fast_b, fast_n, et_b, et_n};
+    const uint32_t grid = gen_n + fast_n + et_n;
+    if (grid == 0) return hipSuccess;
+    if (dtype == 1)
+        k_chunk<double><<<grid, kThreads, lds, st>>>(p, c);
+    else
+        k_chunk<float><<<grid, kThreads, lds, st>>>(p, c);
+    return hipGetLastError();
 }
 
 }  // namespace wc
