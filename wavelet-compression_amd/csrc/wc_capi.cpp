@@ -71,7 +71,7 @@ struct Plan {
     int64_t lag = 0, ring_req = 0;
     std::vector<UnitDev> units;
     std::vector<XTile> xtiles;
-    std::vector<FTile> ftiles, etiles;
+    std::vector<FTile> ftiles, etiles, dtiles;
     std::vector<uint32_t> items, waits, segs;
     int seg_max = 0, seg_min = 0;  // whole-unit emit: WC_OPT_EMIT_SEG_MAX / _MIN_UNITS
     uint32_t ngen = 0, nfast = 0;
@@ -91,7 +91,7 @@ struct Plan {
     std::vector<Chunk> chunks;
     uint64_t slot_floats = 0;
     int nslots = 0;
-    DevBuf d_units, d_xtiles, d_ftiles, d_etiles, d_items, d_waits, d_segs;
+    DevBuf d_units, d_xtiles, d_ftiles, d_etiles, d_items, d_waits, d_segs, d_dtiles;
 };
 
 int ceil_log2(int64_t v) {
@@ -466,6 +466,17 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         d.nftiles = (uint32_t)((d.ncells + kFlatTile - 1) / kFlatTile);
         for (uint32_t t = 0; t < d.nftiles; ++t) P.ftiles.push_back(FTile{(uint32_t)i, t});
     }
+    // Decode blocks, interleaved by tile index across units: the pair tiles a
+    // payload actually has (the low indices) are dispatched first, the blocks
+    // past a unit's pairs (which exit at once) last.
+    P.dtiles.clear();
+    {
+        uint32_t maxt = 0;
+        for (const UnitDev& d : P.units) maxt = std::max(maxt, d.nftiles);
+        for (uint32_t t = 0; t < maxt; ++t)
+            for (int i = 0; i < n; ++i)
+                if (t < P.units[i].nftiles) P.dtiles.push_back(FTile{(uint32_t)i, t});
+    }
     P.coef_extent = coef_cursor ? coef_cursor + kFlatTile : 0;  // slack: flat tiles read whole float4 groups
     build_etiles(P, n);
     if (!P.pipe && P.chunk_req > 0) build_chunks(P, n);
@@ -480,7 +491,8 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         (rc = upload(c, P.d_etiles, P.etiles.data(), sizeof(FTile) * P.etiles.size(), "upload etiles")) ||
         (rc = upload(c, P.d_items, P.items.data(), sizeof(uint32_t) * P.items.size(), "upload items")) ||
         (rc = upload(c, P.d_waits, P.waits.data(), sizeof(uint32_t) * P.waits.size(), "upload waits")) ||
-        (rc = upload(c, P.d_segs, P.segs.data(), sizeof(uint32_t) * P.segs.size(), "upload segs")))
+        (rc = upload(c, P.d_segs, P.segs.data(), sizeof(uint32_t) * P.segs.size(), "upload segs")) ||
+        (rc = upload(c, P.d_dtiles, P.dtiles.data(), sizeof(FTile) * P.dtiles.size(), "upload dtiles")))
         return rc;
     // The host vectors back the async copies: finish them before returning.
     hipError_t e = hipStreamSynchronize(c->stream);
@@ -699,7 +711,7 @@ void wc_ctx_destroy(wc_ctx* c) {
                       &c->ring,      &c->state,     &c->stats,      &c->h_cells,    &c->h_payload,
                       &c->h_packed,  &c->h_offsets, &c->h_poff,    &c->h_kept,     &c->h_out,
                       &c->plan.d_units, &c->plan.d_xtiles, &c->plan.d_ftiles, &c->plan.d_etiles,
-                      &c->plan.d_items, &c->plan.d_waits, &c->plan.d_segs};
+                      &c->plan.d_items, &c->plan.d_waits, &c->plan.d_segs, &c->plan.d_dtiles};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& m : c->marks) {
@@ -852,8 +864,8 @@ int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, c
         return hip_fail(c, e, "memset");
     {
         StageTimer t(c, WC_STAGE_DECODE);
-        e = launch_decode(c->stream, (const UnitDev*)P.d_units.p, (const FTile*)P.d_ftiles.p,
-                          (uint32_t)P.ftiles.size(), d_payload, d_offsets, (uint32_t*)st,
+        e = launch_decode(c->stream, (const UnitDev*)P.d_units.p, (const FTile*)P.d_dtiles.p,
+                          (uint32_t)P.dtiles.size(), d_payload, d_offsets, (uint32_t*)st,
                           (unsigned long long*)(st + round_up(4ull * n, 8)), (float*)c->coef.p,
                           (uint32_t*)c->errflag.p);
     }
