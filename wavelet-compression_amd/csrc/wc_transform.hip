@@ -10,6 +10,8 @@
 // -fno-gpu-flush-denormals-to-zero so subnormals round identically.
 #include "wc_xform.h"
 
+#include <algorithm>
+
 namespace wc {
 
 // Output position of a unit's flat coefficients: 0 the dense flat scratch
@@ -70,6 +72,65 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
     }
 }
 
+// fp32 cells, fast tiles, persistent: a tile of fp32 cells is half the bytes
+// of an fp64 one, so with the LDS-bound 4 tiles per CU the plain kernel keeps
+// too few bytes in flight.  Each workgroup walks tiles t, t + grid, ... and
+// loads tile t + grid's cells into registers before transforming tile t
+// (two column buffers, alternating).
+template <bool KEYS>
+__global__ __launch_bounds__(kThreads) void k_transform_fast_pf(
+    const float* __restrict__ cells, const UnitDev* __restrict__ units, const XTile* __restrict__ tiles,
+    uint32_t ntiles, float* __restrict__ out, int out_mode, unsigned long long* __restrict__ unit_key) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int tid = threadIdx.x;
+    FastCol buf[2];
+    uint32_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    XTile td[2];
+    bool have[2];
+    td[0] = tiles[t];
+    have[0] = fast_load<float>(cells + units[td[0].unit].cell_off, units[td[0].unit], td[0], tid, buf[0]);
+    auto step = [&](int cb) {
+        const int nb = cb ^ 1;
+        const uint32_t tn = t + gridDim.x;
+        have[nb] = false;
+        if (tn < ntiles) {
+            td[nb] = tiles[tn];
+            const UnitDev& Un = units[td[nb].unit];
+            have[nb] = fast_load<float>(cells + Un.cell_off, Un, td[nb], tid, buf[nb]);
+        }
+        const UnitDev& U = units[td[cb].unit];
+        if (have[cb]) fast_butterfly(U, buf[cb], lds, tid);
+        __syncthreads();
+        const uint64_t obase = out_base(U, out_mode);
+        float* __restrict__ dst = out + obase;
+        unsigned long long kmax;
+        if ((obase & 3) == 0) {
+            kmax = xform_fast_p2<KEYS>(U, td[cb], lds, tid,
+                                       [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
+        } else {
+            kmax = xform_fast_p2<KEYS>(U, td[cb], lds, tid, [&](int64_t f, float4 v) {
+                dst[f] = v.x;
+                dst[f + 1] = v.y;
+                dst[f + 2] = v.z;
+                dst[f + 3] = v.w;
+            });
+        }
+        if constexpr (KEYS) {
+            kmax = wave_max_u64(kmax);
+            if (lane_id() == 0 && kmax != 0) atomicMax(unit_key + td[cb].unit, kmax);
+        }
+        __syncthreads();  // LDS rows reused by the next tile
+        t = tn;
+    };
+    for (;;) {
+        step(0);
+        if (t >= ntiles) break;
+        step(1);
+        if (t >= ntiles) break;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Launch wrappers
 size_t transform_lds_bytes(int lbx, int lby, int lbz) {
@@ -102,10 +163,36 @@ hipError_t launch_transform(hipStream_t st, const void* cells, int dtype, const 
     return hipGetLastError();
 }
 
+// Workgroups of k_transform_fast_pf that fit on the device at once.
+static uint32_t pf_grid(size_t lds, bool keys) {
+    static int per_cu[2] = {0, 0}, ncu = 0;
+    const int k = keys ? 1 : 0;
+    if (!per_cu[k]) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        const void* fn = keys ? (const void*)k_transform_fast_pf<true> : (const void*)k_transform_fast_pf<false>;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[k], fn, kThreads, lds) != hipSuccess ||
+            per_cu[k] < 1)
+            per_cu[k] = 2;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+    }
+    return (uint32_t)per_cu[k] * (uint32_t)ncu;
+}
+
 hipError_t launch_transform_fast(hipStream_t st, const void* cells, int dtype, const UnitDev* units,
                                  const XTile* tiles, uint32_t ntiles, size_t lds, float* out,
                                  int out_mode, unsigned long long* keys) {
     if (ntiles == 0) return hipSuccess;
+    if (dtype != 1) {  // fp32 cells: persistent, next tile's cells in flight
+        const uint32_t grid = std::min(ntiles, pf_grid(lds, keys != nullptr));
+        if (keys)
+            k_transform_fast_pf<true><<<grid, kThreads, lds, st>>>((const float*)cells, units, tiles, ntiles, out,
+                                                                 out_mode, keys);
+        else
+            k_transform_fast_pf<false><<<grid, kThreads, lds, st>>>((const float*)cells, units, tiles, ntiles, out,
+                                                                  out_mode, keys);
+        return hipGetLastError();
+    }
     if (dtype == 1) {
         if (keys)
             k_transform_fast<double, true><<<ntiles, kThreads, lds, st>>>((const double*)cells, units, tiles, out,

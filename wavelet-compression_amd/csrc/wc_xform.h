@@ -232,6 +232,78 @@ __device__ __forceinline__ void xform_fast_p1(const T* __restrict__ src, const U
     }
 }
 
+// Split form of the fast phase 1 for a persistent kernel that keeps the next
+// tile's cells in flight while it transforms the current one: a fast tile
+// has at most kThreads columns (kMaxTileBlocks / 4), so a thread owns at most
+// one.  fast_load reads thread tid's column; fast_butterfly transforms it into
+// the LDS rows exactly as xform_fast_p1 does.
+struct FastCol {
+    float v[8][2][2];  // [z plane][dy][dx]
+};
+
+template <typename T>
+__device__ __forceinline__ bool fast_load(const T* __restrict__ src, const UnitDev& U, const XTile& td, int tid,
+                                          FastCol& c) {
+    const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
+    const int TX = 1 << lbx, TY = 1 << lby, TZ = 1 << lbz;
+    const int ci = tid;
+    if (ci >= ((TX * TY * TZ) >> 2)) return false;
+    const int bx = td.bx0 + (ci & (TX - 1)), by = td.by0 + ((ci >> lbx) & (TY - 1));
+    const int bzb = td.bz0 + 4 * (ci >> (lbx + lby));
+    if (bx >= U.hx || by >= U.hy || bzb >= U.hz) return false;
+    const int64_t sy = U.nx, sz = (int64_t)U.nx * U.ny;
+    const bool vec = (U.cell_off & 1) == 0;
+    const T* p0 = src + 2 * (int64_t)bx + sy * (2 * by) + sz * (2 * (int64_t)bzb);
+#pragma unroll
+    for (int zp = 0; zp < 8; ++zp)
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) load_xpair<T>(p0 + sz * zp + sy * dy, true, vec, c.v[zp][dy][0], c.v[zp][dy][1]);
+    return true;
+}
+
+__device__ __forceinline__ void fast_butterfly(const UnitDev& U, const FastCol& col, float* lds, int tid) {
+    const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
+    const int TX = 1 << lbx, TY = 1 << lby, TZ = 1 << lbz;
+    const int rstride = 2 * TZ + 4;
+    const int bxl = tid & (TX - 1), byl = (tid >> lbx) & (TY - 1), bzq = tid >> (lbx + lby);
+    float c[4][2][2][2];  // [q][sz][sy][sx]
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        float a[2][2][2];
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx) {
+                a[0][dy][dx] = haar_lo(col.v[2 * q][dy][dx], col.v[2 * q + 1][dy][dx]);
+                a[1][dy][dx] = haar_hi(col.v[2 * q][dy][dx], col.v[2 * q + 1][dy][dx]);
+            }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            float b[2][2];
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx) {
+                b[0][dx] = haar_lo(a[s][0][dx], a[s][1][dx]);
+                b[1][dx] = haar_hi(a[s][0][dx], a[s][1][dx]);
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                c[q][s][t][0] = haar_lo(b[t][0], b[t][1]);
+                c[q][s][t][1] = haar_hi(b[t][0], b[t][1]);
+            }
+        }
+    }
+#pragma unroll
+    for (int ssz = 0; ssz < 2; ++ssz)
+#pragma unroll
+        for (int ssy = 0; ssy < 2; ++ssy)
+#pragma unroll
+            for (int ssx = 0; ssx < 2; ++ssx) {
+                const int row = ((((ssy << lby) + byl) * 2 + ssx) << lbx) + bxl;
+                *reinterpret_cast<float4*>(lds + row * rstride + (ssz << lbz) + 4 * bzq) =
+                    make_float4(c[0][ssz][ssy][ssx], c[1][ssz][ssy][ssx], c[2][ssz][ssy][ssx], c[3][ssz][ssy][ssx]);
+            }
+}
+
 // Phase 2 of a fast tile: st(flat index within the unit (multiple of 4), float4);
 // with KEYS, returns this thread's max key.
 template <bool KEYS, class Store4>
