@@ -222,4 +222,19 @@ __device__ __forceinline__ uint64_t wave_incl_sum(uint64_t v) {
     return v;
 }
 
+// Workgroup max of a 64-bit key folded into *dst with ONE atomicMax per
+// workgroup (all tiles of a unit update the same key word).  s: 4 LDS
+// slots; contains a barrier (call from uniform control flow).
+__device__ __forceinline__ void block_key_max(unsigned long long v, unsigned long long* s,
+                                              unsigned long long* dst) {
+    v = wave_max_u64(v);
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = s[0];
+        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = s[i] > m ? s[i] : m;
+        if (m != 0) atomicMax(dst, m);
+    }
+}
+
 }  // namespace wc

@@ -37,8 +37,8 @@ __global__ __launch_bounds__(kThreads) void k_transform(
     float* __restrict__ dst = out + out_base(U, out_mode);
     unsigned long long kmax = xform_generic_p2<KEYS>(U, td, lds, threadIdx.x, [&](int64_t f, float v) { dst[f] = v; });
     if constexpr (KEYS) {
-        kmax = wave_max_u64(kmax);
-        if (lane_id() == 0 && kmax != 0) atomicMax(unit_key + td.unit, kmax);
+        __shared__ unsigned long long s_key[kThreads / kWave];
+        block_key_max(kmax, s_key, unit_key + td.unit);
     }
 }
 
@@ -67,8 +67,8 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
         });
     }
     if constexpr (KEYS) {
-        kmax = wave_max_u64(kmax);
-        if (lane_id() == 0 && kmax != 0) atomicMax(unit_key + td.unit, kmax);
+        __shared__ unsigned long long s_key[kThreads / kWave];
+        block_key_max(kmax, s_key, unit_key + td.unit);
     }
 }
 
@@ -82,6 +82,7 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast_pf(
     const float* __restrict__ cells, const UnitDev* __restrict__ units, const XTile* __restrict__ tiles,
     uint32_t ntiles, float* __restrict__ out, int out_mode, unsigned long long* __restrict__ unit_key) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ unsigned long long s_key[kThreads / kWave];
     const int tid = threadIdx.x;
     FastCol buf[2];
     uint32_t t = blockIdx.x;
@@ -116,10 +117,7 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast_pf(
                 dst[f + 3] = v.w;
             });
         }
-        if constexpr (KEYS) {
-            kmax = wave_max_u64(kmax);
-            if (lane_id() == 0 && kmax != 0) atomicMax(unit_key + td[cb].unit, kmax);
-        }
+        if constexpr (KEYS) block_key_max(kmax, s_key, unit_key + td[cb].unit);
         __syncthreads();  // LDS rows reused by the next tile
         t = tn;
     };
