@@ -72,7 +72,7 @@ struct Plan {
     std::vector<UnitDev> units;
     std::vector<XTile> xtiles;
     std::vector<FTile> ftiles, etiles, dtiles;
-    std::vector<uint32_t> items, waits, segs;
+    std::vector<uint32_t> items, waits, segs, eunits;
     int seg_max = 0, seg_min = 0;  // whole-unit emit: WC_OPT_EMIT_SEG_MAX / _MIN_UNITS
     uint32_t ngen = 0, nfast = 0;
     uint64_t coef_extent = 0;  // floats of staged coefficient scratch
@@ -91,7 +91,7 @@ struct Plan {
     std::vector<Chunk> chunks;
     uint64_t slot_floats = 0;
     int nslots = 0;
-    DevBuf d_units, d_xtiles, d_ftiles, d_etiles, d_items, d_waits, d_segs, d_dtiles;
+    DevBuf d_units, d_xtiles, d_ftiles, d_etiles, d_items, d_waits, d_segs, d_dtiles, d_eunits;
 };
 
 int ceil_log2(int64_t v) {
@@ -265,6 +265,15 @@ void build_etiles(Plan& P, int n) {
         for (uint32_t t = 0; t < d.net; ++t) P.etiles.push_back(FTile{(uint32_t)i, t});
     }
     P.state_bytes = round_up(16 + 16ull * n + 8ull * P.etiles.size(), 16);
+    // Dispatch order of the look-back blocks: interleaved by tile index across
+    // units, so the ticket atomics of one unit are spread over the launch
+    // instead of arriving in one burst (units of hundreds of tiles).
+    P.eunits.clear();
+    uint32_t maxt = 0;
+    for (int i = 0; i < n; ++i) maxt = std::max(maxt, P.units[i].net);
+    for (uint32_t t = 0; t < maxt; ++t)
+        for (int i = 0; i < n; ++i)
+            if (t < P.units[i].net) P.eunits.push_back((uint32_t)i);
 }
 
 void build_pipe(Plan& P, int n) {
@@ -492,7 +501,8 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         (rc = upload(c, P.d_items, P.items.data(), sizeof(uint32_t) * P.items.size(), "upload items")) ||
         (rc = upload(c, P.d_waits, P.waits.data(), sizeof(uint32_t) * P.waits.size(), "upload waits")) ||
         (rc = upload(c, P.d_segs, P.segs.data(), sizeof(uint32_t) * P.segs.size(), "upload segs")) ||
-        (rc = upload(c, P.d_dtiles, P.dtiles.data(), sizeof(FTile) * P.dtiles.size(), "upload dtiles")))
+        (rc = upload(c, P.d_dtiles, P.dtiles.data(), sizeof(FTile) * P.dtiles.size(), "upload dtiles")) ||
+        (rc = upload(c, P.d_eunits, P.eunits.data(), sizeof(uint32_t) * P.eunits.size(), "upload eunits")))
         return rc;
     // The host vectors back the async copies: finish them before returning.
     hipError_t e = hipStreamSynchronize(c->stream);
@@ -631,6 +641,7 @@ int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep
     if (e != hipSuccess) return hip_fail(c, e, "transform launch");
     {
         StageTimer t(c, WC_STAGE_EMIT);
+        p.eunits = (const uint32_t*)P.d_eunits.p;
         e = launch_emit(c->stream, p, coef, (uint32_t)P.segs.size(), (uint32_t)P.etiles.size());
     }
     if (e != hipSuccess) return hip_fail(c, e, "emit launch");
@@ -711,7 +722,7 @@ void wc_ctx_destroy(wc_ctx* c) {
                       &c->ring,      &c->state,     &c->stats,      &c->h_cells,    &c->h_payload,
                       &c->h_packed,  &c->h_offsets, &c->h_poff,    &c->h_kept,     &c->h_out,
                       &c->plan.d_units, &c->plan.d_xtiles, &c->plan.d_ftiles, &c->plan.d_etiles,
-                      &c->plan.d_items, &c->plan.d_waits, &c->plan.d_segs, &c->plan.d_dtiles};
+                      &c->plan.d_items, &c->plan.d_waits, &c->plan.d_segs, &c->plan.d_dtiles, &c->plan.d_eunits};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& m : c->marks) {

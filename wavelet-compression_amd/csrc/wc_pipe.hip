@@ -564,7 +564,8 @@ __global__ __launch_bounds__(kThreads, 4) void k_emit(PipeParams P, const float*
         }
     }
     if (tid == 0) {
-        const uint32_t u = P.etiles[P.etile_base + (blockIdx.x - nseg)].unit;
+        const uint32_t b = blockIdx.x - nseg;
+        const uint32_t u = P.eunits ? P.eunits[b] : P.etiles[P.etile_base + b].unit;
         sm[16] = P.units[u].et_begin + atomicAdd(P.tdone + u, 1u);
     }
     __syncthreads();
