@@ -45,17 +45,21 @@ __global__ __launch_bounds__(kThreads) void k_decode(const UnitDev* __restrict__
     __shared__ unsigned long long s_w[4];
     __shared__ unsigned long long s_x[2];
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const uint32_t u = tiles[blockIdx.x].unit;
+    const FTile ft = tiles[blockIdx.x];
+    const uint32_t u = ft.unit;
     const UnitDev& U = units[u];
-    if (tid == 0) s_x[0] = atomicAdd(ticket + u, 1u);
-    __syncthreads();
-    const uint32_t t = (uint32_t)s_x[0];
     const uint8_t* ph = payload + offsets[u];
     int32_t nrle;
     const bool hok = read_header(U, ph, nrle);
     const int64_t n = hok ? nrle : 0;
     const uint32_t ntile = n ? (uint32_t)((n + kFlatTile - 1) / kFlatTile) : 1u;
-    if (t >= ntile) return;  // uniform: no pairs left for this block
+    // The plan launches ceil(ncoeff / kFlatTile) blocks per unit; those whose
+    // plan index is past the payload's pair tiles exit before any atomic.
+    // The others take their tile from the unit's ticket.
+    if (ft.index >= ntile) return;  // uniform
+    if (tid == 0) s_x[0] = atomicAdd(ticket + u, 1u);
+    __syncthreads();
+    const uint32_t t = (uint32_t)s_x[0];
     if (!hok && t == 0 && tid == 0) atomicOr(err, kErrHeader);
 
     // 1. this lane's pairs and their in-wave inclusive sums of (run + 1)
