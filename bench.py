@@ -43,6 +43,9 @@ def parse():
                     help="PMC traffic summary (tools/pmc_summary.py) merged into roofline.traffic")
     ap.add_argument("--pipe", action="store_true", help="run the pipelined single-launch forward (WC_OPT_PIPE)")
     ap.add_argument("--no-inverse", action="store_true", help="skip the inverse-path figures")
+    ap.add_argument("--hist-quantile", type=float, default=None,
+                    help="also time the opt-in global-threshold mode (NOT the reference rule): stage + "
+                         "magnitude histogram, one all-reduce over ranks (RCCL), threshold at this quantile, emit")
     return ap.parse_args()
 
 
@@ -195,6 +198,10 @@ def main():
     if not args.no_inverse:
         out["inverse"] = inverse_figures(args, ctx, capi, units, n, ncells, payload, offsets, kept_total, dev)
 
+    if args.hist_quantile is not None:
+        out["global_hist"] = global_hist_figures(args, ctx, capi, units, n, dtype_code, cells, payload, cap,
+                                                 offsets, kept, dev, world, s_in)
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, cells, payload, offsets, kept, s_in, keep)
 
@@ -203,6 +210,60 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def global_hist_figures(args, ctx, capi, units, n, dtype_code, cells, payload, cap, offsets, kept, dev, world,
+                        s_in):
+    """Opt-in global-threshold mode, timed like the headline step: per step one
+    stage (K1 + histogram), ONE all-reduce of the 4096-bin histogram over all
+    ranks (RCCL over xGMI when world > 1), the threshold on the host, one emit."""
+    import torch
+    import torch.distributed as dist
+    from wavelet_compression_amd.shard import global_threshold
+
+    hist = torch.zeros(capi.HIST_BINS, dtype=torch.int64, device=dev)
+    res = {}
+
+    def step():
+        hist.zero_()
+        t, r = global_threshold(ctx, cells.data_ptr(), dtype_code, units, n, args.hist_quantile, hist)
+        ctx.forward_emit(units, n, 0.0, t, payload.data_ptr(), cap, offsets.data_ptr(), kept.data_ptr())
+        res.update(thresh=t, retained=r)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    ctx.synchronize()
+    ctx.profile_enable(True)
+    ctx.profile_read()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.profile_enable(False)
+    stages = ctx.profile_read()
+    kept_rank = int(kept.sum().item())
+    cells_rank = args.boxes * args.dim ** 3
+    m = {"seconds": elapsed, "kept": kept_rank, "cells": cells_rank}
+    if world > 1:
+        from wavelet_compression_amd.shard import reduce_metrics
+        m = reduce_metrics(m, device=dev)
+    return {
+        "mode": "global histogram threshold (opt-in, not the reference rule)",
+        "quantile": args.hist_quantile, "threshold": res["thresh"],
+        "retained": res["retained"], "kept_check": m["kept"] == res["retained"],
+        "kept_fraction": m["kept"] / m["cells"],
+        "value": m["cells"] * args.steps / m["seconds"], "unit": "cells/s",
+        "ms_per_step": m["seconds"] / args.steps * 1e3,
+        "stage_ms_per_launch": {k: round(ms / cnt, 4) for k, (ms, cnt) in stages.items()},
+        "allreduce": f"{capi.HIST_BINS} x u64 over {world} rank(s)" + (" (RCCL)" if world > 1 else " (none)"),
+    }
 
 
 def inverse_figures(args, ctx, capi, units, n, ncells, payload, offsets, kept_total, dev):

@@ -131,6 +131,36 @@ int wc_forward_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* un
                     double keep, uint8_t* payload, uint64_t payload_capacity,
                     uint64_t* offsets, uint32_t* kept);
 
+/* Opt-in global-threshold mode (NOT the reference's rule; BASELINE north_star's
+ * "keep-percentile histogram + RCCL all-reduce").  The reference thresholds each
+ * box at its own max * (1 - keep) (src/compressor.cpp:212-216); this mode picks
+ * ONE fp32 threshold for a whole run from the coefficient-magnitude histogram
+ * summed over every unit on every rank.  Payload format and decoder unchanged.
+ *
+ *   wc_forward_stage: transform a batch into the context's coefficient scratch
+ *     (the first half of wc_forward) and, when d_hist is not null, ADD the
+ *     batch's magnitude histogram to d_hist (WC_HIST_BINS uint64 on the device;
+ *     bin = fp32 bits of |c| >> WC_HIST_SHIFT, NaN not counted).
+ *   (caller: all-reduce d_hist over ranks, e.g. RCCL sum of 4096 uint64)
+ *   wc_hist_threshold: host-only; the fp32 threshold that keeps every
+ *     coefficient whose bin is >= the highest bin b at which the count of
+ *     coefficients in bins >= b reaches N - floor(quantile * N), N = the total
+ *     count (retained >= (1 - quantile) N, by less than one bin's population).
+ *     *retained receives that count (may be null).
+ *   wc_forward_emit: threshold + pack the staged batch; thresh = NULL applies
+ *     the reference per-unit rule with `keep` (so stage + emit == wc_forward),
+ *     else every coefficient with |c| > *thresh is kept.  Needs the staged
+ *     coefficients of the same units: any other compute call on the context in
+ *     between invalidates them (WC_ERR_INVALID).  Needs the default staged
+ *     forward (WC_OPT_PIPE and WC_OPT_CHUNK off). */
+#define WC_HIST_BINS 4096
+#define WC_HIST_SHIFT 19
+int wc_forward_stage(wc_ctx* ctx, const void* d_cells, int dtype, const wc_unit* units, int n,
+                     uint64_t* d_hist);
+int wc_hist_threshold(const uint64_t* hist, double quantile, float* thresh, uint64_t* retained);
+int wc_forward_emit(wc_ctx* ctx, const wc_unit* units, int n, double keep, const float* thresh,
+                    uint8_t* d_payload, uint64_t payload_capacity, uint64_t* d_offsets, uint32_t* d_kept);
+
 /* Transform only: cells -> flat fp32 coefficients (x-slowest order), written
  * at the same element offsets as the cells (d_flat has the cell buffer's extent). */
 int wc_decompose(wc_ctx* ctx, const void* d_cells, int dtype, const wc_unit* units, int n,
@@ -176,7 +206,8 @@ int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* 
 #define WC_STAGE_RMSE 7       /* K7  */
 #define WC_STAGE_PIPE 8       /* pipelined forward kernel (whole wc_forward) */
 #define WC_STAGE_CHUNKED 9    /* chunked forward, first to last launch (whole wc_forward) */
-#define WC_NUM_STAGES 10
+#define WC_STAGE_HIST 10      /* coefficient-magnitude histogram (wc_forward_stage with d_hist) */
+#define WC_NUM_STAGES 11
 int wc_profile_enable(wc_ctx* ctx, int on);
 int wc_profile_read(wc_ctx* ctx, double* total_ms, uint32_t* launches, int nstages);
 

@@ -188,3 +188,42 @@ def synth_box_f64(seed: int, lo, W: int, H: int, D: int, sigma: float = 0.05) ->
     lib().wco_synth_box_f64(ctypes.c_uint64(seed), int(lo[0]), int(lo[1]), int(lo[2]),
                             W, H, D, float(sigma), _p(out, ctypes.c_double))
     return out
+
+
+# ---- opt-in global-threshold mode (not the reference's rule) -------------
+# numpy restatement of include/wavelet_amd.h's histogram + threshold choice;
+# the payload with a given threshold reuses the reference's mask + rle_encode +
+# serialize (wco_threshold_rle / wco_serialize: src/compressor.cpp:24-80,222-238)
+# with `thresh` in place of max * (1 - keep).
+HIST_BINS, HIST_SHIFT = 4096, 19
+
+
+def magnitude_hist(flat: np.ndarray) -> np.ndarray:
+    bits = np.ascontiguousarray(flat, dtype=np.float32).view(np.uint32) & np.uint32(0x7FFFFFFF)
+    bits = bits[bits <= 0x7F800000]
+    return np.bincount((bits >> HIST_SHIFT).astype(np.int64), minlength=HIST_BINS).astype(np.uint64)
+
+
+def hist_threshold(hist: np.ndarray, quantile: float):
+    """(fp32 threshold, retained) by the rule wc_hist_threshold documents."""
+    h = [int(x) for x in hist]
+    total = sum(h)
+    target = total - min(int(np.floor(quantile * float(total))), total)
+    if target == 0:
+        return float("inf"), 0
+    cum = 0
+    for b in range(HIST_BINS - 1, -1, -1):
+        cum += h[b]
+        if cum >= target:
+            if b == 0:
+                return -1.0, cum
+            return float(np.array([(b << HIST_SHIFT) - 1], np.uint32).view(np.float32)[0]), cum
+    return float("inf"), 0
+
+
+def compress_payload_thresh(box: np.ndarray, thresh: float) -> bytes:
+    """One component's payload with an explicit threshold (|c| > thresh kept)."""
+    b = np.ascontiguousarray(box, dtype=np.float32)
+    W, H, D = _box_dims(b)
+    runs, vals = threshold_rle(wavelet_decompose(b), thresh)
+    return serialize(W, H, D, W * H * D, runs, vals)

@@ -5,6 +5,7 @@ import ctypes
 import re
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -76,3 +77,33 @@ def test_package_has_no_cpu_fallback():
         if f.is_file() and f.suffix in (".py", ".cpp", ".hip", ".h"):
             text = f.read_text()
             assert "oracle" not in text.replace("oracle/", "").lower() or f.name == "__init__.py", f
+
+
+def test_hist_threshold_matches_restatement(wc, oracle):
+    """wc_hist_threshold (host only) against the numpy restatement, including
+    the empty histogram, quantile 0 / 1, bin 0 and the +inf bin."""
+    rng = np.random.default_rng(7)
+    cases = [np.zeros(4096, np.uint64)]
+    h = np.zeros(4096, np.uint64)
+    h[0] = 5
+    h[4080] = 2  # +inf
+    cases.append(h)
+    for _ in range(6):
+        h = np.zeros(4096, np.uint64)
+        idx = rng.integers(0, 4096, 40)
+        h[idx] = rng.integers(1, 10 ** 6, 40).astype(np.uint64)
+        cases.append(h)
+    for h in cases:
+        for q in (0.0, 0.3, 0.5, 0.9, 0.999, 1.0):
+            assert wc.capi.hist_threshold(h, q) == oracle.hist_threshold(h, q), (q, np.nonzero(h))
+    with pytest.raises(wc.WaveletError):
+        wc.capi.hist_threshold(np.zeros(4096, np.uint64), 1.5)
+
+
+def test_hist_threshold_is_exact_on_coefficients(wc, oracle):
+    """Keeping |c| > threshold retains exactly the histogram's retained count."""
+    flat = oracle.wavelet_decompose(oracle.narrow(oracle.synth_box_f64(11, (0, 0, 0), 16, 8, 32)))
+    h = oracle.magnitude_hist(flat)
+    for q in (0.1, 0.7, 0.99):
+        t, r = wc.capi.hist_threshold(h, q)
+        assert int(np.count_nonzero(np.abs(flat) > np.float32(t))) == r

@@ -88,3 +88,78 @@ def test_gloo_two_ranks_reproduce_single_process(wc, oracle):
     assert m["kept"] == kept and m["boxes"] == len(dims)
     assert m["cells"] == sum(w * h * d for (w, h, d) in dims)
     assert m["seconds"] == pytest.approx(0.2) and m["min_value"] == 0.0 and m["max_value"] == 1.0
+
+
+class _OracleStageCtx:
+    """Stands in for capi.Context on a CPU rank: forward_stage adds the oracle's
+    coefficient-magnitude histogram of this rank's units to the hist buffer."""
+
+    def __init__(self, O, units):
+        self.O, self.units = O, units
+
+    def forward_stage(self, d_cells, dtype, units, n, d_hist):
+        import ctypes
+        h = np.ctypeslib.as_array((ctypes.c_uint64 * self.O.HIST_BINS).from_address(d_hist))
+        for cells in self.units:
+            h += self.O.magnitude_hist(self.O.wavelet_decompose(self.O.narrow(cells)))
+
+    def synchronize(self):
+        pass
+
+
+def _hist_worker(rank, world, port, dims, quantile, out_q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(root))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WCAMD_NO_TORCH="1")
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import wcamd  # noqa: F401
+    from wavelet_compression_amd.shard import global_threshold, plan_shards
+    from oracle import oracle as O
+    a, b = plan_shards([w * h * d for (w, h, d) in dims], world)[rank]
+    cells = [O.synth_box_f64(O.unit_seed(0, 0, u, 0), (0, 0, 0), *dims[u]) for u in range(a, b)]
+    hist = torch.zeros(O.HIST_BINS, dtype=torch.int64)
+    thresh, retained = global_threshold(_OracleStageCtx(O, cells), 0, 1, None, b - a, quantile, hist)
+    payloads = {u: O.compress_payload_thresh(O.narrow(c), thresh) for u, c in zip(range(a, b), cells)}
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (thresh, retained, payloads))
+    if rank == 0:
+        out_q.put(gathered)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("quantile", [0.5, 0.9])
+def test_gloo_global_histogram_threshold(wc, oracle, quantile):
+    """Opt-in global-threshold mode over two gloo ranks: one all-reduce of the
+    4096-bin histogram gives every rank the threshold a single process computes
+    over all units, and the kept count equals the histogram's retained count."""
+    import torch.multiprocessing as mp
+    dims = [(16, 16, 16), (8, 4, 2), (32, 16, 8), (6, 10, 14), (16, 32, 64), (3, 5, 7)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hist_worker, args=(r, 2, port, dims, quantile, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    gathered = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    flats = [oracle.wavelet_decompose(oracle.narrow(
+        oracle.synth_box_f64(oracle.unit_seed(0, 0, u, 0), (0, 0, 0), *d))) for u, d in enumerate(dims)]
+    hist = sum(oracle.magnitude_hist(f) for f in flats)
+    thresh, retained = oracle.hist_threshold(hist, quantile)
+    assert wc.capi.hist_threshold(hist, quantile) == (thresh, retained)
+    merged = {}
+    for t, r, p in gathered:
+        assert (t, r) == (thresh, retained)
+        merged.update(p)
+    total = sum(int(f.size) for f in flats)
+    kept = sum(int(np.count_nonzero(np.abs(f.astype(np.float64)) > thresh)) for f in flats)
+    assert kept == retained >= total - int(np.floor(quantile * total))
+    assert merged == {u: oracle.compress_payload_thresh(oracle.narrow(
+        oracle.synth_box_f64(oracle.unit_seed(0, 0, u, 0), (0, 0, 0), *d)), thresh) for u, d in enumerate(dims)}

@@ -195,7 +195,7 @@ int main(int argc, char** argv) {
     double ksum = 0;
     for (uint32_t k : hk) ksum += k;
     const char* names[WC_NUM_STAGES] = {"transform", "flat_count", "unit_scan", "unit_offsets",
-                                        "flat_emit", "decode", "inverse", "rmse", "pipe", "chunked"};
+                                        "flat_emit", "decode", "inverse", "rmse", "pipe", "chunked", "hist"};
     std::printf("{\"boxes\": %d, \"dim\": %d, \"dtype\": \"%s\", \"keep\": %.17g, \"steps\": %d, "
                 "\"ms_per_step\": %.4f, \"cells_per_s\": %.6e, \"kept_fraction\": %.6f, \"payload_bytes\": %llu, "
                 "\"pipe\": %d, \"lag\": %lld, \"ring\": %lld, \"chunk\": %lld, \"slots\": %d, \"seg\": %d, "

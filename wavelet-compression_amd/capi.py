@@ -27,7 +27,8 @@ EXPORTED = (
     "wc_payload_bound", "wc_cell_count", "wc_forward", "wc_forward_host", "wc_decompose",
     "wc_inverse", "wc_inverse_host", "wc_inverse_flat", "wc_rmse", "wc_version",
     "wc_profile_enable", "wc_profile_read", "wc_set_option", "wc_inverse_flat_host", "wc_rmse_host",
-    "wc_decompose_host", "wc_device_count", "wc_pipe_stats",
+    "wc_decompose_host", "wc_device_count", "wc_pipe_stats", "wc_forward_stage", "wc_hist_threshold",
+    "wc_forward_emit",
 )
 WC_OPT_PIPE, WC_OPT_PIPE_LAG, WC_OPT_PIPE_RING = 1, 2, 3
 WC_OPT_PIPE_CLAIM, WC_OPT_PIPE_PREFETCH, WC_OPT_PIPE_WGS, WC_OPT_PIPE_STATS = 4, 5, 6, 7
@@ -36,7 +37,7 @@ WC_OPT_EMIT_SEG_MAX, WC_OPT_EMIT_SEG_MIN_UNITS = 10, 11
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*), kernel names as rocprof shows them.
 STAGES = ("transform", "flat_count", "unit_scan", "unit_offsets", "flat_emit", "decode", "inverse", "rmse",
-          "pipe", "chunked")
+          "pipe", "chunked", "hist")
 
 
 class WcUnit(ctypes.Structure):
@@ -90,6 +91,11 @@ def load_library() -> ctypes.CDLL:
         "wc_decompose_host": (i32, [vp, vp, i32, up, i32, vp]),
         "wc_profile_read": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32), i32]),
         "wc_pipe_stats": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), i32]),
+        "wc_forward_stage": (i32, [vp, vp, i32, up, i32, vp]),
+        "wc_hist_threshold": (i32, [vp, ctypes.c_double, ctypes.POINTER(ctypes.c_float),
+                                    ctypes.POINTER(ctypes.c_uint64)]),
+        "wc_forward_emit": (i32, [vp, up, i32, ctypes.c_double, ctypes.POINTER(ctypes.c_float), vp, u64,
+                                  vp, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -226,6 +232,20 @@ class Context:
                                        float(keep), ctypes.c_void_p(d_payload), capacity,
                                        ctypes.c_void_p(d_offsets), ctypes.c_void_p(d_kept)))
 
+    def forward_stage(self, d_cells: int, dtype: int, units, n: int, d_hist: int | None = None):
+        """Global-threshold mode, step 1 (include/wavelet_amd.h): transform into
+        the context scratch; add the magnitude histogram to d_hist if given."""
+        self._check(self._L.wc_forward_stage(self._h, ctypes.c_void_p(d_cells), dtype, units, n,
+                                             ctypes.c_void_p(d_hist or 0)))
+
+    def forward_emit(self, units, n: int, keep: float, thresh: float | None, d_payload: int,
+                     capacity: int, d_offsets: int, d_kept: int):
+        """Step 2: pack the staged batch with one fp32 threshold (None: the
+        reference's per-unit rule with `keep`)."""
+        t = None if thresh is None else ctypes.byref(ctypes.c_float(thresh))
+        self._check(self._L.wc_forward_emit(self._h, units, n, float(keep), t, ctypes.c_void_p(d_payload),
+                                            capacity, ctypes.c_void_p(d_offsets), ctypes.c_void_p(d_kept)))
+
     def decompose(self, d_cells: int, dtype: int, units, n: int, d_flat: int):
         self._check(self._L.wc_decompose(self._h, ctypes.c_void_p(d_cells), dtype, units, n,
                                          ctypes.c_void_p(d_flat)))
@@ -286,6 +306,24 @@ class Context:
         self._check(self._L.wc_inverse_host(self._h, p.ctypes.data, o.ctypes.data, units, n,
                                             out.ctypes.data))
         return out[:extent]
+
+
+HIST_BINS = 4096  # WC_HIST_BINS
+HIST_SHIFT = 19   # WC_HIST_SHIFT
+
+
+def hist_threshold(hist: np.ndarray, quantile: float):
+    """wc_hist_threshold (host only): (fp32 threshold, retained count) for an
+    all-reduced WC_HIST_BINS uint64 histogram."""
+    h = np.ascontiguousarray(hist, dtype=np.uint64)
+    if h.size != HIST_BINS:
+        raise ValueError(f"histogram must have {HIST_BINS} bins")
+    t = ctypes.c_float()
+    r = ctypes.c_uint64()
+    rc = load_library().wc_hist_threshold(h.ctypes.data, float(quantile), ctypes.byref(t), ctypes.byref(r))
+    if rc:
+        raise WaveletError(rc, "wc_hist_threshold: invalid argument")
+    return float(t.value), int(r.value)
 
 
 def unit_payload(payload: np.ndarray, offsets: np.ndarray, kept: np.ndarray, u: int) -> bytes:

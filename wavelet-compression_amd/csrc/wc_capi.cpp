@@ -20,6 +20,7 @@
 #include "wc_internal.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -44,6 +45,8 @@ hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDe
                        uint32_t, double*, double*);
 hipError_t launch_forward_pipe(hipStream_t, int, size_t, uint32_t, const PipeParams&);
 hipError_t launch_emit(hipStream_t, const PipeParams&, const float*, uint32_t, uint32_t);
+hipError_t launch_hist(hipStream_t, const UnitDev*, const FTile*, uint32_t, const float*, uint32_t*, uint32_t,
+                       unsigned long long*);
 size_t chunk_lds_bytes(size_t tile_lds);
 hipError_t launch_chunk(hipStream_t, int, size_t, const PipeParams&, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
                         uint32_t);
@@ -121,8 +124,12 @@ struct wc_ctx {
     int opt_seg_max = 0;     // WC_OPT_EMIT_SEG_MAX (0: look-back tiles only, the faster layout measured)
     int opt_seg_min = 256;   // WC_OPT_EMIT_SEG_MIN_UNITS
     bool err_check_pending = false;
+    // wc_forward_stage left this plan's coefficients + unit keys in coef/state
+    // (cleared by set_device, i.e. by every other compute entry point)
+    bool staged = false;
+    uint64_t plan_gen = 0;  // bumped whenever get_plan rebuilds the plan
     // scratch (grow-only)
-    DevBuf coef, part, errflag, ring, state, stats;
+    DevBuf coef, part, errflag, ring, state, stats, hist_rows;
     // host-path staging
     DevBuf h_cells, h_payload, h_packed, h_offsets, h_poff, h_kept, h_out;
     // per-kernel event timing (wc_profile_enable / wc_profile_read)
@@ -412,6 +419,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         (int)P.key.size() == n && (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0))
         return WC_OK;
     c->plan_valid = false;
+    ++c->plan_gen;
     P.key.assign(units, units + n);
     P.pipe = c->opt_pipe;
     P.items.clear();
@@ -537,6 +545,7 @@ int ensure_pipe_scratch(wc_ctx* c) {
 }
 
 int set_device(wc_ctx* c) {
+    c->staged = false;
     hipError_t e = hipSetDevice(c->device);
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "hipSetDevice");
 }
@@ -621,31 +630,48 @@ int forward_pipe(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, 
     return WC_OK;
 }
 
-int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
-                   uint64_t* d_offsets, uint32_t* d_kept) {
+// Staged forward, first half: K1 transform into the flat coefficient
+// scratch + per-unit max keys (zeroed state).
+int stage_transform(wc_ctx* c, const void* d_cells, int dtype) {
     Plan& P = c->plan;
     const UnitDev* du = (const UnitDev*)P.d_units.p;
     const XTile* dxt = (const XTile*)P.d_xtiles.p;
     hipError_t e = hipSuccess;
     if ((e = hipMemsetAsync(c->state.p, 0, P.state_bytes, c->stream)) != hipSuccess)
         return hip_fail(c, e, "memset state");
-    PipeParams p = pipe_params(c, d_cells, n, keep, d_payload, d_offsets, d_kept);
+    unsigned long long* key = (unsigned long long*)((uint8_t*)c->state.p + 16);
     float* coef = (float*)c->coef.p;
     {
         StageTimer t(c, WC_STAGE_TRANSFORM);
-        e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, coef, 0, p.key);
+        e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, coef, 0, key);
         if (e == hipSuccess)
             e = launch_transform_fast(c->stream, d_cells, dtype, du, dxt + P.ngen, P.nfast, P.lds_fast, coef, 0,
-                                      p.key);
+                                      key);
     }
-    if (e != hipSuccess) return hip_fail(c, e, "transform launch");
-    {
-        StageTimer t(c, WC_STAGE_EMIT);
-        p.eunits = (const uint32_t*)P.d_eunits.p;
-        e = launch_emit(c->stream, p, coef, (uint32_t)P.segs.size(), (uint32_t)P.etiles.size());
+    return e == hipSuccess ? WC_OK : hip_fail(c, e, "transform launch");
+}
+
+// Second half: K2 threshold + ordered pack of the staged coefficients
+// (gthresh: the global-threshold mode's fp32 threshold, or null).
+int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_payload, uint64_t* d_offsets,
+               uint32_t* d_kept) {
+    Plan& P = c->plan;
+    PipeParams p = pipe_params(c, nullptr, n, keep, d_payload, d_offsets, d_kept);
+    if (gthresh) {
+        p.use_gthresh = 1;
+        p.gthresh = *gthresh;
     }
-    if (e != hipSuccess) return hip_fail(c, e, "emit launch");
-    return WC_OK;
+    p.eunits = (const uint32_t*)P.d_eunits.p;
+    StageTimer t(c, WC_STAGE_EMIT);
+    hipError_t e = launch_emit(c->stream, p, (const float*)c->coef.p, (uint32_t)P.segs.size(),
+                               (uint32_t)P.etiles.size());
+    return e == hipSuccess ? WC_OK : hip_fail(c, e, "emit launch");
+}
+
+int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
+                   uint64_t* d_offsets, uint32_t* d_kept) {
+    int rc = stage_transform(c, d_cells, dtype);
+    return rc ? rc : stage_emit(c, n, keep, nullptr, d_payload, d_offsets, d_kept);
 }
 
 // Chunked forward: launch k transforms chunk k into slot k % nslots and packs
@@ -836,6 +862,87 @@ int wc_forward(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, 
     }
     if ((rc = ensure_scratch(c))) return rc;
     return forward_staged(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
+}
+
+int wc_forward_stage(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, int n, uint64_t* d_hist) {
+    if (!c) return WC_ERR_INVALID;
+    int rc;
+    if ((rc = validate_units(c, units, n))) return rc;
+    if (dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
+    if (n == 0) return WC_OK;
+    if (!d_cells) return fail(c, WC_ERR_INVALID, "null buffer");
+    if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
+    if (c->plan.pipe || !c->plan.chunks.empty())
+        return fail(c, WC_ERR_INVALID, "wc_forward_stage needs the staged forward (WC_OPT_PIPE / WC_OPT_CHUNK off)");
+    if ((rc = ensure_scratch(c)) || (rc = stage_transform(c, d_cells, dtype))) return rc;
+    if (d_hist) {
+        const uint32_t nrows = 1024;  // 4 workgroups per CU; rows = 16 MiB of u32 bins
+        if ((rc = ensure(c, c->hist_rows, sizeof(uint32_t) * WC_HIST_BINS * nrows))) return rc;
+        const Plan& P = c->plan;
+        StageTimer t(c, WC_STAGE_HIST);
+        hipError_t e = launch_hist(c->stream, (const UnitDev*)P.d_units.p, (const FTile*)P.d_ftiles.p,
+                                   (uint32_t)P.ftiles.size(), (const float*)c->coef.p, (uint32_t*)c->hist_rows.p,
+                                   nrows, (unsigned long long*)d_hist);
+        if (e != hipSuccess) return hip_fail(c, e, "histogram launch");
+    }
+    c->staged = true;
+    return WC_OK;
+}
+
+int wc_hist_threshold(const uint64_t* hist, double quantile, float* thresh, uint64_t* retained) {
+    if (!hist || !thresh || !(quantile >= 0.0 && quantile <= 1.0)) return WC_ERR_INVALID;
+    uint64_t total = 0;
+    for (int b = 0; b < WC_HIST_BINS; ++b) total += hist[b];
+    const uint64_t drop = (uint64_t)std::floor(quantile * (double)total);
+    const uint64_t target = total - std::min(drop, total);
+    uint64_t cum = 0;
+    int bstar = -1;  // -1: keep nothing
+    if (target > 0)
+        for (int b = WC_HIST_BINS - 1; b >= 0; --b) {
+            cum += hist[b];
+            if (cum >= target) {
+                bstar = b;
+                break;
+            }
+        }
+    float t;
+    if (bstar < 0) {
+        t = __builtin_inff();  // |c| > inf never holds
+        cum = 0;
+    } else if (bstar == 0) {
+        t = -1.0f;  // every non-NaN coefficient
+    } else {
+        const uint32_t bits = ((uint32_t)bstar << WC_HIST_SHIFT) - 1u;
+        std::memcpy(&t, &bits, 4);
+    }
+    *thresh = t;
+    if (retained) *retained = cum;
+    return WC_OK;
+}
+
+int wc_forward_emit(wc_ctx* c, const wc_unit* units, int n, double keep, const float* thresh, uint8_t* d_payload,
+                    uint64_t cap, uint64_t* d_offsets, uint32_t* d_kept) {
+    if (!c) return WC_ERR_INVALID;
+    int rc;
+    if ((rc = validate_units(c, units, n))) return rc;
+    if (n == 0) return WC_OK;
+    if (!d_payload || !d_offsets || !d_kept) return fail(c, WC_ERR_INVALID, "null buffer");
+    if (cap < wc_payload_bound(units, n)) return fail(c, WC_ERR_INVALID, "payload_capacity < wc_payload_bound");
+    const bool staged = c->staged;
+    const uint64_t gen = c->plan_gen;
+    if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
+    // get_plan keeps the cached plan (and so the staged scratch) only for the same units
+    if (!staged || gen != c->plan_gen || c->plan.pipe || !c->plan.chunks.empty())
+        return fail(c, WC_ERR_INVALID, "wc_forward_emit: no staged coefficients for these units (wc_forward_stage)");
+    // per-unit tile tickets (tdone) and look-back status words are per call:
+    // zero everything after the unit keys
+    const Plan& P = c->plan;
+    const size_t st_off = 16 + 8ull * n;
+    hipError_t e = hipMemsetAsync((uint8_t*)c->state.p + st_off, 0, P.state_bytes - st_off, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "memset status");
+    if ((rc = stage_emit(c, n, keep, thresh, d_payload, d_offsets, d_kept))) return rc;
+    c->staged = true;  // the coefficients are still there: emit again with another threshold
+    return WC_OK;
 }
 
 int wc_decompose(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, int n, float* d_flat) {

@@ -113,6 +113,8 @@ struct PipeParams {
     uint32_t seg_base;             // k_emit: first entry of segs in this launch
     uint32_t etile_base;           // k_emit: first look-back emit tile of this launch
     uint32_t ring_coefs;           // k_emit: 1 = coefficients at ring_off (chunk slots), 0 = coef_off
+    uint32_t use_gthresh;          // 1: every unit uses gthresh (global histogram mode), 0: reference rule
+    float gthresh;                 // fp32 threshold: keep |c| > gthresh
 };
 
 }  // namespace wc

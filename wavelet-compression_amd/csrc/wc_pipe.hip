@@ -63,6 +63,13 @@ __device__ __forceinline__ float4 ring_ld4(__amdgpu_buffer_rsrc_t r, uint32_t by
     return make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z), __uint_as_float(d.w));
 }
 
+// fp32 keep threshold of a unit: the reference rule from the unit's max key
+// (src/compressor.cpp:212-216), or the one global threshold of the opt-in
+// histogram mode (wc_forward_emit with a threshold).
+__device__ __forceinline__ float unit_thresh(const PipeParams& P, unsigned long long key) {
+    return P.use_gthresh ? P.gthresh : thresh_as_float(key_thresh(key, P.keep));
+}
+
 __device__ __forceinline__ unsigned long long now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
 // ---------------------------------------------------------------------------
@@ -249,7 +256,7 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
         }
     }
     __syncthreads();
-    const float tf = thresh_as_float(key_thresh(smk[0], P.keep));
+    const float tf = unit_thresh(P, smk[0]);
     const uint32_t start = ft.index * (uint32_t)kEmitTile;
     const uint32_t len = (uint32_t)min((uint64_t)kEmitTile, U.ncells - start);
 
@@ -374,7 +381,7 @@ __device__ __forceinline__ void pipe_emit_unit(const PipeParams& P, __amdgpu_buf
         if (P.stats) st[kStEWait] += now_ticks() - t0;
     }
     __syncthreads();
-    const float tf = thresh_as_float(key_thresh(smk[0], P.keep));
+    const float tf = unit_thresh(P, smk[0]);
     const uint32_t nc = (uint32_t)U.ncells;
     const uint32_t nch = (nc + kEmitTile - 1) / kEmitTile;
     const uint32_t rbase = 4u * (uint32_t)U.ring_off;
@@ -525,7 +532,7 @@ __device__ __forceinline__ void emit_seg(const PipeParams& P, const float* __res
                                          uint32_t* sm, uint2* stage, int tid) {
     const UnitDev& U = P.units[u];
     const int w = tid >> 6, l = tid & 63;
-    const float tf = thresh_as_float(key_thresh(P.key[u], P.keep));
+    const float tf = unit_thresh(P, P.key[u]);
     const uint32_t nc = (uint32_t)U.ncells;
     const uint32_t nch = (nc + kEmitTile - 1) / kEmitTile;
     const float4* __restrict__ p4 = reinterpret_cast<const float4*>(coef + (P.ring_coefs ? U.ring_off : U.coef_off));

@@ -57,3 +57,27 @@ def reduce_metrics(local: Dict[str, float], group=None, device=None) -> Dict[str
         dist.all_reduce(t, op=op, group=group)
         out.update({k: float(v) for k, v in zip(ks, t.tolist())})
     return out
+
+
+def global_threshold(ctx, d_cells: int, dtype: int, units, n: int, quantile: float, hist, group=None):
+    """Opt-in global-threshold mode (include/wavelet_amd.h wc_forward_stage):
+    transform this rank's units, add their coefficient-magnitude histogram to
+    `hist` (a zeroed int64 torch tensor of capi.HIST_BINS bins on this rank's
+    device, reinterpreted as uint64 by the library), sum it over ranks with ONE
+    all-reduce (RCCL over xGMI on GPUs, gloo on CPU) and return
+    (fp32 threshold, retained count over all ranks).  Follow with
+    ctx.forward_emit(units, n, keep, threshold, ...).
+
+    Not the reference's rule (a per-box max threshold, src/compressor.cpp:212-216):
+    the retained index set differs from the reference by design."""
+    import numpy as np
+    import torch.distributed as dist
+
+    from . import capi
+
+    ctx.forward_stage(d_cells, dtype, units, n, hist.data_ptr())
+    ctx.synchronize()  # the context stream may not be the collective's stream
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+    h = hist.cpu().numpy().view(np.uint64)
+    return capi.hist_threshold(h, quantile)
