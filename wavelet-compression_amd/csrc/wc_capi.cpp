@@ -45,7 +45,7 @@ hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDe
                        uint32_t, double*, double*);
 hipError_t launch_forward_pipe(hipStream_t, int, size_t, uint32_t, const PipeParams&);
 hipError_t launch_emit(hipStream_t, const PipeParams&, const float*, uint32_t, uint32_t);
-hipError_t launch_hist(hipStream_t, const UnitDev*, const FTile*, uint32_t, const float*, uint32_t*, uint32_t,
+hipError_t launch_hist(hipStream_t, const UnitDev*, const FTile*, uint32_t, const float*, uint32_t,
                        unsigned long long*);
 size_t chunk_lds_bytes(size_t tile_lds);
 hipError_t launch_chunk(hipStream_t, int, size_t, const PipeParams&, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
@@ -129,7 +129,7 @@ struct wc_ctx {
     bool staged = false;
     uint64_t plan_gen = 0;  // bumped whenever get_plan rebuilds the plan
     // scratch (grow-only)
-    DevBuf coef, part, errflag, ring, state, stats, hist_rows;
+    DevBuf coef, part, errflag, ring, state, stats;
     // host-path staging
     DevBuf h_cells, h_payload, h_packed, h_offsets, h_poff, h_kept, h_out;
     // per-kernel event timing (wc_profile_enable / wc_profile_read)
@@ -876,13 +876,12 @@ int wc_forward_stage(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* u
         return fail(c, WC_ERR_INVALID, "wc_forward_stage needs the staged forward (WC_OPT_PIPE / WC_OPT_CHUNK off)");
     if ((rc = ensure_scratch(c)) || (rc = stage_transform(c, d_cells, dtype))) return rc;
     if (d_hist) {
-        const uint32_t nrows = 1024;  // 4 workgroups per CU; rows = 16 MiB of u32 bins
-        if ((rc = ensure(c, c->hist_rows, sizeof(uint32_t) * WC_HIST_BINS * nrows))) return rc;
+        const uint32_t max_blocks = 2048;  // 8 workgroups per CU, 256 CUs
         const Plan& P = c->plan;
         StageTimer t(c, WC_STAGE_HIST);
         hipError_t e = launch_hist(c->stream, (const UnitDev*)P.d_units.p, (const FTile*)P.d_ftiles.p,
-                                   (uint32_t)P.ftiles.size(), (const float*)c->coef.p, (uint32_t*)c->hist_rows.p,
-                                   nrows, (unsigned long long*)d_hist);
+                                   (uint32_t)P.ftiles.size(), (const float*)c->coef.p, max_blocks,
+                                   (unsigned long long*)d_hist);
         if (e != hipSuccess) return hip_fail(c, e, "histogram launch");
     }
     c->staged = true;

@@ -15,8 +15,8 @@
 // the strict test the emit kernels already apply.
 //
 // HBM-bound: one 16-B load per 4 coefficients (4 B/coefficient read), LDS
-// privatized bins per workgroup, per-workgroup rows written once and summed
-// column-wise by a second small kernel (no global atomics, deterministic).
+// privatized bins per workgroup, one 64-bit global atomic per nonzero bin per
+// workgroup at the end.
 #include "wc_device.h"
 
 namespace wc {
@@ -27,20 +27,40 @@ constexpr int kHistBins = 4096;
 constexpr int kHistShift = 19;
 constexpr int kHistThreads = 256;
 
-__device__ __forceinline__ void hist_add(uint32_t* h, float v) {
-    const uint32_t b = __float_as_uint(v) & 0x7fffffffu;
-    if (b <= 0x7f800000u) atomicAdd(h + (b >> kHistShift), 1u);
+// Wave-aggregated LDS increment: the coefficients of a box crowd into a few
+// bins (the detail bands of smooth data), and same-address LDS atomics of one
+// wave serialize.  kPeel rounds each take the bin of the first pending
+// lane, count every lane with that bin by ballot and add the count with ONE
+// atomic; lanes still pending after that add their own.
+constexpr int kPeel = 1;
+
+__device__ __forceinline__ void hist_add(uint32_t* h, float v, bool valid) {
+    const uint32_t m = __float_as_uint(v) & 0x7fffffffu;
+    const uint32_t bin = m >> kHistShift;
+    bool pending = valid && m <= 0x7f800000u;  // NaN is not counted
+#pragma unroll
+    for (int r = 0; r < kPeel; ++r) {
+        const unsigned long long act = __ballot(pending);
+        if (!act) return;
+        const int leader = __ffsll((long long)act) - 1;
+        const uint32_t lb = __builtin_amdgcn_readlane(bin, leader);
+        const unsigned long long same = __ballot(pending && bin == lb);
+        if ((int)(threadIdx.x & 63) == leader) atomicAdd(h + lb, (uint32_t)__popcll(same));
+        pending = pending && bin != lb;
+    }
+    if (pending) atomicAdd(h + bin, 1u);
 }
 
 }  // namespace
 
 // Workgroup g folds flat tiles g, g + G, ... (kFlatTile coefficients of one
-// unit each, in the staged flat scratch at coef + coef_off) into its LDS bins
-// and writes them as row g of rows[G][kHistBins].
-__global__ __launch_bounds__(kHistThreads) void k_hist_rows(const UnitDev* __restrict__ units,
-                                                          const FTile* __restrict__ ftiles, uint32_t nftiles,
-                                                          const float* __restrict__ coef,
-                                                          uint32_t* __restrict__ rows) {
+// unit each, in the staged flat scratch at coef + coef_off) into its LDS bins,
+// then adds its nonzero bins to hist with 64-bit atomics (integer sums: the
+// result does not depend on their order).
+__global__ __launch_bounds__(kHistThreads) void k_hist(const UnitDev* __restrict__ units,
+                                                     const FTile* __restrict__ ftiles, uint32_t nftiles,
+                                                     const float* __restrict__ coef,
+                                                     unsigned long long* __restrict__ hist) {
     __shared__ uint32_t h[kHistBins];
     for (int i = threadIdx.x; i < kHistBins; i += kHistThreads) h[i] = 0u;
     __syncthreads();
@@ -51,36 +71,32 @@ __global__ __launch_bounds__(kHistThreads) void k_hist_rows(const UnitDev* __res
         const uint32_t len = (uint32_t)min((uint64_t)kFlatTile, U.ncells - start);
         // coef_off is 16-B aligned and kFlatTile a multiple of 4: float4 loads
         const float4* __restrict__ p4 = reinterpret_cast<const float4*>(coef + U.coef_off + start);
-#pragma unroll 4
-        for (uint32_t q = threadIdx.x; 4 * q < len; q += kHistThreads) {
-            const float4 v = p4[q];
-            const uint32_t e = 4 * q;
-            hist_add(h, v.x);
-            if (e + 1 < len) hist_add(h, v.y);
-            if (e + 2 < len) hist_add(h, v.z);
-            if (e + 3 < len) hist_add(h, v.w);
+        constexpr int kIt = kFlatTile / (4 * kHistThreads);  // 4: every load of the tile in flight at once
+        float4 v[kIt];
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+            const uint32_t q = it * kHistThreads + threadIdx.x;
+            v[it] = 4 * q < len ? p4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+            const uint32_t e = 4 * (it * kHistThreads + threadIdx.x);
+            hist_add(h, v[it].x, e < len);
+            hist_add(h, v[it].y, e + 1 < len);
+            hist_add(h, v[it].z, e + 2 < len);
+            hist_add(h, v[it].w, e + 3 < len);
         }
     }
     __syncthreads();
-    uint32_t* row = rows + (uint64_t)blockIdx.x * kHistBins;
-    for (int i = threadIdx.x; i < kHistBins; i += kHistThreads) row[i] = h[i];
-}
-
-// hist[b] += sum over rows of rows[r][b]: one thread per bin, coalesced rows.
-__global__ __launch_bounds__(kHistThreads) void k_hist_sum(const uint32_t* __restrict__ rows, uint32_t nrows,
-                                                         unsigned long long* __restrict__ hist) {
-    const int b = blockIdx.x * kHistThreads + threadIdx.x;
-    unsigned long long s = 0;
-    for (uint32_t r = 0; r < nrows; ++r) s += rows[(uint64_t)r * kHistBins + b];
-    hist[b] += s;
+    for (int i = threadIdx.x; i < kHistBins; i += kHistThreads)
+        if (h[i]) atomicAdd(hist + i, (unsigned long long)h[i]);
 }
 
 hipError_t launch_hist(hipStream_t st, const UnitDev* units, const FTile* ftiles, uint32_t nftiles,
-                       const float* coef, uint32_t* rows, uint32_t nrows, unsigned long long* hist) {
+                       const float* coef, uint32_t max_blocks, unsigned long long* hist) {
     if (nftiles == 0) return hipSuccess;
-    const uint32_t g = nftiles < nrows ? nftiles : nrows;
-    k_hist_rows<<<g, kHistThreads, 0, st>>>(units, ftiles, nftiles, coef, rows);
-    k_hist_sum<<<kHistBins / kHistThreads, kHistThreads, 0, st>>>(rows, g, hist);
+    const uint32_t g = nftiles < max_blocks ? nftiles : max_blocks;
+    k_hist<<<g, kHistThreads, 0, st>>>(units, ftiles, nftiles, coef, hist);
     return hipGetLastError();
 }
 
