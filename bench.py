@@ -152,6 +152,19 @@ def main():
     achieved = alg_bytes_stage.get(dominant, 0) / (dom_ms * 1e-3) / 1e9
     path_ms = sum(v[0] for v in per_launch.values())
     path_bytes = s_in * ncells + 8 * kept_step + 20 * n
+    # Reference point for "achievable": a device-to-device copy of the cell
+    # buffer (torch's copy kernel, read + write bytes per second).
+    scratch = torch.empty_like(cells)
+    scratch.copy_(cells)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(5):
+        scratch.copy_(cells)
+    ev1.record()
+    torch.cuda.synchronize()
+    copy_gbps = 2 * cells.numel() * cells.element_size() * 5 / (ev0.elapsed_time(ev1) * 1e-3) / 1e9
+    del scratch
     traffic = None
     pmc_path = Path(args.pmc)
     if pmc_path.exists():
@@ -188,6 +201,9 @@ def main():
             "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBPS,
             "traffic": traffic,
+            # HBM bytes the kernel actually moved (PMC, incl. the fp32 coefficient staging) per second
+            "traffic_GBps": (traffic / (dom_ms * 1e-3) / 1e9) if traffic else None,
+            "copy_GBps": copy_gbps,
         },
         "roofline_path": {"achieved": path_bytes / (path_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS,
                           "unit": "GB/s", "frac": path_bytes / (path_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,

@@ -106,6 +106,9 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports kernel-side errors of earlier 
                                    whole by one workgroup each, no look-back (default 0 = never: the
                                    look-back tiles measured faster) */
 #define WC_OPT_EMIT_SEG_MIN_UNITS 11 /* ... when the batch holds at least this many of them (default 256) */
+#define WC_OPT_SPARSE 12        /* staged forward (default 1): K1 stores only the 32-coefficient flat segments
+                                   that hold some |c| > (tile max) * (1 - keep) and flags them; the emit loads
+                                   only flagged segments.  Same bytes out; 0 = dense staging */
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 
 /* Diagnostics of the pipelined kernel (WC_OPT_PIPE_STATS on): summed over

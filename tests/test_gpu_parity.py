@@ -40,6 +40,7 @@ def set_path(ctx, path, lag=0, ring=0):
     ctx.set_pipe(path == "pipe", lag=lag, ring=ring)
     ctx.set_chunk(16384 if path == "chunked" else 0, slots=2)
     ctx.set_emit_seg(64 if path == "seg" else 0, 1)
+    ctx.set_option(12, 0 if path == "dense" else 1)  # WC_OPT_SPARSE
 
 
 def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None, path="staged", lag=0, ring=0):
@@ -58,10 +59,10 @@ def oracle_payload(O, b, keep):
 
 
 # Forward paths, all byte-identical: the library default (look-back emit
-# tiles); whole-unit emit forced for units of <= 64 tiles, beside look-back
+# tiles, sparse staging of 32-coefficient segments); "dense" staging (WC_OPT_SPARSE 0); whole-unit emit forced for units of <= 64 tiles, beside look-back
 # tiles for larger units in the same launch; chunked two-stream (16 Ki-cell
 # chunks, 2 coefficient slots); the pipelined single launch.
-PATHS = ["staged", "seg", "chunked", "pipe"]
+PATHS = ["staged", "dense", "seg", "chunked", "pipe"]
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -456,3 +457,26 @@ def test_gpu_matches_committed_golden_fixtures(wc, ctx, path):
         regen = wc.decompress_payloads(got)
         for i, c in enumerate(cases):
             assert regen[i].tobytes() == z[c["name"] + "/regen"].tobytes(), c["name"]
+
+
+SPARSE_DIMS = [(64, 64, 64), (16, 32, 64), (32, 8, 128), (64, 64, 64), (8, 2, 64), (64, 64, 64)]
+
+
+@pytest.mark.parametrize("keep", [float(np.float32(k)) for k in (0.999, 0.5, 1.0, 1.5)])
+def test_sparse_staging_sign_and_keep_edges(wc, ctx, oracle, keep):
+    """Sparse staging (32-coefficient flat segments, D % 64 == 0 units) against
+    the oracle where its tile bound matters: a unit whose signed max is NEGATIVE
+    in one tile while the other tiles are positive (thresh < 0: every
+    coefficient kept, re-staged densely), an all-negative field, keep = 1
+    (thresh 0) and keep > 1 (thresh < 0 for positive maxima)."""
+    boxes = synth(oracle, SPARSE_DIMS, seed0=9)
+    boxes[1] = -boxes[1]                       # all-negative field
+    boxes[3] = boxes[3].copy()
+    boxes[3][40, 40, 40] = -1.0e6              # one negative spike: signed max < 0
+    boxes[5] = boxes[5].copy()
+    boxes[5][:, :, :] *= 1e-3
+    boxes[5][3, 3, 3] = 2.0e4                  # one positive spike far above the rest
+    for path in ("staged", "dense"):
+        got, _ = gpu_payloads(wc, ctx, boxes, keep, path=path)
+        for i, b in enumerate(boxes):
+            assert got[i] == oracle_payload(oracle, b, keep), f"{path} unit {i} dims {SPARSE_DIMS[i]} keep {keep}"

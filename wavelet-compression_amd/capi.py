@@ -34,6 +34,7 @@ WC_OPT_PIPE, WC_OPT_PIPE_LAG, WC_OPT_PIPE_RING = 1, 2, 3
 WC_OPT_PIPE_CLAIM, WC_OPT_PIPE_PREFETCH, WC_OPT_PIPE_WGS, WC_OPT_PIPE_STATS = 4, 5, 6, 7
 WC_OPT_CHUNK, WC_OPT_CHUNK_SLOTS = 8, 9
 WC_OPT_EMIT_SEG_MAX, WC_OPT_EMIT_SEG_MIN_UNITS = 10, 11
+WC_OPT_SPARSE = 12
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*), kernel names as rocprof shows them.
 STAGES = ("transform", "flat_count", "unit_scan", "unit_offsets", "flat_emit", "decode", "inverse", "rmse",

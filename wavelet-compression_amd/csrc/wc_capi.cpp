@@ -35,7 +35,9 @@ uint32_t pipe_grid(int dtype, size_t lds, int max_per_cu);
 hipError_t launch_transform(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
                             float*, int, unsigned long long*);
 hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
-                                 float*, int, unsigned long long*);
+                                 float*, int, unsigned long long*, uint8_t*, double);
+hipError_t launch_transform_fallback(hipStream_t, const void*, int, const UnitDev*, int, const XTile*, size_t, float*,
+                                     const unsigned long long*, double);
 hipError_t launch_pack(hipStream_t, const UnitDev*, int, const uint32_t*, const uint8_t*, uint64_t*, uint8_t*);
 hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, const uint8_t*, const uint64_t*,
                          uint32_t*, unsigned long long*, float*, uint32_t*);
@@ -79,6 +81,7 @@ struct Plan {
     std::vector<uint32_t> items, waits, segs, eunits;
     int seg_max = 0, seg_min = 0;  // whole-unit emit: WC_OPT_EMIT_SEG_MAX / _MIN_UNITS
     uint32_t ngen = 0, nfast = 0;
+    bool any_sparse = false;
     uint64_t coef_extent = 0;  // floats of staged coefficient scratch
     uint64_t ring_floats = 0;  // pipe coefficient ring
     size_t lds_gen = 0, lds_fast = 0, lds_inverse = 0, lds_pipe = 0;
@@ -128,9 +131,11 @@ struct wc_ctx {
     // wc_forward_stage left this plan's coefficients + unit keys in coef/state
     // (cleared by set_device, i.e. by every other compute entry point)
     bool staged = false;
+    bool sparse_staged = false;  // the last stage_transform used sparse staging
+    bool opt_sparse = true;      // WC_OPT_SPARSE
     uint64_t plan_gen = 0;  // bumped whenever get_plan rebuilds the plan
     // scratch (grow-only)
-    DevBuf coef, part, errflag, ring, state, stats;
+    DevBuf coef, part, errflag, ring, state, stats, flags;
     // host-path staging
     DevBuf h_cells, h_payload, h_packed, h_offsets, h_poff, h_kept, h_out;
     // per-kernel event timing (wc_profile_enable / wc_profile_read)
@@ -456,6 +461,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     P.xtiles.clear();
     P.ftiles.clear();
     P.ngen = P.nfast = 0;
+    P.any_sparse = false;
     P.lds_gen = P.lds_fast = P.lds_inverse = P.lds_pipe = 0;
     std::vector<XTile> gen, fast;
     uint64_t coef_cursor = 0, pay_cursor = 4;
@@ -477,7 +483,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         d.ntz = (d.nbz + (1 << d.lbz) - 1) >> d.lbz;
         d.pay_off = pay_cursor;  // slot of 20 + 8*ncells bytes + 4 pad: next slot stays == 4 (mod 8)
         pay_cursor += 24 + 8 * d.ncells;
-        d.coef_off = (coef_cursor + 3) & ~uint64_t(3);
+        d.coef_off = (coef_cursor + 31) & ~uint64_t(31);  // 128 B: sparse-staging segments align
         coef_cursor = d.coef_off + d.ncells;
         if (d.ncells == 0) continue;
         d.fast = (u.nx % 2 == 0) && (u.ny % 2 == 0) && (u.nz % 8 == 0);
@@ -485,6 +491,10 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         const size_t before = dst.size();
         push_tiles(dst, d, (uint32_t)i);
         d.ntx = (uint32_t)(dst.size() - before);
+        // Sparse staging (wc_xform.h xform_fast_p2_sparse): 32-block z tiles
+        // whose flat segments of 32 coefficients each belong to one tile.
+        d.sparse = (d.fast && d.lbz == kSegShift && d.hz % 32 == 0) ? 1u : 0u;
+        P.any_sparse |= d.sparse != 0;
         d.xt_begin = (uint32_t)before;  // rebased below for fast units
         if (d.fast)
             P.lds_fast = std::max(P.lds_fast, transform_fast_lds_bytes(d.lbx, d.lby, d.lbz));
@@ -557,6 +567,7 @@ int ensure_scratch(wc_ctx* c) {
     const size_t nft = P.ftiles.size();
     int rc;
     if ((rc = ensure(c, c->coef, sizeof(float) * std::max<uint64_t>(P.coef_extent, 1))) ||
+        (rc = ensure(c, c->flags, (P.coef_extent >> kSegShift) + kEmitTile)) ||
         (rc = ensure(c, c->part, sizeof(double) * nft)) || (rc = ensure(c, c->errflag, 16)) ||
         (rc = ensure(c, c->state, std::max<size_t>(P.state_bytes, decode_state_bytes(P)))))
         return rc;
@@ -661,7 +672,7 @@ int forward_pipe(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, 
 
 // Staged forward, first half: K1 transform into the flat coefficient
 // scratch + per-unit max keys (zeroed state).
-int stage_transform(wc_ctx* c, const void* d_cells, int dtype) {
+int stage_transform(wc_ctx* c, const void* d_cells, int dtype, double keep, bool sparse) {
     Plan& P = c->plan;
     const UnitDev* du = (const UnitDev*)P.d_units.p;
     const XTile* dxt = (const XTile*)P.d_xtiles.p;
@@ -670,13 +681,19 @@ int stage_transform(wc_ctx* c, const void* d_cells, int dtype) {
         return hip_fail(c, e, "memset state");
     unsigned long long* key = (unsigned long long*)((uint8_t*)c->state.p + 16);
     float* coef = (float*)c->coef.p;
+    uint8_t* flags = sparse && P.any_sparse ? (uint8_t*)c->flags.p : nullptr;
     {
         StageTimer t(c, WC_STAGE_TRANSFORM);
         e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, coef, 0, key);
         if (e == hipSuccess)
             e = launch_transform_fast(c->stream, d_cells, dtype, du, dxt + P.ngen, P.nfast, P.lds_fast, coef, 0,
-                                      key);
+                                      key, flags, keep);
+        // units whose thresh came out < 0 need every coefficient (rare: negative signed max)
+        if (e == hipSuccess && flags)
+            e = launch_transform_fallback(c->stream, d_cells, dtype, du, (int)P.units.size(), dxt, P.lds_fast, coef,
+                                          key, keep);
     }
+    c->sparse_staged = flags != nullptr;
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "transform launch");
 }
 
@@ -691,6 +708,7 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
         p.gthresh = *gthresh;
     }
     p.eunits = (const uint32_t*)P.d_eunits.p;
+    p.flags = (c->sparse_staged && !gthresh) ? (const uint8_t*)c->flags.p : nullptr;
     StageTimer t(c, WC_STAGE_EMIT);
     hipError_t e = launch_emit(c->stream, p, (const float*)c->coef.p, (uint32_t)P.segs.size(),
                                (uint32_t)P.etiles.size());
@@ -699,7 +717,7 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
 
 int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
                    uint64_t* d_offsets, uint32_t* d_kept) {
-    int rc = stage_transform(c, d_cells, dtype);
+    int rc = stage_transform(c, d_cells, dtype, keep, c->opt_sparse);
     return rc ? rc : stage_emit(c, n, keep, nullptr, d_payload, d_offsets, d_kept);
 }
 
@@ -834,6 +852,9 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
             if (value < 0 || value > 65536) return fail(c, WC_ERR_INVALID, "seg max tiles must be 0..65536");
             c->opt_seg_max = (int)value;
             return WC_OK;
+        case WC_OPT_SPARSE:
+            c->opt_sparse = value != 0;
+            return WC_OK;
         case WC_OPT_EMIT_SEG_MIN_UNITS:
             if (value < 1 || value > (int64_t(1) << 30)) return fail(c, WC_ERR_INVALID, "seg min units must be >= 1");
             c->opt_seg_min = (int)value;
@@ -903,7 +924,8 @@ int wc_forward_stage(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* u
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
     if (c->plan.pipe || !c->plan.chunks.empty())
         return fail(c, WC_ERR_INVALID, "wc_forward_stage needs the staged forward (WC_OPT_PIPE / WC_OPT_CHUNK off)");
-    if ((rc = ensure_scratch(c)) || (rc = stage_transform(c, d_cells, dtype))) return rc;
+    // dense staging: the histogram and any later threshold need every coefficient
+    if ((rc = ensure_scratch(c)) || (rc = stage_transform(c, d_cells, dtype, 0.0, false))) return rc;
     if (d_hist) {
         const uint32_t max_blocks = 2048;  // 8 workgroups per CU, 256 CUs
         const Plan& P = c->plan;
@@ -988,7 +1010,7 @@ int wc_decompose(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units
     hipError_t e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, d_flat, 1, nullptr);
     if (e == hipSuccess)
         e = launch_transform_fast(c->stream, d_cells, dtype, du, dxt + P.ngen, P.nfast, P.lds_fast, d_flat, 1,
-                                  nullptr);
+                                  nullptr, nullptr, 0.0);
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "transform launch");
 }
 

@@ -20,7 +20,7 @@ constexpr int kFlatPerThread = kFlatTile / kThreads;  // 16 = 4 x float4
 // pass-through "tail" block at b = n/2.
 struct UnitDev {
     uint64_t cell_off;   // element offset of the unit's cells
-    uint64_t coef_off;   // element offset in the flat coefficient scratch (16-B aligned)
+    uint64_t coef_off;   // element offset in the flat coefficient scratch (128-B aligned)
     uint64_t ncells;     // W*H*D
     int32_t nx, ny, nz;  // W, H, D
     int32_t hx, hy, hz;  // n/2 per axis (number of pairs)
@@ -40,7 +40,7 @@ struct UnitDev {
     uint32_t wl_len;        //   this unit's transform tiles overwrite their ring chunks
     uint32_t xt_begin;      // first transform tile of the unit in the plan's tile list
     uint32_t ewant;         // pipe: emit items of the unit (1 = one whole-unit item, else net tiles)
-    uint32_t pad_;
+    uint32_t sparse;        // 1: staged forward stores only flagged 32-coefficient segments (wc_xform.h)
 };
 
 // A transform tile: a (1<<lbx) x (1<<lby) x (1<<lbz) box of 2x2x2 blocks.
@@ -115,6 +115,9 @@ struct PipeParams {
     uint32_t ring_coefs;           // k_emit: 1 = coefficients at ring_off (chunk slots), 0 = coef_off
     uint32_t use_gthresh;          // 1: every unit uses gthresh (global histogram mode), 0: reference rule
     float gthresh;                 // fp32 threshold: keep |c| > gthresh
+    const uint8_t* flags;          // k_emit: sparse-staging segment flags (null: every unit dense)
 };
+
+constexpr int kSegShift = 5;  // sparse staging: flag per 32 flat coefficients
 
 }  // namespace wc

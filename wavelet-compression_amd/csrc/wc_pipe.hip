@@ -240,6 +240,16 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
     const UnitDev& U = P.units[u];
     const int w = tid >> 6, l = tid & 63;
     unsigned long long* smk = reinterpret_cast<unsigned long long*>(sm);  // sm[0..1]: key
+    // Sparse staging: this thread's 8 segment flags, loaded before the key
+    // wait (one flag per 8 lanes = 32 coefficients, wc_xform.h).
+    const bool sparse = !RING && P.flags && U.sparse;
+    uint32_t segf = 0xffu;  // bit it: group it may hold kept coefficients
+    if (sparse) {
+        const uint8_t* fl = P.flags + ((U.coef_off + (uint64_t)ft.index * kEmitTile) >> kSegShift);
+        segf = 0;
+#pragma unroll
+        for (int it = 0; it < 8; ++it) segf |= (uint32_t)(fl[w * 64 + it * 8 + (l >> 3)] != 0) << it;
+    }
 
     // 1. the unit's transform tiles are all in the ring
     if (tid == 0) {
@@ -270,9 +280,13 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
         // flat scratch: 16-B aligned per unit, kFlatTile slack past the last unit
         const float4* __restrict__ p4 =
             reinterpret_cast<const float4*>(coef + (P.ring_coefs ? U.ring_off : U.coef_off) + start);
+        // sparse units with thresh >= 0 skip unflagged segments (never stored);
+        // thresh < 0 units were re-staged densely (k_transform_fallback)
+        if (!(tf >= 0.0f)) segf = 0xffu;
 #pragma unroll
-        for (int it = 0; it < 8; ++it) q[it] = (uint32_t)(w * 2048 + it * 256 + 4 * l) < len ? p4[w * 512 + it * 64 + l]
-                                                                                              : make_float4(0, 0, 0, 0);
+        for (int it = 0; it < 8; ++it)
+            q[it] = ((segf >> it) & 1u) && (uint32_t)(w * 2048 + it * 256 + 4 * l) < len ? p4[w * 512 + it * 64 + l]
+                                                                                          : make_float4(0, 0, 0, 0);
     }
     const uint32_t kb = keep_bits(q, tf, len, w, l);
     uint32_t wcnt, wlast;

@@ -43,17 +43,30 @@ __global__ __launch_bounds__(kThreads) void k_transform(
 }
 
 // Even W, H, D with D % 8 == 0: 4 z-blocks per thread, 16-B LDS and global stores.
+// flags != null (staged forward): units with U.sparse store only the flagged
+// 32-coefficient segments (xform_fast_p2_sparse).
 template <typename T, bool KEYS>
 __global__ __launch_bounds__(kThreads) void k_transform_fast(
     const T* __restrict__ cells, const UnitDev* __restrict__ units, const XTile* __restrict__ tiles,
-    float* __restrict__ out, int out_mode, unsigned long long* __restrict__ unit_key) {
+    float* __restrict__ out, int out_mode, unsigned long long* __restrict__ unit_key,
+    uint8_t* __restrict__ flags, double keep) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ unsigned long long s_key[kThreads / kWave];
     const XTile td = tiles[blockIdx.x];
     const UnitDev& U = units[td.unit];
     xform_fast_p1<T>(cells + U.cell_off, U, td, lds, threadIdx.x);
     __syncthreads();
     const uint64_t obase = out_base(U, out_mode);
     float* __restrict__ dst = out + obase;
+    if constexpr (KEYS) {
+        if (flags && U.sparse) {  // uniform; coef_off is 128-B aligned here
+            const unsigned long long tk = xform_fast_p2_sparse(
+                U, td, lds, threadIdx.x, keep, s_key, flags,
+                [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
+            if (threadIdx.x == 0 && tk != 0) atomicMax(unit_key + td.unit, tk);
+            return;
+        }
+    }
     unsigned long long kmax;
     if ((obase & 3) == 0) {
         kmax = xform_fast_p2<KEYS>(U, td, lds, threadIdx.x,
@@ -66,9 +79,31 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
             dst[f + 3] = v.w;
         });
     }
-    if constexpr (KEYS) {
-        __shared__ unsigned long long s_key[kThreads / kWave];
-        block_key_max(kmax, s_key, unit_key + td.unit);
+    if constexpr (KEYS) block_key_max(kmax, s_key, unit_key + td.unit);
+}
+
+// Sparse-staged units whose thresh is < 0 (negative signed max, or keep > 1:
+// every coefficient is kept, src/compressor.cpp:216-226) need every
+// coefficient: workgroup u re-stages unit u densely, tile by tile.  Every
+// other workgroup exits after one key load.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void k_transform_fallback(const T* __restrict__ cells,
+                                                               const UnitDev* __restrict__ units,
+                                                               const XTile* __restrict__ tiles, float* __restrict__ out,
+                                                               const unsigned long long* __restrict__ unit_key,
+                                                               double keep) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const UnitDev& U = units[blockIdx.x];
+    if (!U.sparse) return;
+    if (!(key_thresh(unit_key[blockIdx.x], keep) < 0.0)) return;  // uniform
+    float* __restrict__ dst = out + U.coef_off;
+    for (uint32_t t = 0; t < U.ntx; ++t) {
+        const XTile td = tiles[U.xt_begin + t];
+        xform_fast_p1<T>(cells + U.cell_off, U, td, lds, threadIdx.x);
+        __syncthreads();
+        (void)xform_fast_p2<false>(U, td, lds, threadIdx.x,
+                                   [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
+        __syncthreads();
     }
 }
 
@@ -179,9 +214,9 @@ static uint32_t pf_grid(size_t lds, bool keys) {
 
 hipError_t launch_transform_fast(hipStream_t st, const void* cells, int dtype, const UnitDev* units,
                                  const XTile* tiles, uint32_t ntiles, size_t lds, float* out,
-                                 int out_mode, unsigned long long* keys) {
+                                 int out_mode, unsigned long long* keys, uint8_t* flags, double keep) {
     if (ntiles == 0) return hipSuccess;
-    if (dtype != 1) {  // fp32 cells: persistent, next tile's cells in flight
+    if (dtype != 1 && !flags) {  // fp32 cells, dense staging: persistent, next tile's cells in flight
         const uint32_t grid = std::min(ntiles, pf_grid(lds, keys != nullptr));
         if (keys)
             k_transform_fast_pf<true><<<grid, kThreads, lds, st>>>((const float*)cells, units, tiles, ntiles, out,
@@ -194,18 +229,29 @@ hipError_t launch_transform_fast(hipStream_t st, const void* cells, int dtype, c
     if (dtype == 1) {
         if (keys)
             k_transform_fast<double, true><<<ntiles, kThreads, lds, st>>>((const double*)cells, units, tiles, out,
-                                                                        out_mode, keys);
+                                                                  out_mode, keys, flags, keep);
         else
             k_transform_fast<double, false><<<ntiles, kThreads, lds, st>>>((const double*)cells, units, tiles, out,
-                                                                         out_mode, keys);
+                                                                  out_mode, keys, flags, keep);
     } else {
         if (keys)
             k_transform_fast<float, true><<<ntiles, kThreads, lds, st>>>((const float*)cells, units, tiles, out,
-                                                                       out_mode, keys);
+                                                                  out_mode, keys, flags, keep);
         else
             k_transform_fast<float, false><<<ntiles, kThreads, lds, st>>>((const float*)cells, units, tiles, out,
-                                                                        out_mode, keys);
+                                                                  out_mode, keys, flags, keep);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_transform_fallback(hipStream_t st, const void* cells, int dtype, const UnitDev* units, int n,
+                                     const XTile* tiles, size_t lds, float* out, const unsigned long long* keys,
+                                     double keep) {
+    if (n == 0) return hipSuccess;
+    if (dtype == 1)
+        k_transform_fallback<double><<<n, kThreads, lds, st>>>((const double*)cells, units, tiles, out, keys, keep);
+    else
+        k_transform_fallback<float><<<n, kThreads, lds, st>>>((const float*)cells, units, tiles, out, keys, keep);
     return hipGetLastError();
 }
 

@@ -345,4 +345,81 @@ __device__ __forceinline__ unsigned long long xform_fast_p2(const UnitDev& U, co
     return kmax;
 }
 
+
+// Phase 2 of a fast tile with SPARSE staging (U.sparse: 32-block z tiles,
+// hz % 32 == 0, so each 32-coefficient flat segment belongs to one tile and
+// to one aligned group of 8 lanes).  Pass A folds the tile's max key over the
+// whole workgroup; with m = |that max|, bound = m * (1 - keep) (fp64, as
+// src/compressor.cpp:216) is <= the unit's thresh whenever thresh >= 0, so a
+// segment with no |c| > bound holds no kept coefficient.  Pass B stores only
+// segments with some |c| > bound and writes EVERY segment's flag byte, so the
+// emit skips the others' loads.  Units whose thresh turns out < 0 (negative
+// signed max: everything kept) are re-staged densely by k_transform_fallback.
+// Returns the tile key (all threads); s_key: 4 LDS words.
+template <class Store4>
+__device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev& U, const XTile& td,
+                                                                   const float* lds, int tid, double keep,
+                                                                   unsigned long long* s_key,
+                                                                   uint8_t* __restrict__ flags, Store4 st) {
+    const int H = U.ny, D = U.nz;
+    const int hx = U.hx, hy = U.hy, hz = U.hz;
+    const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
+    const int TX = 1 << lbx, TY = 1 << lby, TZ = 1 << lbz;
+    const int rstride = 2 * TZ + 4;
+    const int nrows = 4 * TX * TY;
+    const int q4 = lbz - 1;
+    const int total4 = nrows << q4;
+    unsigned long long kmax = 0;
+    for (int e = tid; e < total4; e += kThreads) {
+        const int row = e >> q4;
+        const int col = (e & ((1 << q4) - 1)) << 2;
+        const int ssz = col >> lbz, bzl = col & (TZ - 1);
+        int bxl, ssx, byl, ssy;
+        row_of(row, lbx, lby, bxl, ssx, byl, ssy);
+        const int bx = td.bx0 + bxl, by = td.by0 + byl, bz = td.bz0 + bzl;
+        if (bx >= hx || by >= hy || bz >= hz) continue;
+        const int I = bx + ssx * hx, J = by + ssy * hy, K = bz + ssz * hz;
+        const uint32_t f0 = (uint32_t)(((int64_t)I * H + J) * D + K);
+        const float4 v = *reinterpret_cast<const float4*>(lds + row * rstride + col);
+        unsigned long long k = coef_key(v.x, f0);
+        kmax = k > kmax ? k : kmax;
+        k = coef_key(v.y, f0 + 1);
+        kmax = k > kmax ? k : kmax;
+        k = coef_key(v.z, f0 + 2);
+        kmax = k > kmax ? k : kmax;
+        k = coef_key(v.w, f0 + 3);
+        kmax = k > kmax ? k : kmax;
+    }
+    kmax = wave_max_u64(kmax);
+    if ((tid & 63) == 0) s_key[tid >> 6] = kmax;
+    __syncthreads();
+    unsigned long long tk = s_key[0];
+#pragma unroll
+    for (int i = 1; i < kThreads / kWave; ++i) tk = s_key[i] > tk ? s_key[i] : tk;
+    double bound = -1.0;  // flag every segment
+    if (tk != kKeyNaNFirst) {
+        const double b = (double)__uint_as_float((uint32_t)(tk >> 32) & 0x7fffffffu) * (1.0 - keep);
+        if (b >= 0.0) bound = b;
+    }
+    const int g8 = (tid & 63) & ~7;
+    for (int e = tid; e < total4; e += kThreads) {
+        const int row = e >> q4;
+        const int col = (e & ((1 << q4) - 1)) << 2;
+        const int ssz = col >> lbz, bzl = col & (TZ - 1);
+        int bxl, ssx, byl, ssy;
+        row_of(row, lbx, lby, bxl, ssx, byl, ssy);
+        const int bx = td.bx0 + bxl, by = td.by0 + byl, bz = td.bz0 + bzl;
+        if (bx >= hx || by >= hy || bz >= hz) continue;  // uniform per 8-lane segment
+        const int I = bx + ssx * hx, J = by + ssy * hy, K = bz + ssz * hz;
+        const int64_t f = ((int64_t)I * H + J) * D + K;
+        const float4 v = *reinterpret_cast<const float4*>(lds + row * rstride + col);
+        const bool cand = (double)fabsf(v.x) > bound || (double)fabsf(v.y) > bound ||
+                          (double)fabsf(v.z) > bound || (double)fabsf(v.w) > bound;
+        const bool flag = ((__ballot(cand) >> g8) & 0xffull) != 0;
+        if (flag) st(f, v);
+        if ((tid & 7) == 0) flags[(U.coef_off + (uint64_t)f) >> kSegShift] = flag ? 1 : 0;
+    }
+    return tk;
+}
+
 }  // namespace wc
