@@ -15,7 +15,7 @@ import json
 import re
 from collections import defaultdict
 
-STAGE_OF = [("k_forward_pipe", "pipe"), ("k_transform", "transform"), ("k_emit", "flat_emit"),
+STAGE_OF = [("k_forward_pipe", "pipe"), ("k_transform_fallback", "fallback"), ("k_transform", "transform"), ("k_emit", "flat_emit"),
             ("k_decode", "decode"), ("k_inverse", "inverse"), ("k_rmse", "rmse")]
 
 
