@@ -52,21 +52,27 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
     uint8_t* __restrict__ flags, double keep) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ unsigned long long s_key[kThreads / kWave];
+    __shared__ uint32_t s_mag[kThreads / kWave];
     const XTile td = tiles[blockIdx.x];
     const UnitDev& U = units[td.unit];
-    xform_fast_p1<T>(cells + U.cell_off, U, td, lds, threadIdx.x);
-    __syncthreads();
     const uint64_t obase = out_base(U, out_mode);
     float* __restrict__ dst = out + obase;
     if constexpr (KEYS) {
         if (flags && U.sparse) {  // uniform; coef_off is 128-B aligned here
-            const unsigned long long tk = xform_fast_p2_sparse(
-                U, td, lds, threadIdx.x, keep, s_key, flags,
+            uint32_t mag = xform_fast_p1<T, false, true>(cells + U.cell_off, U, td, lds, threadIdx.x);
+            mag = wave_max_u32(mag);
+            if ((threadIdx.x & 63) == 0) s_mag[threadIdx.x >> 6] = mag;
+            __syncthreads();
+            mag = max(max(s_mag[0], s_mag[1]), max(s_mag[2], s_mag[3]));
+            const unsigned long long kmax = xform_fast_p2_sparse(
+                U, td, lds, threadIdx.x, sparse_bound(mag, keep), flags,
                 [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
-            if (threadIdx.x == 0 && tk != 0) atomicMax(unit_key + td.unit, tk);
+            block_key_max(kmax, s_key, unit_key + td.unit);
             return;
         }
     }
+    xform_fast_p1<T>(cells + U.cell_off, U, td, lds, threadIdx.x);
+    __syncthreads();
     unsigned long long kmax;
     if ((obase & 3) == 0) {
         kmax = xform_fast_p2<KEYS>(U, td, lds, threadIdx.x,

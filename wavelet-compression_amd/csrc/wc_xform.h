@@ -161,9 +161,12 @@ __device__ __forceinline__ unsigned long long xform_generic_p2(const UnitDev& U,
 // flight, and each of its 8 output rows gets 4 consecutive K -> one 16-B LDS
 // write.  LDS row stride 2*TZ + 4 floats (16-B rows; b128 writes of 8 lanes
 // hit 32 banks).  Keys come from phase 2.
-template <typename T, bool SPLIT = false>
-__device__ __forceinline__ void xform_fast_p1(const T* __restrict__ src, const UnitDev& U,
-                                                            const XTile& td, float* lds, int tid) {
+// MAG: also return the max of this thread's |c| bit patterns (NaN patterns
+// are above +inf's), for the sparse-staging bound.
+template <typename T, bool SPLIT = false, bool MAG = false>
+__device__ __forceinline__ uint32_t xform_fast_p1(const T* __restrict__ src, const UnitDev& U,
+                                                  const XTile& td, float* lds, int tid) {
+    uint32_t mag = 0;
     const int W = U.nx, H = U.ny;
     const int hx = U.hx, hy = U.hy, hz = U.hz;
     const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
@@ -228,8 +231,13 @@ __device__ __forceinline__ void xform_fast_p1(const T* __restrict__ src, const U
                     *reinterpret_cast<float4*>(lds + row * rstride + (ssz << lbz) + 4 * bzq) =
                         make_float4(c[0][ssz][ssy][ssx], c[1][ssz][ssy][ssx], c[2][ssz][ssy][ssx],
                                     c[3][ssz][ssy][ssx]);
+                    if constexpr (MAG) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) mag = max(mag, __float_as_uint(c[q][ssz][ssy][ssx]) & 0x7fffffffu);
+                    }
                 }
     }
+    return mag;
 }
 
 // Split form of the fast phase 1 for a persistent kernel that keeps the next
@@ -346,20 +354,26 @@ __device__ __forceinline__ unsigned long long xform_fast_p2(const UnitDev& U, co
 }
 
 
-// Phase 2 of a fast tile with SPARSE staging (U.sparse: 32-block z tiles,
-// hz % 32 == 0, so each 32-coefficient flat segment belongs to one tile and
-// to one aligned group of 8 lanes).  Pass A folds the tile's max key over the
-// whole workgroup; with m = |that max|, bound = m * (1 - keep) (fp64, as
-// src/compressor.cpp:216) is <= the unit's thresh whenever thresh >= 0, so a
-// segment with no |c| > bound holds no kept coefficient.  Pass B stores only
-// segments with some |c| > bound and writes EVERY segment's flag byte, so the
-// emit skips the others' loads.  Units whose thresh turns out < 0 (negative
-// signed max: everything kept) are re-staged densely by k_transform_fallback.
-// Returns the tile key (all threads); s_key: 4 LDS words.
+// Sparse staging (U.sparse: 32-block z tiles, hz % 32 == 0, so each
+// 32-coefficient flat segment belongs to one tile and to one aligned group of
+// 8 lanes).  With m = the tile's max |c| (from phase 1), bound = m * (1 - keep)
+// (fp64, as src/compressor.cpp:216) is <= the unit's thresh whenever
+// thresh >= 0 (|tile max| <= |unit max|), so a segment with no |c| > bound
+// holds no kept coefficient.  A NaN in the tile, or a bound that is not >= 0,
+// flags every segment.  Units whose thresh turns out < 0 (negative signed
+// max: everything kept) are re-staged densely by k_transform_fallback.
+__device__ __forceinline__ double sparse_bound(uint32_t magbits, double keep) {
+    if (magbits > 0x7f800000u) return -1.0;
+    const double b = (double)__uint_as_float(magbits) * (1.0 - keep);
+    return b >= 0.0 ? b : -1.0;
+}
+
+// Phase 2 with sparse staging: stores only segments with some |c| > bound,
+// writes EVERY segment's flag byte (the emit skips the others' loads), and
+// returns this thread's max key over all its coefficients.
 template <class Store4>
 __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev& U, const XTile& td,
-                                                                   const float* lds, int tid, double keep,
-                                                                   unsigned long long* s_key,
+                                                                   const float* lds, int tid, double bound,
                                                                    uint8_t* __restrict__ flags, Store4 st) {
     const int H = U.ny, D = U.nz;
     const int hx = U.hx, hy = U.hy, hz = U.hz;
@@ -369,39 +383,8 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
     const int nrows = 4 * TX * TY;
     const int q4 = lbz - 1;
     const int total4 = nrows << q4;
-    unsigned long long kmax = 0;
-    for (int e = tid; e < total4; e += kThreads) {
-        const int row = e >> q4;
-        const int col = (e & ((1 << q4) - 1)) << 2;
-        const int ssz = col >> lbz, bzl = col & (TZ - 1);
-        int bxl, ssx, byl, ssy;
-        row_of(row, lbx, lby, bxl, ssx, byl, ssy);
-        const int bx = td.bx0 + bxl, by = td.by0 + byl, bz = td.bz0 + bzl;
-        if (bx >= hx || by >= hy || bz >= hz) continue;
-        const int I = bx + ssx * hx, J = by + ssy * hy, K = bz + ssz * hz;
-        const uint32_t f0 = (uint32_t)(((int64_t)I * H + J) * D + K);
-        const float4 v = *reinterpret_cast<const float4*>(lds + row * rstride + col);
-        unsigned long long k = coef_key(v.x, f0);
-        kmax = k > kmax ? k : kmax;
-        k = coef_key(v.y, f0 + 1);
-        kmax = k > kmax ? k : kmax;
-        k = coef_key(v.z, f0 + 2);
-        kmax = k > kmax ? k : kmax;
-        k = coef_key(v.w, f0 + 3);
-        kmax = k > kmax ? k : kmax;
-    }
-    kmax = wave_max_u64(kmax);
-    if ((tid & 63) == 0) s_key[tid >> 6] = kmax;
-    __syncthreads();
-    unsigned long long tk = s_key[0];
-#pragma unroll
-    for (int i = 1; i < kThreads / kWave; ++i) tk = s_key[i] > tk ? s_key[i] : tk;
-    double bound = -1.0;  // flag every segment
-    if (tk != kKeyNaNFirst) {
-        const double b = (double)__uint_as_float((uint32_t)(tk >> 32) & 0x7fffffffu) * (1.0 - keep);
-        if (b >= 0.0) bound = b;
-    }
     const int g8 = (tid & 63) & ~7;
+    unsigned long long kmax = 0;
     for (int e = tid; e < total4; e += kThreads) {
         const int row = e >> q4;
         const int col = (e & ((1 << q4) - 1)) << 2;
@@ -418,8 +401,17 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
         const bool flag = ((__ballot(cand) >> g8) & 0xffull) != 0;
         if (flag) st(f, v);
         if ((tid & 7) == 0) flags[(U.coef_off + (uint64_t)f) >> kSegShift] = flag ? 1 : 0;
+        const uint32_t f0 = (uint32_t)f;
+        unsigned long long k = coef_key(v.x, f0);
+        kmax = k > kmax ? k : kmax;
+        k = coef_key(v.y, f0 + 1);
+        kmax = k > kmax ? k : kmax;
+        k = coef_key(v.z, f0 + 2);
+        kmax = k > kmax ? k : kmax;
+        k = coef_key(v.w, f0 + 3);
+        kmax = k > kmax ? k : kmax;
     }
-    return tk;
+    return kmax;
 }
 
 }  // namespace wc
