@@ -459,7 +459,8 @@ def test_gpu_matches_committed_golden_fixtures(wc, ctx, path):
             assert regen[i].tobytes() == z[c["name"] + "/regen"].tobytes(), c["name"]
 
 
-SPARSE_DIMS = [(64, 64, 64), (16, 32, 64), (32, 8, 128), (64, 64, 64), (8, 2, 64), (64, 64, 64)]
+SPARSE_DIMS = [(64, 64, 64), (16, 32, 64), (32, 8, 128), (64, 64, 64), (8, 2, 64), (64, 64, 64), (32, 32, 32),
+               (16, 16, 32), (8, 8, 16), (2, 4, 96)]
 
 
 @pytest.mark.parametrize("keep", [float(np.float32(k)) for k in (0.999, 0.5, 1.0, 1.5)])

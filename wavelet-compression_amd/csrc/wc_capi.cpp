@@ -491,9 +491,9 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         const size_t before = dst.size();
         push_tiles(dst, d, (uint32_t)i);
         d.ntx = (uint32_t)(dst.size() - before);
-        // Sparse staging (wc_xform.h xform_fast_p2_sparse): 32-block z tiles
-        // whose flat segments of 32 coefficients each belong to one tile.
-        d.sparse = (d.fast && d.lbz == kSegShift && d.hz % 32 == 0) ? 1u : 0u;
+        // Sparse staging (wc_xform.h xform_fast_p2_sparse): z tiles of >= 16
+        // blocks whose flat segments of TZ coefficients each belong to one tile.
+        d.sparse = (d.fast && d.lbz >= kSegShift && d.hz % (1 << d.lbz) == 0) ? 1u : 0u;
         P.any_sparse |= d.sparse != 0;
         d.xt_begin = (uint32_t)before;  // rebased below for fast units
         if (d.fast)

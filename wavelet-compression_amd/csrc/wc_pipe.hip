@@ -241,14 +241,14 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
     const int w = tid >> 6, l = tid & 63;
     unsigned long long* smk = reinterpret_cast<unsigned long long*>(sm);  // sm[0..1]: key
     // Sparse staging: this thread's 8 segment flags, loaded before the key
-    // wait (one flag per 8 lanes = 32 coefficients, wc_xform.h).
+    // wait (one flag byte per 16 coefficients = 4 lanes, wc_xform.h).
     const bool sparse = !RING && P.flags && U.sparse;
     uint32_t segf = 0xffu;  // bit it: group it may hold kept coefficients
     if (sparse) {
         const uint8_t* fl = P.flags + ((U.coef_off + (uint64_t)ft.index * kEmitTile) >> kSegShift);
         segf = 0;
 #pragma unroll
-        for (int it = 0; it < 8; ++it) segf |= (uint32_t)(fl[w * 64 + it * 8 + (l >> 3)] != 0) << it;
+        for (int it = 0; it < 8; ++it) segf |= (uint32_t)(fl[w * 128 + it * 16 + (l >> 2)] != 0) << it;
     }
 
     // 1. the unit's transform tiles are all in the ring

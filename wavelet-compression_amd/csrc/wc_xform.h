@@ -354,9 +354,9 @@ __device__ __forceinline__ unsigned long long xform_fast_p2(const UnitDev& U, co
 }
 
 
-// Sparse staging (U.sparse: 32-block z tiles, hz % 32 == 0, so each
-// 32-coefficient flat segment belongs to one tile and to one aligned group of
-// 8 lanes).  With m = the tile's max |c| (from phase 1), bound = m * (1 - keep)
+// Sparse staging (U.sparse: TZ >= 16 blocks per z tile and hz % TZ == 0, so
+// each TZ-coefficient flat segment belongs to one tile and to one aligned
+// group of TZ/4 lanes; flags are kept per 16 coefficients).  With m = the tile's max |c| (from phase 1), bound = m * (1 - keep)
 // (fp64, as src/compressor.cpp:216) is <= the unit's thresh whenever
 // thresh >= 0 (|tile max| <= |unit max|), so a segment with no |c| > bound
 // holds no kept coefficient.  A NaN in the tile, or a bound that is not >= 0,
@@ -383,7 +383,9 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
     const int nrows = 4 * TX * TY;
     const int q4 = lbz - 1;
     const int total4 = nrows << q4;
-    const int g8 = (tid & 63) & ~7;
+    const int glanes = TZ >> 2;  // lanes per segment: 4 (TZ 16) or 8 (TZ 32)
+    const int g0 = (tid & 63) & ~(glanes - 1);
+    const unsigned long long gmask = (1ull << glanes) - 1ull;
     unsigned long long kmax = 0;
     for (int e = tid; e < total4; e += kThreads) {
         const int row = e >> q4;
@@ -398,9 +400,9 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
         const float4 v = *reinterpret_cast<const float4*>(lds + row * rstride + col);
         const bool cand = (double)fabsf(v.x) > bound || (double)fabsf(v.y) > bound ||
                           (double)fabsf(v.z) > bound || (double)fabsf(v.w) > bound;
-        const bool flag = ((__ballot(cand) >> g8) & 0xffull) != 0;
+        const bool flag = ((__ballot(cand) >> g0) & gmask) != 0;
         if (flag) st(f, v);
-        if ((tid & 7) == 0) flags[(U.coef_off + (uint64_t)f) >> kSegShift] = flag ? 1 : 0;
+        if ((tid & 3) == 0) flags[(U.coef_off + (uint64_t)f) >> kSegShift] = flag ? 1 : 0;  // per 16
         const uint32_t f0 = (uint32_t)f;
         unsigned long long k = coef_key(v.x, f0);
         kmax = k > kmax ? k : kmax;
