@@ -1,0 +1,17 @@
+#!/bin/bash
+# Builds libwavelet_amd.so variants (one -D each) under tools/variants/<name>/ for
+# A/B runs of tools/bin/wc_bench with LD_LIBRARY_PATH (its RUNPATH yields to it).
+set -e
+CS=wavelet-compression_amd/csrc
+FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-gpu-flush-denormals-to-zero -fno-fast-math -Iinclude -I$CS"
+for spec in "$@"; do
+  name="${spec%%:*}"; defs="${spec#*:}"
+  out=tools/variants/$name; mkdir -p $out/obj
+  for f in wc_transform wc_hist wc_compact wc_inverse wc_pipe; do
+    /opt/rocm/bin/hipcc $FLAGS $defs -c $CS/$f.hip -o $out/obj/$f.o &
+  done
+  /opt/rocm/bin/hipcc $FLAGS $defs -c $CS/wc_capi.cpp -o $out/obj/wc_capi.o &
+  wait
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out/libwavelet_amd.so $out/obj/*.o
+  rm -rf $out/obj
+done

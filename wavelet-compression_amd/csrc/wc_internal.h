@@ -118,6 +118,6 @@ struct PipeParams {
     const uint8_t* flags;          // k_emit: sparse-staging segment flags (null: every unit dense)
 };
 
-constexpr int kSegShift = 4;  // sparse staging: one flag byte per 16 flat coefficients
+constexpr int kSegShift = 4;  // sparse staging: flag index space of 16 coefficients per byte (min segment)
 
 }  // namespace wc

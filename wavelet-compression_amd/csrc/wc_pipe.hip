@@ -241,14 +241,16 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
     const int w = tid >> 6, l = tid & 63;
     unsigned long long* smk = reinterpret_cast<unsigned long long*>(sm);  // sm[0..1]: key
     // Sparse staging: this thread's 8 segment flags, loaded before the key
-    // wait (one flag byte per 16 coefficients = 4 lanes, wc_xform.h).
+    // wait (wc_xform.h).
     const bool sparse = !RING && P.flags && U.sparse;
     uint32_t segf = 0xffu;  // bit it: group it may hold kept coefficients
     if (sparse) {
-        const uint8_t* fl = P.flags + ((U.coef_off + (uint64_t)ft.index * kEmitTile) >> kSegShift);
+        // one flag byte per segment of TZ = 2^lbz coefficients (16 or 32)
+        const uint8_t* fl = P.flags + (U.coef_off >> kSegShift) + (((uint64_t)ft.index * kEmitTile) >> U.lbz);
+        const int sh = U.lbz;
         segf = 0;
 #pragma unroll
-        for (int it = 0; it < 8; ++it) segf |= (uint32_t)(fl[w * 128 + it * 16 + (l >> 2)] != 0) << it;
+        for (int it = 0; it < 8; ++it) segf |= (uint32_t)(fl[(w * 2048 + it * 256 + 4 * l) >> sh] != 0) << it;
     }
 
     // 1. the unit's transform tiles are all in the ring
@@ -573,7 +575,10 @@ __device__ __forceinline__ void emit_seg(const PipeParams& P, const float* __res
 // per unit.  SEG = false compiles the look-back path alone (its register
 // budget is not raised by the whole-unit path's double buffer).
 template <bool SEG>
-__global__ __launch_bounds__(kThreads, 4) void k_emit(PipeParams P, const float* __restrict__ coef, uint32_t nseg) {
+#ifndef WC_EMIT_MINB
+#define WC_EMIT_MINB 4  // workgroups per CU the register budget is sized for (tools/sweeps/emit_variants.sh)
+#endif
+__global__ __launch_bounds__(kThreads, WC_EMIT_MINB) void k_emit(PipeParams P, const float* __restrict__ coef, uint32_t nseg) {
     __shared__ __attribute__((aligned(16))) uint32_t sm[32];
     __shared__ uint2 stage_all[kThreads / kWave][256];  // per-wave pair stage (emit_pairs)
     const int tid = threadIdx.x;

@@ -356,7 +356,8 @@ __device__ __forceinline__ unsigned long long xform_fast_p2(const UnitDev& U, co
 
 // Sparse staging (U.sparse: TZ >= 16 blocks per z tile and hz % TZ == 0, so
 // each TZ-coefficient flat segment belongs to one tile and to one aligned
-// group of TZ/4 lanes; flags are kept per 16 coefficients).  With m = the tile's max |c| (from phase 1), bound = m * (1 - keep)
+// group of TZ/4 lanes).  Flag byte of segment s of a unit: (coef_off >> 4) + s,
+// inside the unit's 16-coefficient index range (coef_off is a multiple of 32).  With m = the tile's max |c| (from phase 1), bound = m * (1 - keep)
 // (fp64, as src/compressor.cpp:216) is <= the unit's thresh whenever
 // thresh >= 0 (|tile max| <= |unit max|), so a segment with no |c| > bound
 // holds no kept coefficient.  A NaN in the tile, or a bound that is not >= 0,
@@ -402,7 +403,7 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
                           (double)fabsf(v.z) > bound || (double)fabsf(v.w) > bound;
         const bool flag = ((__ballot(cand) >> g0) & gmask) != 0;
         if (flag) st(f, v);
-        if ((tid & 3) == 0) flags[(U.coef_off + (uint64_t)f) >> kSegShift] = flag ? 1 : 0;  // per 16
+        if ((tid & (glanes - 1)) == 0) flags[(U.coef_off >> kSegShift) + ((uint64_t)f >> lbz)] = flag ? 1 : 0;
         const uint32_t f0 = (uint32_t)f;
         unsigned long long k = coef_key(v.x, f0);
         kmax = k > kmax ? k : kmax;
