@@ -220,10 +220,12 @@ def test_inverse_bit_exact(wc, ctx, oracle, keep):
         assert regen[o:o + b.size].tobytes() == want.tobytes(), f"dims {DIMS[i]}"
 
 
-def test_inverse_writes_every_coefficient(wc, ctx, oracle):
+@pytest.mark.parametrize("sparse", [1, 0])
+def test_inverse_writes_every_coefficient(wc, ctx, oracle, sparse):
     """The decode writes zeros between pairs instead of clearing its scratch first: an
     inverse right after a dense one, over sparse, empty-payload (all-zero, NaN-first) and
     sign-quirk units, must equal the oracle's decompress exactly."""
+    ctx.set_option(12, sparse)  # WC_OPT_SPARSE
     dense = synth(oracle, [(32, 32, 32)] * 4 + [(64, 16, 8)], seed0=15)
     units, n, extent, cells = pack(wc, dense)
     payload, offs, kept = ctx.forward_host(cells, units, n, KEEPS[0])
@@ -236,6 +238,7 @@ def test_inverse_writes_every_coefficient(wc, ctx, oracle):
     units, n, extent, cells = pack(wc, boxes, np.float32)
     payload, offs, kept = ctx.forward_host(cells, units, n, KEEPS[2])
     regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
+    ctx.set_option(12, 1)
     for i, b in enumerate(boxes):
         o = units[i].cell_offset
         want = oracle.decompress_payload(wc.capi.unit_payload(payload, offs, kept, i)).ravel()
@@ -481,3 +484,21 @@ def test_sparse_staging_sign_and_keep_edges(wc, ctx, oracle, keep):
         got, _ = gpu_payloads(wc, ctx, boxes, keep, path=path)
         for i, b in enumerate(boxes):
             assert got[i] == oracle_payload(oracle, b, keep), f"{path} unit {i} dims {SPARSE_DIMS[i]} keep {keep}"
+
+
+@pytest.mark.parametrize("keep", [float(np.float32(k)) for k in (0.5, 0.99, 0.9999)])
+def test_sparse_decode_tile_boundaries(wc, ctx, oracle, keep):
+    """4096-pair decode tiles end mid-row; dense payloads (keep 0.5) put tile ends
+    everywhere.  Reconstruction must equal the oracle's with WC_OPT_SPARSE on and
+    off (payloads from the sparse-staged forward)."""
+    boxes = synth(oracle, [(64, 64, 64), (32, 32, 32), (16, 16, 32), (64, 8, 64), (48, 32, 16)], seed0=21)
+    units, n, extent, cells = pack(wc, boxes)
+    payload, offs, kept = ctx.forward_host(cells, units, n, keep)
+    for sparse in (1, 0):
+        ctx.set_option(12, sparse)
+        regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
+        for i, b in enumerate(boxes):
+            o = units[i].cell_offset
+            want = oracle.decompress_payload(wc.capi.unit_payload(payload, offs, kept, i)).ravel()
+            assert regen[o:o + b.size].tobytes() == want.tobytes(), (sparse, i)
+    ctx.set_option(12, 1)
