@@ -234,8 +234,10 @@ __device__ __forceinline__ void finish_unit(const PipeParams& P, const UnitDev& 
 template <bool RING>
 __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_rsrc_t ring,
                                           const float* __restrict__ coef, uint32_t et, uint32_t* sm, uint2* stage,
-                                          int tid, unsigned long long* st) {
-    const FTile ft = P.etiles[et];
+                                          int tid, unsigned long long* st, const FTile* known = nullptr) {
+    // known (k_emit): the tile's unit and index are already known from the
+    // ticket, and its unit key sits in sm[0..1]; skip both dependent loads.
+    const FTile ft = known ? *known : P.etiles[et];
     const uint32_t u = ft.unit;
     const UnitDev& U = P.units[u];
     const int w = tid >> 6, l = tid & 63;
@@ -264,7 +266,7 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
             smk[0] = ld_rlx(P.key + u);
             if (P.stats) st[kStEWait] += now_ticks() - t0;
         } else {
-            smk[0] = P.key[u];
+            if (!known) smk[0] = P.key[u];
         }
     }
     __syncthreads();
@@ -592,13 +594,18 @@ __global__ __launch_bounds__(kThreads, WC_EMIT_MINB) void k_emit(PipeParams P, c
     if (tid == 0) {
         const uint32_t b = blockIdx.x - nseg;
         const uint32_t u = P.eunits ? P.eunits[b] : P.etiles[P.etile_base + b].unit;
-        sm[16] = P.units[u].et_begin + atomicAdd(P.tdone + u, 1u);
+        // the unit key and the tile ticket in flight together
+        const unsigned long long key = P.key[u];
+        const uint32_t t = atomicAdd(P.tdone + u, 1u);
+        reinterpret_cast<unsigned long long*>(sm)[0] = key;
+        sm[16] = t;
+        sm[17] = u;
     }
     __syncthreads();
-    const uint32_t et = __builtin_amdgcn_readfirstlane(sm[16]);
-    __syncthreads();
+    const FTile ft{(uint32_t)__builtin_amdgcn_readfirstlane(sm[17]), (uint32_t)__builtin_amdgcn_readfirstlane(sm[16])};
+    const uint32_t et = P.units[ft.unit].et_begin + ft.index;
     __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(nullptr, 0, 0, 0x00020000);
-    pipe_emit<false>(P, none, coef, et, sm, stage, tid, nullptr);
+    pipe_emit<false>(P, none, coef, et, sm, stage, tid, nullptr, &ft);
 }
 
 // ---------------------------------------------------------------------------
