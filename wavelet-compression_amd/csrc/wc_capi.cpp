@@ -291,7 +291,10 @@ void build_etiles(Plan& P, int n) {
     P.eunits.clear();
     uint32_t maxt = 0;
     for (int i = 0; i < n; ++i) maxt = std::max(maxt, P.units[i].net);
-    const uint64_t group_tiles = std::max<uint64_t>(8192, 128ull * maxt);
+#ifndef WC_EMIT_GROUP_TILES
+#define WC_EMIT_GROUP_TILES 8192  // tools/sweeps/emit_variants.sh
+#endif
+    const uint64_t group_tiles = std::max<uint64_t>(WC_EMIT_GROUP_TILES, 128ull * maxt);
     std::vector<std::pair<int, int>> groups;  // unit ranges [i0, i1)
     for (int i0 = 0; i0 < n;) {
         uint64_t tiles = 0;
