@@ -502,3 +502,31 @@ def test_sparse_decode_tile_boundaries(wc, ctx, oracle, keep):
             want = oracle.decompress_payload(wc.capi.unit_payload(payload, offs, kept, i)).ravel()
             assert regen[o:o + b.size].tobytes() == want.tobytes(), (sparse, i)
     ctx.set_option(12, 1)
+
+
+def test_sparse_staging_special_values(wc, ctx, oracle):
+    """The reference's quirks on sparse-staged shapes (D = 32 and 64, 16/32-block z
+    tiles): NaN first (nothing kept), NaN later, +inf, negative constant (sign
+    quirk: everything kept -> dense re-staging), zeros, +M/-M ties, denormals."""
+    def box(shape, fill, edits=()):
+        b = np.full(shape, fill, np.float32)
+        for idx, v in edits:
+            b[idx] = v
+        return b
+    s1, s2 = (32, 4, 4), (64, 4, 8)
+    boxes = [
+        box(s1, 2.0, [((slice(0, 2), slice(0, 2), slice(0, 2)), np.nan)]),
+        box(s1, 2.0, [((31, 3, 3), np.nan)]),
+        box(s2, 1.0, [((0, 0, 0), np.inf)]),
+        box(s2, 1.0, [((40, 2, 5), -np.inf)]),
+        box(s1, -5.0),
+        box(s2, 0.0),
+        box(s2, 0.0, [((3, 2, 2), 3.0), ((3, 2, 3), -3.0), ((60, 3, 1), -3.0)]),
+        box(s1, np.float32(1e-40), [((9, 1, 1), np.float32(3e-39))]),
+        box(s2, 300.0, [((17, 1, 6), -1.0e5)]),
+    ]
+    for keep in (KEEPS[1], 1.0):
+        for path in ("staged", "dense"):
+            got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, path=path)
+            for i, b in enumerate(boxes):
+                assert got[i] == oracle.compress_payload(b, keep)[0], (path, keep, i)
