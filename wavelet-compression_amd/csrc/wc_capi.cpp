@@ -78,7 +78,7 @@ struct Plan {
     std::vector<XTile> xtiles;
     std::vector<XTile> ixtiles;  // inverse launch order (see get_plan)
     std::vector<FTile> ftiles, etiles, dtiles;
-    std::vector<uint32_t> items, waits, segs, eunits;
+    std::vector<uint32_t> items, waits, segs, eunits, eidx;
     int seg_max = 0, seg_min = 0;  // whole-unit emit: WC_OPT_EMIT_SEG_MAX / _MIN_UNITS
     uint32_t ngen = 0, nfast = 0;
     bool any_sparse = false;
@@ -98,7 +98,7 @@ struct Plan {
     std::vector<Chunk> chunks;
     uint64_t slot_floats = 0;
     int nslots = 0;
-    DevBuf d_units, d_xtiles, d_ftiles, d_etiles, d_items, d_waits, d_segs, d_dtiles, d_eunits, d_ixtiles;
+    DevBuf d_units, d_xtiles, d_ftiles, d_etiles, d_items, d_waits, d_segs, d_dtiles, d_eunits, d_ixtiles, d_eidx;
 };
 
 int ceil_log2(int64_t v) {
@@ -289,6 +289,7 @@ void build_etiles(Plan& P, int n) {
     // Measured: 1024 x 64^3 emit 0.346 -> 0.327 ms; batches of
     // 128^3 units (256-tile chains) stay one group up to 128 units.
     P.eunits.clear();
+    P.eidx.clear();
     uint32_t maxt = 0;
     for (int i = 0; i < n; ++i) maxt = std::max(maxt, P.units[i].net);
 #ifndef WC_EMIT_GROUP_TILES
@@ -308,7 +309,10 @@ void build_etiles(Plan& P, int n) {
         for (int i = g->first; i < g->second; ++i) gmax = std::max(gmax, P.units[i].net);
         for (uint32_t t = 0; t < gmax; ++t)
             for (int i = g->first; i < g->second; ++i)
-                if (t < P.units[i].net) P.eunits.push_back((uint32_t)i);
+                if (t < P.units[i].net) {
+                    P.eunits.push_back((uint32_t)i);
+                    P.eidx.push_back(t);
+                }
     }
 }
 
@@ -552,7 +556,8 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         (rc = upload(c, P.d_waits, P.waits.data(), sizeof(uint32_t) * P.waits.size(), "upload waits")) ||
         (rc = upload(c, P.d_segs, P.segs.data(), sizeof(uint32_t) * P.segs.size(), "upload segs")) ||
         (rc = upload(c, P.d_dtiles, P.dtiles.data(), sizeof(FTile) * P.dtiles.size(), "upload dtiles")) ||
-        (rc = upload(c, P.d_eunits, P.eunits.data(), sizeof(uint32_t) * P.eunits.size(), "upload eunits")))
+        (rc = upload(c, P.d_eunits, P.eunits.data(), sizeof(uint32_t) * P.eunits.size(), "upload eunits")) ||
+        (rc = upload(c, P.d_eidx, P.eidx.data(), sizeof(uint32_t) * P.eidx.size(), "upload eidx")))
         return rc;
     // The host vectors back the async copies: finish them before returning.
     hipError_t e = hipStreamSynchronize(c->stream);
@@ -711,6 +716,7 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
         p.gthresh = *gthresh;
     }
     p.eunits = (const uint32_t*)P.d_eunits.p;
+    p.eidx = (const uint32_t*)P.d_eidx.p;
     p.flags = (c->sparse_staged && !gthresh) ? (const uint8_t*)c->flags.p : nullptr;
     StageTimer t(c, WC_STAGE_EMIT);
     hipError_t e = launch_emit(c->stream, p, (const float*)c->coef.p, (uint32_t)P.segs.size(),
@@ -798,7 +804,7 @@ void wc_ctx_destroy(wc_ctx* c) {
                       &c->ring,      &c->state,     &c->stats,      &c->h_cells,    &c->h_payload,
                       &c->h_packed,  &c->h_offsets, &c->h_poff,    &c->h_kept,     &c->h_out,
                       &c->plan.d_units, &c->plan.d_xtiles, &c->plan.d_ftiles, &c->plan.d_etiles,
-                      &c->plan.d_items, &c->plan.d_waits, &c->plan.d_segs, &c->plan.d_dtiles, &c->plan.d_eunits, &c->plan.d_ixtiles};
+                      &c->plan.d_items, &c->plan.d_waits, &c->plan.d_segs, &c->plan.d_dtiles, &c->plan.d_eunits, &c->plan.d_ixtiles, &c->plan.d_eidx};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& m : c->marks) {

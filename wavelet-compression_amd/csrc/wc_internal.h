@@ -110,6 +110,7 @@ struct PipeParams {
     double keep;
     const uint32_t* segs;          // k_emit: units packed whole, one workgroup each
     const uint32_t* eunits;        // k_emit: unit of each look-back block (interleaved order), or null
+    const uint32_t* eidx;          // k_emit: tile index of each look-back block (same order as eunits)
     uint32_t seg_base;             // k_emit: first entry of segs in this launch
     uint32_t etile_base;           // k_emit: first look-back emit tile of this launch
     uint32_t ring_coefs;           // k_emit: 1 = coefficients at ring_off (chunk slots), 0 = coef_off

@@ -234,9 +234,10 @@ __device__ __forceinline__ void finish_unit(const PipeParams& P, const UnitDev& 
 template <bool RING>
 __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_rsrc_t ring,
                                           const float* __restrict__ coef, uint32_t et, uint32_t* sm, uint2* stage,
-                                          int tid, unsigned long long* st, const FTile* known = nullptr) {
-    // known (k_emit): the tile's unit and index are already known from the
-    // ticket, and its unit key sits in sm[0..1]; skip both dependent loads.
+                                          int tid, unsigned long long* st, const FTile* known = nullptr,
+                                          bool key_ready = false) {
+    // known (k_emit): the tile's unit and index are already known (ticket or
+    // dispatch order); key_ready: its unit key already sits in sm[0..1].
     const FTile ft = known ? *known : P.etiles[et];
     const uint32_t u = ft.unit;
     const UnitDev& U = P.units[u];
@@ -266,7 +267,7 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
             smk[0] = ld_rlx(P.key + u);
             if (P.stats) st[kStEWait] += now_ticks() - t0;
         } else {
-            if (!known) smk[0] = P.key[u];
+            if (!key_ready) smk[0] = P.key[u];
         }
     }
     __syncthreads();
@@ -577,6 +578,9 @@ __device__ __forceinline__ void emit_seg(const PipeParams& P, const float* __res
 // per unit.  SEG = false compiles the look-back path alone (its register
 // budget is not raised by the whole-unit path's double buffer).
 template <bool SEG>
+#ifndef WC_EMIT_ORDERED
+#define WC_EMIT_ORDERED 1  // 0: take the look-back tile index from a per-unit ticket atomic instead
+#endif
 #ifndef WC_EMIT_MINB
 #define WC_EMIT_MINB 4  // workgroups per CU the register budget is sized for (tools/sweeps/emit_variants.sh)
 #endif
@@ -591,6 +595,19 @@ __global__ __launch_bounds__(kThreads, WC_EMIT_MINB) void k_emit(PipeParams P, c
             return;
         }
     }
+    __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(nullptr, 0, 0, 0x00020000);
+#if WC_EMIT_ORDERED
+    // Tile index from the dispatch order: a block's look-back waits only on
+    // lower-indexed tiles of its unit, which have lower block ids, and each
+    // XCD dispatches its blocks in increasing id order, so no wait is on an
+    // undispatched block (waits stay bounded by spin_fail regardless).
+    if (P.eidx) {
+        const uint32_t b = blockIdx.x - nseg;
+        const FTile ft{P.eunits[b], P.eidx[b]};
+        pipe_emit<false>(P, none, coef, P.units[ft.unit].et_begin + ft.index, sm, stage, tid, nullptr, &ft);
+        return;
+    }
+#endif
     if (tid == 0) {
         const uint32_t b = blockIdx.x - nseg;
         const uint32_t u = P.eunits ? P.eunits[b] : P.etiles[P.etile_base + b].unit;
@@ -604,8 +621,7 @@ __global__ __launch_bounds__(kThreads, WC_EMIT_MINB) void k_emit(PipeParams P, c
     __syncthreads();
     const FTile ft{(uint32_t)__builtin_amdgcn_readfirstlane(sm[17]), (uint32_t)__builtin_amdgcn_readfirstlane(sm[16])};
     const uint32_t et = P.units[ft.unit].et_begin + ft.index;
-    __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(nullptr, 0, 0, 0x00020000);
-    pipe_emit<false>(P, none, coef, et, sm, stage, tid, nullptr, &ft);
+    pipe_emit<false>(P, none, coef, et, sm, stage, tid, nullptr, &ft, true);
 }
 
 // ---------------------------------------------------------------------------
