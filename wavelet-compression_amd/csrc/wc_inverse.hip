@@ -35,6 +35,9 @@ __device__ __forceinline__ bool read_header(const UnitDev& U, const uint8_t* __r
            (uint64_t)nrle <= U.ncells;
 }
 
+#ifndef WC_DEC_ORDERED
+#define WC_DEC_ORDERED 1  // 0: take the look-back tile index from a per-unit ticket atomic instead
+#endif
 __global__ __launch_bounds__(kThreads) void k_decode(const UnitDev* __restrict__ units,
                                                    const FTile* __restrict__ tiles,
                                                    const uint8_t* __restrict__ payload,
@@ -55,11 +58,19 @@ __global__ __launch_bounds__(kThreads) void k_decode(const UnitDev* __restrict__
     const uint32_t ntile = n ? (uint32_t)((n + kFlatTile - 1) / kFlatTile) : 1u;
     // The plan launches ceil(ncoeff / kFlatTile) blocks per unit; those whose
     // plan index is past the payload's pair tiles exit before any atomic.
-    // The others take their tile from the unit's ticket.
     if (ft.index >= ntile) return;  // uniform
+#if WC_DEC_ORDERED
+    // Tile = plan index: the plan interleaves tiles by index across units, so a
+    // tile's look-back waits only on lower block ids of its unit, and each XCD
+    // dispatches its blocks in increasing id order (waits stay bounded).
+    (void)ticket;
+    const uint32_t t = ft.index;
+#else
+    // The others take their tile from the unit's ticket.
     if (tid == 0) s_x[0] = atomicAdd(ticket + u, 1u);
     __syncthreads();
     const uint32_t t = (uint32_t)s_x[0];
+#endif
     if (!hok && t == 0 && tid == 0) atomicOr(err, kErrHeader);
 
     // 1. this lane's pairs and their in-wave inclusive sums of (run + 1)
