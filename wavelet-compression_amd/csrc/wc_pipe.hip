@@ -256,9 +256,10 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
         for (int it = 0; it < 8; ++it) segf |= (uint32_t)(fl[(w * 2048 + it * 256 + 4 * l) >> sh] != 0) << it;
     }
 
-    // 1. the unit's transform tiles are all in the ring
-    if (tid == 0) {
-        if constexpr (RING) {
+    // 1. the unit's transform tiles are all in the ring (RING); the unit key
+    unsigned long long ukey;
+    if constexpr (RING) {
+        if (tid == 0) {
             const unsigned long long t0 = P.stats ? now_ticks() : 0;
             for (uint32_t spins = 0;;) {
                 if (ld_rlx(P.tdone + u) >= U.ntx) break;
@@ -266,12 +267,15 @@ __device__ __forceinline__ void pipe_emit(const PipeParams& P, __amdgpu_buffer_r
             }
             smk[0] = ld_rlx(P.key + u);
             if (P.stats) st[kStEWait] += now_ticks() - t0;
-        } else {
-            if (!key_ready) smk[0] = P.key[u];
         }
+        __syncthreads();
+        ukey = smk[0];
+    } else if (key_ready) {
+        ukey = smk[0];  // stored before the caller's barrier
+    } else {
+        ukey = P.key[u];  // a finished earlier launch wrote it: one uniform load, no barrier
     }
-    __syncthreads();
-    const float tf = unit_thresh(P, smk[0]);
+    const float tf = unit_thresh(P, ukey);
     const uint32_t start = ft.index * (uint32_t)kEmitTile;
     const uint32_t len = (uint32_t)min((uint64_t)kEmitTile, U.ncells - start);
 
