@@ -107,9 +107,8 @@ def main():
     for _ in range(args.warmup):
         step()
     ctx.synchronize()
-    ctx.profile_enable(True)
-    ctx.profile_read()  # reset
 
+    # Timed region: no per-kernel events (they would sit between the launches).
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -122,6 +121,14 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+
+    # Per-kernel launch times (hipEvents on the context's stream, where the
+    # kernels run) from the same number of steps right after.
+    ctx.profile_enable(True)
+    ctx.profile_read()  # reset
+    for _ in range(args.steps):
+        step()
+    ctx.synchronize()
     ctx.profile_enable(False)
     stages = ctx.profile_read()
 
@@ -294,8 +301,6 @@ def inverse_figures(args, ctx, capi, units, n, ncells, payload, offsets, kept_to
     for _ in range(2):
         istep()
     ctx.synchronize()
-    ctx.profile_enable(True)
-    ctx.profile_read()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -303,6 +308,11 @@ def inverse_figures(args, ctx, capi, units, n, ncells, payload, offsets, kept_to
     ctx.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    ctx.profile_enable(True)  # per-kernel times from a separate loop (events off in the timed one)
+    ctx.profile_read()
+    for _ in range(args.steps):
+        istep()
+    ctx.synchronize()
     ctx.profile_enable(False)
     st = ctx.profile_read()
     ms = (t1 - t0) / args.steps * 1e3
