@@ -8,6 +8,7 @@ in a fixed tree order).
 """
 import numpy as np
 import pytest
+from wavelet_compression_amd.capi import WC_OPT_SPARSE
 
 pytestmark = pytest.mark.gpu
 
@@ -40,7 +41,7 @@ def set_path(ctx, path, lag=0, ring=0):
     ctx.set_pipe(path == "pipe", lag=lag, ring=ring)
     ctx.set_chunk(16384 if path == "chunked" else 0, slots=2)
     ctx.set_emit_seg(64 if path == "seg" else 0, 1)
-    ctx.set_option(12, 0 if path == "dense" else 1)  # WC_OPT_SPARSE
+    ctx.set_option(WC_OPT_SPARSE, 0 if path == "dense" else 1)
 
 
 def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None, path="staged", lag=0, ring=0):
@@ -225,7 +226,7 @@ def test_inverse_writes_every_coefficient(wc, ctx, oracle, sparse):
     """The decode writes zeros between pairs instead of clearing its scratch first: an
     inverse right after a dense one, over sparse, empty-payload (all-zero, NaN-first) and
     sign-quirk units, must equal the oracle's decompress exactly."""
-    ctx.set_option(12, sparse)  # WC_OPT_SPARSE
+    ctx.set_option(WC_OPT_SPARSE, sparse)
     dense = synth(oracle, [(32, 32, 32)] * 4 + [(64, 16, 8)], seed0=15)
     units, n, extent, cells = pack(wc, dense)
     payload, offs, kept = ctx.forward_host(cells, units, n, KEEPS[0])
@@ -238,7 +239,7 @@ def test_inverse_writes_every_coefficient(wc, ctx, oracle, sparse):
     units, n, extent, cells = pack(wc, boxes, np.float32)
     payload, offs, kept = ctx.forward_host(cells, units, n, KEEPS[2])
     regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
-    ctx.set_option(12, 1)
+    ctx.set_option(WC_OPT_SPARSE, 1)
     for i, b in enumerate(boxes):
         o = units[i].cell_offset
         want = oracle.decompress_payload(wc.capi.unit_payload(payload, offs, kept, i)).ravel()
@@ -495,13 +496,13 @@ def test_sparse_decode_tile_boundaries(wc, ctx, oracle, keep):
     units, n, extent, cells = pack(wc, boxes)
     payload, offs, kept = ctx.forward_host(cells, units, n, keep)
     for sparse in (1, 0):
-        ctx.set_option(12, sparse)
+        ctx.set_option(WC_OPT_SPARSE, sparse)
         regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
         for i, b in enumerate(boxes):
             o = units[i].cell_offset
             want = oracle.decompress_payload(wc.capi.unit_payload(payload, offs, kept, i)).ravel()
             assert regen[o:o + b.size].tobytes() == want.tobytes(), (sparse, i)
-    ctx.set_option(12, 1)
+    ctx.set_option(WC_OPT_SPARSE, 1)
 
 
 def test_sparse_staging_special_values(wc, ctx, oracle):
