@@ -128,6 +128,7 @@ struct wc_ctx {
     int opt_seg_max = 0;     // WC_OPT_EMIT_SEG_MAX (0: look-back tiles only, the faster layout measured)
     int opt_seg_min = 256;   // WC_OPT_EMIT_SEG_MIN_UNITS
     bool err_check_pending = false;
+    uint32_t* err_src = nullptr;  // device error word of the pending call (null: errflag)
     // wc_forward_stage left this plan's coefficients + unit keys in coef/state
     // (cleared by set_device, i.e. by every other compute entry point)
     bool staged = false;
@@ -606,7 +607,9 @@ int check_kernel_errors(wc_ctx* c) {
     if (!c->err_check_pending) return WC_OK;
     c->err_check_pending = false;
     uint32_t flag = 0;
-    hipError_t e = hipMemcpyAsync(&flag, c->errflag.p, 4, hipMemcpyDeviceToHost, c->stream);
+    const void* src = c->err_src ? (const void*)c->err_src : c->errflag.p;
+    c->err_src = nullptr;
+    hipError_t e = hipMemcpyAsync(&flag, src, 4, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "error flag readback");
     if (flag & (kErrHeader | kErrNegativeRun)) {
@@ -675,6 +678,7 @@ int forward_pipe(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, 
     }
     if (e != hipSuccess) return hip_fail(c, e, "pipe launch");
     c->err_check_pending = true;
+    c->err_src = nullptr;
     return WC_OK;
 }
 
@@ -717,11 +721,17 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
     }
     p.eunits = (const uint32_t*)P.d_eunits.p;
     p.eidx = (const uint32_t*)P.d_eidx.p;
+    // error word inside the per-call state header (zeroed with it; the staged
+    // path does not use the pipe's ticket word next to it): no extra memset
+    p.err = (uint32_t*)((uint8_t*)c->state.p + 4);
+    c->err_src = p.err;
     p.flags = (c->sparse_staged && !gthresh) ? (const uint8_t*)c->flags.p : nullptr;
     StageTimer t(c, WC_STAGE_EMIT);
     hipError_t e = launch_emit(c->stream, p, (const float*)c->coef.p, (uint32_t)P.segs.size(),
                                (uint32_t)P.etiles.size());
-    return e == hipSuccess ? WC_OK : hip_fail(c, e, "emit launch");
+    if (e != hipSuccess) return hip_fail(c, e, "emit launch");
+    c->err_check_pending = true;  // a look-back wait that timed out surfaces at wc_synchronize
+    return WC_OK;
 }
 
 int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
@@ -1055,6 +1065,7 @@ int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, c
     if (e != hipSuccess) return hip_fail(c, e, "inverse launch");
     // Malformed payloads surface at the next wc_synchronize (WC_ERR_FORMAT).
     c->err_check_pending = true;
+    c->err_src = nullptr;
     return WC_OK;
 }
 
