@@ -1,22 +1,41 @@
-"""bench.py — forward hot path (transform + keep threshold + ordered pack) on MI355X.
+"""bench.py — the forward hot path (transform + keep threshold + ordered pack)
+of the wavelet codec on MI355X, plus the inverse / round-trip legs of the
+other BASELINE.json configs.
 
-Workload (BASELINE.json configs[1]): 1024 synthetic 64^3 fp64 boxes per GPU,
-1 component, keep = 0.999f, inputs resident in HBM before the timed region.
-One step = one wc_forward over the whole batch (cells -> serialized payloads).
-Multi-GPU: one process per GPU; every rank compresses its own 1024 boxes
-(independent AMR units, no data-path collective) -> weak scaling.  The only
-collective is a small all-reduce of kept/byte counts after timing.
+Headline (`value`, BASELINE.json configs[1] = C2): 1024 synthetic 64^3 fp64
+boxes per GPU, 1 component, keep = 0.999f, inputs resident in HBM before the
+timed region; one step = one wc_forward over the rank's whole batch (cells ->
+serialized payloads, byte-identical to the reference's serialize()).  N GPUs:
+one process per GPU, each compressing its own 1024 boxes (independent AMR
+units, no data-path collective) -> weak scaling; `value` = all ranks' cells /
+the slowest rank's time.
 
-Prints ONE JSON line on rank 0 (driver contract).  The CPU baseline is the
-oracle restatement (single thread) on a bounded sample of the same boxes; the
-sample's payload bytes are also compared with the GPU's ("sample_parity").
+Legs (sub-objects of the same JSON line):
+  inverse  C2's payloads back to cells (rle_decode + inverse transform) and
+           the per-box RMSE (calc_rmse_per_box) of the reconstruction
+  c3       BASELINE configs[2]: 4-level AMR layout x 4 components, fwd + inv +
+           RMSE round trip on one GPU (world == 1)
+  c5       configs[4]: 512 x 128^3 fp32, keep 0.9999, units split over ranks
+  c4       configs[3]: 10 timesteps x 4 levels x 8 components, units split over
+           ranks; plus the opt-in global-threshold mode (magnitude histogram,
+           ONE all-reduce over ranks: RCCL over xGMI)
+  cpu_baseline  (rank 0, world 1) the CPU restatement on the host cores on a
+           bounded sample, with and without xz preset 6; sample parity and the
+           RMSE check against it.
+
+`python bench.py --gpus N` without WORLD_SIZE in the environment starts N
+ranks itself (torch.distributed.run, before any GPU call); under an outer
+torchrun it is one rank.  `--plumbing` runs the rank/shard/reduction logic on
+CPU (gloo) without kernels, for the CPU test suite.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -25,347 +44,556 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+ALL_LEGS = ("inverse", "c3", "c5", "c4")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--boxes", type=int, default=1024)
-    ap.add_argument("--dim", type=int, default=64)
-    ap.add_argument("--dtype", choices=("f64", "f32"), default="f64")
-    ap.add_argument("--keep", type=float, default=0.999)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="time budget of the CPU-baseline sample (boxes run until it is spent)")
+    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2",
+                    help="headline workload (default: BASELINE configs[1], C2)")
+    ap.add_argument("--legs", default=",".join(ALL_LEGS),
+                    help="comma list of extra legs (inverse,c3,c5,c4) or 'none'")
+    ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of each extra leg")
+    ap.add_argument("--hist-quantile", type=float, default=0.7,
+                    help="c4 leg: quantile of the opt-in global-threshold mode (NOT the reference rule)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="time budget of each CPU-baseline sample (boxes run until it is spent)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r01" / "pmc_forward.json"),
-                    help="PMC traffic summary (tools/pmc_summary.py) merged into roofline.traffic")
-    ap.add_argument("--pipe", action="store_true", help="run the pipelined single-launch forward (WC_OPT_PIPE)")
-    ap.add_argument("--no-inverse", action="store_true", help="skip the inverse-path figures")
-    ap.add_argument("--hist-quantile", type=float, default=None,
-                    help="also time the opt-in global-threshold mode (NOT the reference rule): stage + "
-                         "magnitude histogram, one all-reduce over ranks (RCCL), threshold at this quantile, emit")
-    return ap.parse_args()
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r02" / "pmc_forward.json"),
+                    help="PMC traffic summary (tools/pmc_summary.py) merged into roofline.traffic when it "
+                         "was measured on the same kernel sources")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="CPU/gloo run of the launcher, sharding and reductions (no kernels, no numbers)")
+    return ap.parse_args(argv)
 
 
-def synth_device(torch, dev, nboxes, dim, dtype, rank):
-    """v = 300 + 50 sin(0.1 gx) cos(0.07 gy) + 0.01 gz + 0.05 N(0,1)  (SURVEY.md §8(d)),
-    boxes tiled over a 16 x 8 x (n/128) grid of 64^3 patches, generated on device."""
-    td = torch.float64 if dtype == "f64" else torch.float32
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + 7919 * rank)
-    n = dim
-    z = torch.arange(n, device=dev, dtype=torch.float64).view(n, 1, 1)
-    y = torch.arange(n, device=dev, dtype=torch.float64).view(1, n, 1)
-    x = torch.arange(n, device=dev, dtype=torch.float64).view(1, 1, n)
-    out = torch.empty(nboxes * n ** 3, dtype=td, device=dev)
-    for b in range(nboxes):
-        lx, ly, lz = n * (b % 16), n * ((b // 16) % 8), n * (b // 128) + 4096 * rank
-        v = 300.0 + 50.0 * torch.sin(0.1 * (x + lx)) * torch.cos(0.07 * (y + ly)) + 0.01 * (z + lz)
-        v = v + 0.05 * torch.randn((n, n, n), generator=g, device=dev, dtype=torch.float64)
-        out[b * n ** 3:(b + 1) * n ** 3] = v.reshape(-1).to(td)
-    return out
+# ---------------------------------------------------------------------------
+# launcher
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
-def main():
-    args = parse()
-    import numpy as np
+def spawn_ranks(args) -> int:
+    """Start `--gpus` ranks with torch.distributed.run (one process per GPU) and
+    return its exit status.  Called before anything touches the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve())]
+    cmd += sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------------
+# helpers
+
+def kernel_sources_sha() -> str:
+    """Hash of the kernel + C-ABI sources: a PMC summary applies only to them."""
+    h = hashlib.sha256()
+    cs = ROOT / "wavelet-compression_amd" / "csrc"
+    for p in sorted(list(cs.glob("*.hip")) + list(cs.glob("*.h")) + [cs / "wc_capi.cpp"]):
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def alg_bytes_forward(s_in, cells, kept, nunits):
+    """B = s_in*N_cells + 8*N_kept + 20*N_units."""
+    return s_in * cells + 8 * kept + 20 * nunits
+
+
+def alg_bytes_inverse(cells, kept, nunits):
+    """B = 8*N_kept + 20*N_units + 4*N_cells."""
+    return 8 * kept + 20 * nunits + 4 * cells
+
+
+class Dist:
+    """The rank's view of the job: world, rank, device, barrier, reductions."""
+
+    def __init__(self, plumbing: bool):
+        import torch
+        import torch.distributed as dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.plumbing = plumbing
+        if plumbing:
+            self.dev = torch.device("cpu")
+            if self.world > 1:
+                dist.init_process_group("gloo")
+        else:
+            if self.world > 1:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            torch.cuda.set_device(self.local)
+            self.dev = torch.device("cuda", self.local)
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def reduce(self, metrics):
+        if self.world == 1:
+            return dict(metrics)
+        from wavelet_compression_amd.shard import reduce_metrics
+        return reduce_metrics(metrics, device=self.dev)
+
+    def close(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+
+
+def rank_units(name, d: Dist):
+    """This rank's units of a workload: its own copy (per-GPU workloads, unit
+    ids offset by rank) or its contiguous cell-balanced share (shard.plan_shards)."""
+    import bench_workloads as bw
+    from wavelet_compression_amd.shard import plan_shards
+    spec = bw.WORKLOADS[name]
+    units = spec["units"]()
+    if spec["per_gpu"]:
+        n = len(units)
+        return [bw.Unit(u.t, u.lev, u.box, u.comp, u.W, u.H, u.D,
+                        (u.lo[0], u.lo[1], u.lo[2] + 4096 * d.rank), u.gid + n * d.rank) for u in units], (0, n)
+    a, b = plan_shards([u.cells for u in units], d.world)[d.rank]
+    return units[a:b], (a, b)
+
+
+class Batch:
+    """A rank's batch on the device: cells, the unit table and output buffers."""
+
+    def __init__(self, d: Dist, units, dtype, keep, inverse=False):
+        import numpy as np
+        import torch
+        import bench_workloads as bw
+        import wcamd
+        self.capi = wcamd.capi
+        self.units = units
+        self.dtype = dtype
+        self.keep = float(np.float32(keep))  # Config::keep is a float (src/argparse.h:13)
+        self.s_in = 8 if dtype == "f64" else 4
+        self.code = self.capi.WC_F64 if dtype == "f64" else self.capi.WC_F32
+        self.cells_dev, offs, self.extent = bw.synth_cells(torch, d.dev, units, dtype)
+        self.tab, self.n, _ = bw.units_array(self.capi, units, offs)
+        self.offs = offs
+        self.ncells = sum(u.cells for u in units)
+        self.cap = self.capi.payload_bound(self.tab, self.n) if self.n else 16
+        self.payload = torch.empty(self.cap, dtype=torch.uint8, device=d.dev)
+        self.offsets = torch.zeros(self.n + 1, dtype=torch.int64, device=d.dev)
+        self.kept = torch.zeros(max(self.n, 1), dtype=torch.int32, device=d.dev)
+        self.regen = torch.empty(max(self.extent, 1), dtype=torch.float32, device=d.dev) if inverse else None
+        self.rmse = torch.zeros(max(self.n, 1), dtype=torch.float64, device=d.dev) if inverse else None
+        torch.cuda.synchronize()
+
+    def forward(self, ctx):
+        if self.n:
+            ctx.forward(self.cells_dev.data_ptr(), self.code, self.tab, self.n, self.keep, self.payload.data_ptr(),
+                        self.cap, self.offsets.data_ptr(), self.kept.data_ptr())
+
+    def inverse(self, ctx):
+        if self.n:
+            ctx.inverse(self.payload.data_ptr(), self.offsets.data_ptr(), self.tab, self.n, self.regen.data_ptr())
+
+    def rmse_step(self, ctx):
+        if self.n:
+            ctx.rmse(self.cells_dev.data_ptr(), self.code, self.regen.data_ptr(), self.tab, self.n,
+                     self.rmse.data_ptr())
+
+    def kept_total(self):
+        return int(self.kept[:self.n].to(self.kept.device).sum().item()) if self.n else 0
+
+
+def timed(d: Dist, ctx, step, steps, warmup):
+    """Warmup, then EXACTLY `steps` steps bracketed by barrier + synchronize on
+    both sides; returns this rank's seconds.  No per-kernel events inside."""
     import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
-    import wcamd
-    capi = wcamd.capi
-    ctx = capi.Context(local)
-    ctx.set_pipe(args.pipe)
-    keep = float(np.float32(args.keep))  # Config::keep is a float (src/argparse.h:13)
-    dims = [(args.dim,) * 3] * args.boxes
-    units, n, extent = capi.make_units(dims)
-    ncells = extent  # dense, 64^3 multiples: no padding
-    dtype_code = capi.WC_F64 if args.dtype == "f64" else capi.WC_F32
-    s_in = 8 if args.dtype == "f64" else 4
-
-    cells = synth_device(torch, dev, args.boxes, args.dim, args.dtype, rank)
-    cap = capi.payload_bound(units, n)
-    payload = torch.empty(cap, dtype=torch.uint8, device=dev)
-    offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    kept = torch.zeros(n, dtype=torch.int32, device=dev)
-    torch.cuda.synchronize()
-
-    def step():
-        ctx.forward(cells.data_ptr(), dtype_code, units, n, keep, payload.data_ptr(), cap,
-                    offsets.data_ptr(), kept.data_ptr())
-
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     ctx.synchronize()
-
-    # Timed region: no per-kernel events (they would sit between the launches).
-    if world > 1:
-        dist.barrier()
+    d.barrier()
     torch.cuda.synchronize()
     ctx.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     ctx.synchronize()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
+    d.barrier()
+    return time.perf_counter() - t0
 
-    # Per-kernel launch times (hipEvents on the context's stream, where the
-    # kernels run) from the same number of steps right after.
+
+def stage_times(ctx, step, steps):
+    """Per-kernel average launch times (ms) from hipEvents recorded on the
+    context stream around each launch, from `steps` more steps."""
     ctx.profile_enable(True)
-    ctx.profile_read()  # reset
-    for _ in range(args.steps):
+    ctx.profile_read()
+    for _ in range(steps):
         step()
     ctx.synchronize()
     ctx.profile_enable(False)
-    stages = ctx.profile_read()
+    return {k: (ms / cnt, cnt / steps) for k, (ms, cnt) in ctx.profile_read().items()}
 
-    elapsed = t1 - t0
-    kept_total = int(kept.sum().item())
-    payload_bytes = int(kept.to(torch.int64).sum().item()) * 8 + 20 * n  # serialized bytes (slots excluded)
-    local = {"seconds": elapsed, "kept": kept_total, "payload_bytes": payload_bytes, "cells": ncells}
-    if world > 1:
-        # the one collective: run metrics (a few bytes) over RCCL, after timing
-        from wavelet_compression_amd.shard import reduce_metrics
-        local = reduce_metrics(local, device=dev)
-    elapsed = local["seconds"]
-    kept_all, bytes_all, cells_all = local["kept"], local["payload_bytes"], local["cells"]
 
-    # ---- roofline of the dominant kernel (per-launch averages from hipEvents) ----
-    per_launch = {k: (ms / cnt, cnt) for k, (ms, cnt) in stages.items()}
-    dominant = max(per_launch, key=lambda k: per_launch[k][0])
-    kept_step = kept_total  # per launch (this rank)
-    alg_bytes_stage = {
-        # algorithmic bytes each kernel owns of B = s_in*N + 8*N_kept + 20*N_units (SURVEY §8(d));
-        # the fp32 coefficient staging between K1 and K2 is overhead, not algorithmic traffic.
-        "transform": s_in * ncells,
-        "flat_emit": 8 * kept_step + 20 * n,
-        # the pipelined kernel owns the whole path: cells in, pairs + headers out
-        "pipe": s_in * ncells + 8 * kept_step + 20 * n,
-    }
-    dom_ms = per_launch[dominant][0]
-    achieved = alg_bytes_stage.get(dominant, 0) / (dom_ms * 1e-3) / 1e9
-    path_ms = sum(v[0] for v in per_launch.values())
-    path_bytes = s_in * ncells + 8 * kept_step + 20 * n
-    # Reference point for "achievable": a device-to-device copy of the cell
-    # buffer (torch's copy kernel, read + write bytes per second).
-    scratch = torch.empty_like(cells)
-    scratch.copy_(cells)
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
-    for _ in range(5):
-        scratch.copy_(cells)
-    ev1.record()
-    torch.cuda.synchronize()
-    copy_gbps = 2 * cells.numel() * cells.element_size() * 5 / (ev0.elapsed_time(ev1) * 1e-3) / 1e9
-    del scratch
-    traffic = None
-    pmc_path = Path(args.pmc)
-    if pmc_path.exists():
-        try:
-            pmc = json.loads(pmc_path.read_text())
-            if pmc.get("config", {}).get("boxes") == args.boxes and pmc.get("config", {}).get("dtype") == args.dtype:
-                traffic = pmc.get("per_launch_bytes", {}).get(dominant)
-        except Exception:
-            traffic = None
+def pmc_traffic(path, workload, dtype, kernel):
+    """Counter bytes per launch for `kernel` from a committed rocprofv3 PMC summary,
+    only if it was measured on this workload AND these kernel sources."""
+    p = Path(path)
+    if not p.exists():
+        return None, {"source": None, "note": "no PMC summary"}
+    try:
+        pmc = json.loads(p.read_text())
+    except Exception:
+        return None, {"source": str(p), "note": "unreadable"}
+    meta = {"source": str(p.relative_to(ROOT)) if p.is_relative_to(ROOT) else str(p),
+            "date": pmc.get("date"), "git": pmc.get("git")}
+    cfg = pmc.get("config", {})
+    if cfg.get("workload") != workload or cfg.get("dtype") != dtype:
+        meta["note"] = "measured on another workload"
+        return None, meta
+    if pmc.get("kernel_sources_sha") != kernel_sources_sha():
+        meta["note"] = "stale: kernel sources changed since the counter run"
+        return None, meta
+    return pmc.get("per_launch_bytes", {}).get(kernel), meta
 
+
+# ---------------------------------------------------------------------------
+# the headline workload
+
+def headline(args, d: Dist, ctx):
+    import bench_workloads as bw
+    spec = bw.WORKLOADS[args.workload]
+    units, span = rank_units(args.workload, d)
+    b = Batch(d, units, spec["dtype"], spec["keep"], inverse="inverse" in args.legs_set)
+    secs = timed(d, ctx, lambda: b.forward(ctx), args.steps, args.warmup)
+    stages = stage_times(ctx, lambda: b.forward(ctx), args.steps)
+    kept = b.kept_total()
+    m = d.reduce({"seconds": secs, "kept": kept, "cells": b.ncells, "boxes": b.n,
+                  "payload_bytes": 8 * kept + 20 * b.n})
+    elapsed = m["seconds"]
+    # roofline of the dominant kernel: its algorithmic bytes (SURVEY §8(d)) per launch / its launch time
+    own = {"transform": b.s_in * b.ncells, "emit": 8 * kept + 20 * b.n}
+    dominant = max(stages, key=lambda k: stages[k][0])
+    dom_ms = stages[dominant][0]
+    achieved = own.get(dominant, 0) / (dom_ms * 1e-3) / 1e9
+    path_ms = sum(v[0] * v[1] for v in stages.values())
+    path_bytes = alg_bytes_forward(b.s_in, b.ncells, kept, b.n)
+    traffic, tmeta = pmc_traffic(args.pmc, args.workload, spec["dtype"], dominant)
+    ms_step = elapsed / args.steps * 1e3
     out = {
-        "metric": f"{'fp64' if args.dtype == 'f64' else 'fp32'} cells/s, fwd transform+threshold+pack, keep={args.keep}",
-        "value": cells_all * args.steps / elapsed,
+        "metric": f"{'fp64' if spec['dtype'] == 'f64' else 'fp32'} cells/s, fwd transform+threshold+pack, "
+                  f"keep={spec['keep']}",
+        "value": m["cells"] * args.steps / elapsed,
         "unit": "cells/s",
-        "n_gpus": world,
+        "n_gpus": d.world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if spec["per_gpu"] else "strong",
         "vs_baseline": None,
-        "dtype": args.dtype,
-        "data": "synthetic (SURVEY §8(d) field + N(0,0.05) noise, generated on device)",
-        "config": {"workload": f"{args.boxes}x{args.dim}^3 {args.dtype} boxes/GPU, 1 component, "
-                               f"keep={args.keep}f, wc_forward (payload bytes identical to reference)",
-                   "boxes_per_gpu": args.boxes, "box_dim": args.dim, "global_batch": args.boxes * world,
-                   "parallelism": f"box-sharded x{world}"},
-        "compressed_GBps": cells_all * s_in * args.steps / elapsed / 1e9,
-        "kept_fraction": kept_all / cells_all,
-        "payload_bytes_per_step": bytes_all,
-        "stage_ms_per_launch": {k: round(v[0], 4) for k, v in per_launch.items()},
+        "dtype": spec["dtype"],
+        "data": "synthetic (SURVEY §8(d) field + N(0,0.05) noise, generated on device; bench_workloads.py)",
+        "config": {"workload": f"{args.workload}: {spec['desc']}, wc_forward (payload bytes identical to the "
+                               f"reference's serialize())",
+                   "boxes_per_gpu": b.n, "global_batch": int(m["boxes"]),
+                   "parallelism": f"box-sharded x{d.world}"},
+        "compressed_GBps": m["cells"] * b.s_in * args.steps / elapsed / 1e9,
+        "kept_fraction": m["kept"] / max(m["cells"], 1),
+        "payload_bytes_per_step": int(m["payload_bytes"]),
+        "stage_ms_per_launch": {k: round(v[0], 4) for k, v in stages.items()},
         "roofline": {
             "bound": "hbm", "kernel": dominant,
             "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBPS,
             "traffic": traffic,
-            # HBM bytes the kernel actually moved (PMC, incl. the fp32 coefficient staging) per second
             "traffic_GBps": (traffic / (dom_ms * 1e-3) / 1e9) if traffic else None,
-            "copy_GBps": copy_gbps,
+            "traffic_source": tmeta,
+            "alg_bytes_per_launch": own.get(dominant, 0),
         },
-        "roofline_path": {"achieved": path_bytes / (path_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS,
-                          "unit": "GB/s", "frac": path_bytes / (path_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
-                          "bytes_per_step": path_bytes, "kernel_ms_per_step": path_ms},
-        "cpu_baseline": None,
+        "roofline_path": {"achieved": path_bytes / (ms_step * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS,
+                          "unit": "GB/s", "frac": path_bytes / (ms_step * 1e-3) / 1e9 / PEAK_HBM_GBPS,
+                          "bytes_per_step": path_bytes, "kernel_ms_per_step": path_ms,
+                          "note": "algorithmic bytes / driver-clock ms_per_step (launch gaps included)"},
     }
-
-    if not args.no_inverse:
-        out["inverse"] = inverse_figures(args, ctx, capi, units, n, ncells, payload, offsets, kept_total, dev)
-
-    if args.hist_quantile is not None:
-        out["global_hist"] = global_hist_figures(args, ctx, capi, units, n, dtype_code, cells, payload, cap,
-                                                 offsets, kept, dev, world, s_in)
-
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, cells, payload, offsets, kept, s_in, keep)
-
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return out, b
 
 
-def global_hist_figures(args, ctx, capi, units, n, dtype_code, cells, payload, cap, offsets, kept, dev, world,
-                        s_in):
-    """Opt-in global-threshold mode, timed like the headline step: per step one
-    stage (K1 + histogram), ONE all-reduce of the 4096-bin histogram over all
-    ranks (RCCL over xGMI when world > 1), the threshold on the host, one emit."""
+def inverse_leg(args, d: Dist, ctx, b: Batch):
+    """C2's payloads back to cells + per-box RMSE; SURVEY §8(d) inverse bytes."""
     import torch
-    import torch.distributed as dist
-    from wavelet_compression_amd.shard import global_threshold
+    kept = b.kept_total()
+    secs = timed(d, ctx, lambda: b.inverse(ctx), args.steps, 2)
+    st = stage_times(ctx, lambda: b.inverse(ctx), args.steps)
+    b.rmse_step(ctx)
+    ctx.synchronize()
+    r = b.rmse[:b.n]
+    m = d.reduce({"seconds": secs, "cells": b.ncells, "kept": kept, "boxes": b.n,
+                  "rmse_sum": float(r.sum().item()), "max_rmse": float(r.max().item())})
+    ms = m["seconds"] / args.steps * 1e3
+    alg = alg_bytes_inverse(b.ncells, kept, b.n)
+    torch.cuda.synchronize()
+    return {"value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
+            "stage_ms_per_launch": {k: round(v[0], 4) for k, v in st.items()},
+            "roofline_path": {"achieved": alg / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                              "frac": alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, "bytes_per_step": alg},
+            "rmse": {"mean_per_box": m["rmse_sum"] / max(m["boxes"], 1), "max": m["max_rmse"],
+                     "note": "calc_rmse_per_box of the reconstruction vs the narrowed input (GPU K7); "
+                             "checked against the CPU restatement in cpu_baseline.rmse_check"}}
 
-    hist = torch.zeros(capi.HIST_BINS, dtype=torch.int64, device=dev)
+
+def round_trip_leg(args, d: Dist, name):
+    """C3: forward + inverse + RMSE per step over the whole AMR layout (one GPU)."""
+    import bench_workloads as bw
+    import torch
+    import wcamd
+    spec = bw.WORKLOADS[name]
+    units, _ = rank_units(name, d)
+    ctx = wcamd.capi.Context(d.local)
+    b = Batch(d, units, spec["dtype"], spec["keep"], inverse=True)
+
+    def step():
+        b.forward(ctx)
+        b.inverse(ctx)
+        b.rmse_step(ctx)
+
+    secs = timed(d, ctx, step, args.leg_steps, 2)
+    st = stage_times(ctx, step, args.leg_steps)
+    kept = b.kept_total()
+    r = b.rmse[:b.n].cpu().numpy()
+    ms = secs / args.leg_steps * 1e3
+    fwd = alg_bytes_forward(b.s_in, b.ncells, kept, b.n)
+    inv = alg_bytes_inverse(b.ncells, kept, b.n)
+    rm = (b.s_in + 4) * b.ncells
+    per_comp = {}
+    for u, v in zip(units, r):
+        per_comp.setdefault(u.comp, []).append(float(v))
+    out = {"workload": spec["desc"], "units": b.n, "cells": b.ncells, "dtype": spec["dtype"],
+           "kept_fraction": kept / b.ncells, "ms_per_step": ms,
+           "round_trip_cells_per_s": b.ncells / (ms * 1e-3),
+           "stage_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in st.items()},
+           "roofline_path": {"bytes_per_step": fwd + inv + rm, "achieved": (fwd + inv + rm) / (ms * 1e-3) / 1e9,
+                             "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                             "frac": (fwd + inv + rm) / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
+                             "note": "fwd + inverse + RMSE algorithmic bytes / driver-clock step"},
+           "mean_rmse_per_component": {str(c): sum(v) / len(v) for c, v in sorted(per_comp.items())}}
+    ctx.close()
+    del b
+    torch.cuda.empty_cache()
+    return out
+
+
+def sharded_forward_leg(args, d: Dist, name, hist=False):
+    """C5 / C4: the workload's units split over ranks (plan_shards), forward timed
+    as the headline; C4 adds the opt-in global-threshold mode (one all-reduce)."""
+    import bench_workloads as bw
+    import torch
+    import wcamd
+    spec = bw.WORKLOADS[name]
+    units, span = rank_units(name, d)
+    ctx = wcamd.capi.Context(d.local)
+    b = Batch(d, units, spec["dtype"], spec["keep"])
+    secs = timed(d, ctx, lambda: b.forward(ctx), args.leg_steps, 2)
+    st = stage_times(ctx, lambda: b.forward(ctx), args.leg_steps)
+    kept = b.kept_total()
+    m = d.reduce({"seconds": secs, "cells": b.ncells, "kept": kept, "boxes": b.n,
+                  "max_rank_cells": b.ncells, "min_rank_cells": b.ncells})
+    ms = m["seconds"] / args.leg_steps * 1e3
+    alg = alg_bytes_forward(b.s_in, m["cells"], m["kept"], m["boxes"])
+    per_rank_alg = alg_bytes_forward(b.s_in, b.ncells, kept, b.n)
+    out = {"workload": spec["desc"], "units_total": int(m["boxes"]), "units_this_rank": b.n,
+           "rank0_span": list(span), "cells_total": int(m["cells"]), "dtype": spec["dtype"], "keep": spec["keep"],
+           "kept_fraction": m["kept"] / max(m["cells"], 1), "ms_per_step": ms,
+           "value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "scaling": "strong",
+           "rank_cell_balance": m["max_rank_cells"] / max(m["min_rank_cells"], 1),
+           "stage_ms_per_launch": {k: round(v[0], 4) for k, v in st.items()},
+           "roofline_path": {"achieved_per_gpu": per_rank_alg / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS,
+                             "unit": "GB/s", "frac": per_rank_alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
+                             "bytes_per_step_all_ranks": alg}}
+    if hist:
+        out["global_hist"] = global_hist_leg(args, d, ctx, b)
+    ctx.close()
+    del b
+    torch.cuda.empty_cache()
+    return out
+
+
+def global_hist_leg(args, d: Dist, ctx, b: Batch):
+    """Opt-in global-threshold mode, timed like a step: stage (K1 + histogram),
+    ONE all-reduce of the 4096-bin histogram over all ranks (RCCL over xGMI when
+    world > 1), the threshold on the host, one emit."""
+    import torch
+    from wavelet_compression_amd.shard import global_threshold
+    hist = torch.zeros(b.capi.HIST_BINS, dtype=torch.int64, device=d.dev)
     res = {}
 
     def step():
         hist.zero_()
-        t, r = global_threshold(ctx, cells.data_ptr(), dtype_code, units, n, args.hist_quantile, hist)
-        ctx.forward_emit(units, n, 0.0, t, payload.data_ptr(), cap, offsets.data_ptr(), kept.data_ptr())
+        t, r = global_threshold(ctx, b.cells_dev.data_ptr(), b.code, b.tab, b.n, args.hist_quantile, hist)
+        ctx.forward_emit(b.tab, b.n, 0.0, t, b.payload.data_ptr(), b.cap, b.offsets.data_ptr(),
+                         b.kept.data_ptr())
         res.update(thresh=t, retained=r)
 
-    for _ in range(max(1, args.warmup)):
-        step()
-    ctx.synchronize()
-    ctx.profile_enable(True)
-    ctx.profile_read()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    ctx.synchronize()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ctx.profile_enable(False)
-    stages = ctx.profile_read()
-    kept_rank = int(kept.sum().item())
-    cells_rank = args.boxes * args.dim ** 3
-    m = {"seconds": elapsed, "kept": kept_rank, "cells": cells_rank}
-    if world > 1:
-        from wavelet_compression_amd.shard import reduce_metrics
-        m = reduce_metrics(m, device=dev)
-    return {
-        "mode": "global histogram threshold (opt-in, not the reference rule)",
-        "quantile": args.hist_quantile, "threshold": res["thresh"],
-        "retained": res["retained"], "kept_check": m["kept"] == res["retained"],
-        "kept_fraction": m["kept"] / m["cells"],
-        "value": m["cells"] * args.steps / m["seconds"], "unit": "cells/s",
-        "ms_per_step": m["seconds"] / args.steps * 1e3,
-        "stage_ms_per_launch": {k: round(ms / cnt, 4) for k, (ms, cnt) in stages.items()},
-        "allreduce": f"{capi.HIST_BINS} x u64 over {world} rank(s)" + (" (RCCL)" if world > 1 else " (none)"),
-    }
+    secs = timed(d, ctx, step, args.leg_steps, 1)
+    kept = b.kept_total()
+    m = d.reduce({"seconds": secs, "kept": kept, "cells": b.ncells})
+    ms = m["seconds"] / args.leg_steps * 1e3
+    return {"mode": "global histogram threshold (opt-in, not the reference rule)",
+            "quantile": args.hist_quantile, "threshold": res["thresh"], "retained": res["retained"],
+            "kept_check": int(m["kept"]) == res["retained"], "kept_fraction": m["kept"] / m["cells"],
+            "value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
+            "allreduce": f"{b.capi.HIST_BINS} x u64 over {d.world} rank(s)" + (" (RCCL)" if d.world > 1 else " (none)")}
 
 
-def inverse_figures(args, ctx, capi, units, n, ncells, payload, offsets, kept_total, dev):
-    """The inverse path over this step's payloads (wc_inverse: rle_decode + inverse transform),
-    timed like the forward; SURVEY §8(d) inverse bytes = 8*N_kept + 20*N_units + 4*N_cells."""
-    import torch
-    regen = torch.empty(ncells, dtype=torch.float32, device=dev)
+# ---------------------------------------------------------------------------
+# CPU baseline (the oracle: checker + reported baseline only)
 
-    def istep():
-        ctx.inverse(payload.data_ptr(), offsets.data_ptr(), units, n, regen.data_ptr())
-
-    for _ in range(2):
-        istep()
-    ctx.synchronize()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        istep()
-    ctx.synchronize()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    ctx.profile_enable(True)  # per-kernel times from a separate loop (events off in the timed one)
-    ctx.profile_read()
-    for _ in range(args.steps):
-        istep()
-    ctx.synchronize()
-    ctx.profile_enable(False)
-    st = ctx.profile_read()
-    ms = (t1 - t0) / args.steps * 1e3
-    alg = 8 * kept_total + 20 * n + 4 * ncells
-    per = {k: v[0] / v[1] for k, v in st.items()}
-    return {"value": ncells / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
-            "stage_ms_per_launch": {k: round(v, 4) for k, v in per.items()},
-            "roofline_path": {"achieved": alg / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                              "frac": alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, "bytes_per_step": alg}}
+def host_threads():
+    """Threads the CPU baseline uses: this process's CPU share.  On the GPU box
+    the job's share is OMP_NUM_THREADS (16 per GPU); nproc shows the whole host."""
+    aff = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(aff, omp) if omp > 0 else aff), aff
 
 
-def cpu_baseline(args, cells, payload, offsets, kept, s_in, keep):
-    """Oracle restatement (gcc -O2; ctypes releases the GIL) on a bounded sample of the same
-    boxes: one thread, then a thread pool over boxes (the reference's per-box loop is
-    embarrassingly parallel).  The sample's payload bytes are compared with the
-    GPU's ("sample_parity")."""
-    import numpy as np
+def cpu_baseline(args, b: Batch, rmse_dev):
+    """Oracle restatement (gcc -O2; ctypes releases the GIL) on a bounded sample
+    of the same boxes: one thread, then a thread pool over boxes (the
+    reference's per-box loop is embarrassingly parallel); then the
+    reference-faithful compress() equivalent WITH xz preset 6 / CRC64 (the
+    reference's liblzma parameters, src/compressor.cpp:256-291).  The sample's
+    payload bytes and per-box RMSE are compared with the GPU's."""
+    import lzma
     from concurrent.futures import ThreadPoolExecutor
-    from oracle import oracle as O  # checker / CPU baseline leg only
 
-    nb = args.dim ** 3
-    off = offsets.cpu().numpy()
-    kp = kept.cpu().numpy()
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    import numpy as np
+    from oracle import oracle as O
 
-    def one(i):
-        box = host[i]
-        b32 = O.narrow(box) if box.dtype == np.float64 else box
-        return O.compress_payload(b32, keep)[0]
+    threads, aff = host_threads()
+    off = b.offsets.cpu().numpy()
+    kp = b.kept.cpu().numpy()
+    host = {}
 
-    # single thread: boxes until half the budget is spent
-    host, t_one, done, parity = {}, 0.0, 0, True
-    while done < args.boxes and t_one < args.cpu_seconds / 2:
-        host[done] = cells[done * nb:(done + 1) * nb].cpu().numpy().reshape((args.dim,) * 3)
+    def box(i):
+        if i not in host:
+            u = b.units[i]
+            o = b.offs[i]
+            host[i] = b.cells_dev[o:o + u.cells].cpu().numpy().reshape(u.D, u.H, u.W)
+        return host[i]
+
+    def payload(i):
+        x = box(i)
+        return O.compress_payload(O.narrow(x) if x.dtype == np.float64 else x, b.keep)[0]
+
+    t_one, done, parity = 0.0, 0, True
+    budget = args.cpu_seconds
+    while done < b.n and t_one < budget / 2:
+        box(done)
         t0 = time.perf_counter()
-        want = one(done)
+        want = payload(done)
         t_one += time.perf_counter() - t0
         o = int(off[done])
-        parity &= payload[o:o + 20 + 8 * int(kp[done])].cpu().numpy().tobytes() == want
+        parity &= b.payload[o:o + 20 + 8 * int(kp[done])].cpu().numpy().tobytes() == want
         done += 1
-    # thread pool: the same boxes, repeated until the other half is spent
     with ThreadPoolExecutor(threads) as ex:
         t_mt, reps = 0.0, 0
-        while t_mt < args.cpu_seconds / 2:
+        while t_mt < budget / 2:
             t0 = time.perf_counter()
-            list(ex.map(one, range(done)))
+            list(ex.map(payload, range(done)))
             t_mt += time.perf_counter() - t0
             reps += 1
-    return {"value": reps * done * nb / t_mt, "unit": "cells/s", "cores": threads, "kind": "port",
-            "sample": f"first {done} of {args.boxes} boxes ({done * nb} cells) x {reps} passes over {threads} "
+        # compress() with xz preset 6 (~97 % of the reference's time, SURVEY §0.6)
+        xz_done, t_xz = 0, 0.0
+        t0 = time.perf_counter()
+        while t_xz < budget and xz_done < done:
+            chunk = list(range(xz_done, min(done, xz_done + threads)))
+            list(ex.map(lambda i: lzma.compress(payload(i), format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64,
+                                                preset=6), chunk))
+            xz_done += len(chunk)
+            t_xz = time.perf_counter() - t0
+    cells = b.units[0].cells
+    # RMSE check: the oracle's decompress + calc_rmse_per_box on a few sampled boxes
+    nchk = min(done, 8)
+    rmse_ok, rel = True, 0.0
+    if rmse_dev is not None:
+        rg = rmse_dev[:b.n].cpu().numpy()
+        for i in range(nchk):
+            o = int(off[i])
+            x = box(i)
+            want_regen = O.decompress_payload(b.payload[o:o + 20 + 8 * int(kp[i])].cpu().numpy().tobytes())
+            want = O.rmse(O.narrow(x) if x.dtype == np.float64 else x, want_regen)
+            r = abs(rg[i] - want) / max(abs(want), 1e-300)
+            rel = max(rel, r)
+            rmse_ok &= r <= 1e-6
+    return {"value": reps * done * cells / t_mt, "unit": "cells/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "sample": f"first {done} of {b.n} boxes ({done * cells} cells) x {reps} passes over {threads} "
                       f"threads, oracle narrow+transform+threshold+RLE+serialize (no xz), {t_mt:.1f} s",
-            "single_thread": {"value": done * nb / t_one, "cores": 1, "seconds": round(t_one, 2)},
-            "sample_parity": bool(parity)}
+            "single_thread": {"value": done * cells / t_one, "cores": 1, "seconds": round(t_one, 2)},
+            "with_xz": {"value": xz_done * cells / t_xz if t_xz else None, "unit": "cells/s", "cores": threads,
+                        "sample": f"{xz_done} boxes, compress() equivalent incl. xz preset 6 / CRC64 "
+                                  f"(python lzma = liblzma), {t_xz:.1f} s"},
+            "sample_parity": bool(parity),
+            "rmse_check": {"boxes": nchk, "max_rel_diff": rel, "within_1e-6": bool(rmse_ok)}}
+
+
+# ---------------------------------------------------------------------------
+
+def plumbing_run(args, d: Dist):
+    """CPU check of the launcher: ranks, shard plans and the metric reduction."""
+    import bench_workloads as bw
+    shards = {}
+    for name in ("c5", "c4"):
+        units, span = rank_units(name, d)
+        m = d.reduce({"cells": sum(u.cells for u in units), "boxes": len(units),
+                      "max_rank_cells": sum(u.cells for u in units)})
+        shards[name] = {"rank0_span": list(span), "units_total": int(m["boxes"]),
+                        "cells_total": int(m["cells"]),
+                        "expected_total": sum(u.cells for u in bw.WORKLOADS[name]["units"]())}
+    m = d.reduce({"seconds": 0.001 * (d.rank + 1), "boxes": 1})
+    return {"metric": "plumbing (no kernels)", "value": None, "n_gpus": d.world, "ranks_seen": int(m["boxes"]),
+            "max_seconds": m["seconds"], "shards": shards}
+
+
+def main():
+    args = parse()
+    import wcamd  # noqa: F401  (registers the package as wavelet_compression_amd; no GPU call)
+    args.legs_set = set() if args.legs in ("none", "") else set(args.legs.split(","))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
+    d = Dist(args.plumbing)
+    if args.plumbing:
+        out = plumbing_run(args, d)
+        if d.rank == 0:
+            print(json.dumps(out), flush=True)
+        d.close()
+        return
+    import torch
+    import wcamd
+    ctx = wcamd.capi.Context(d.local)
+    out, b = headline(args, d, ctx)
+    if "inverse" in args.legs_set:
+        out["inverse"] = inverse_leg(args, d, ctx, b)
+    out["cpu_baseline"] = None
+    if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, b, b.rmse)
+    ctx.close()
+    del b
+    torch.cuda.empty_cache()
+    if "c3" in args.legs_set and d.world == 1:
+        out["c3"] = round_trip_leg(args, d, "c3")
+    if "c5" in args.legs_set:
+        out["c5"] = sharded_forward_leg(args, d, "c5")
+    if "c4" in args.legs_set:
+        out["c4"] = sharded_forward_leg(args, d, "c4", hist=True)
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+    d.close()
 
 
 if __name__ == "__main__":

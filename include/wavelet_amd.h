@@ -79,44 +79,23 @@ const char* wc_last_error(const wc_ctx* ctx);
 /* Run on an external hipStream_t (e.g. a torch stream); NULL restores the
  * context's own stream. */
 int wc_set_stream(wc_ctx* ctx, void* hip_stream);
-int wc_synchronize(wc_ctx* ctx);  /* also reports kernel-side errors of earlier async calls */
+int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side errors of earlier async calls */
 
-/* Tuning switches.
- * WC_OPT_PIPE (default 0): 0 runs wc_forward as two launches (transform ->
- *   fp32 coefficient scratch in HBM -> one emit launch doing threshold,
- *   decoupled look-back and ordered pack); 1 runs ONE persistent launch that
- *   interleaves transform tiles (coefficients into a ring sized to stay in
- *   the Infinity Cache) with emit tiles.  Results are byte-identical either
- *   way (DESIGN.md has the timings of both).
- * WC_OPT_PIPE_LAG: cells of transform work listed between a unit's last
- *   transform tile and its emit work (0 = default, 16 Mi cells).
- * WC_OPT_PIPE_RING: coefficient ring size in floats (0 = default: lag + 8 Mi
- *   + 2 x the largest unit; never more than the batch needs). */
-#define WC_OPT_PIPE 1
-#define WC_OPT_PIPE_LAG 2
-#define WC_OPT_PIPE_RING 3
-#define WC_OPT_PIPE_CLAIM 4     /* work-list items claimed per ticket (default 1) */
-#define WC_OPT_PIPE_PREFETCH 5  /* 1: claim the next ticket while working (default 0) */
-#define WC_OPT_PIPE_WGS 6       /* workgroups per CU (0 = occupancy limit) */
-#define WC_OPT_PIPE_STATS 7     /* 1: collect wait-time counters (wc_pipe_stats) */
-#define WC_OPT_CHUNK 8          /* forward over chunks of this many cells: one launch per chunk
-                                   transforms it and packs the previous chunk (0 = whole batch) */
-#define WC_OPT_CHUNK_SLOTS 9    /* coefficient slots of the chunked forward (default 2) */
-#define WC_OPT_EMIT_SEG_MAX 10  /* staged emit: units of at most this many 8192-coefficient tiles are packed
-                                   whole by one workgroup each, no look-back (default 0 = never: the
-                                   look-back tiles measured faster) */
-#define WC_OPT_EMIT_SEG_MIN_UNITS 11 /* ... when the batch holds at least this many of them (default 256) */
-#define WC_OPT_SPARSE 12        /* staged forward (default 1): K1 stores only the 32-coefficient flat segments
-                                   that hold some |c| > (tile max) * (1 - keep) and flags them; the emit loads
-                                   only flagged segments.  Same bytes out; 0 = dense staging */
+/* Tuning switches (wc_set_option).
+ * WC_OPT_SPARSE (default 1): the forward's transform stores only the
+ *   32-coefficient flat segments that hold some |c| > (tile max) * (1 - keep)
+ *   and flags them; the emit loads only flagged segments.  Same bytes out;
+ *   0 = dense staging of every coefficient.
+ * WC_OPT_ORDERED (default 1): the look-back kernels (forward emit, inverse
+ *   decode) take each block's tile index from the launch order, relying on
+ *   workgroups being dispatched in increasing id (DESIGN.md §Forward
+ *   progress); 0 takes it from a per-unit ticket atomic instead, which needs no
+ *   assumption about dispatch order.  Same bytes out either way.  Every wait
+ *   between workgroups is bounded: a wait that never ends is reported as
+ *   WC_ERR_HIP at the next wc_synchronize, not a hang. */
+#define WC_OPT_SPARSE 12
+#define WC_OPT_ORDERED 13
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
-
-/* Diagnostics of the pipelined kernel (WC_OPT_PIPE_STATS on): summed over
- * workgroups since the last read, in 100 MHz ticks: [0] transform items,
- * [1] of which ring waits, [2] emit items, [3] of which waits for the unit's
- * transform tiles, [4] of which look-back, [5] ticket waits; [6] transform
- * and [7] emit item counts.  Synchronizes the context stream. */
-int wc_pipe_stats(wc_ctx* ctx, uint64_t* out, int n);
 
 /* Host-side helpers (no device work). */
 uint64_t wc_payload_bound(const wc_unit* units, int n);  /* worst case: every coefficient kept */
@@ -154,8 +133,7 @@ int wc_forward_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* un
  *     the reference per-unit rule with `keep` (so stage + emit == wc_forward),
  *     else every coefficient with |c| > *thresh is kept.  Needs the staged
  *     coefficients of the same units: any other compute call on the context in
- *     between invalidates them (WC_ERR_INVALID).  Needs the default staged
- *     forward (WC_OPT_PIPE and WC_OPT_CHUNK off). */
+ *     between invalidates them (WC_ERR_INVALID). */
 #define WC_HIST_BINS 4096
 #define WC_HIST_SHIFT 19
 int wc_forward_stage(wc_ctx* ctx, const void* d_cells, int dtype, const wc_unit* units, int n,
@@ -199,18 +177,13 @@ int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* 
  * launch (used by bench.py for the live roofline figure).  Stage ids below;
  * wc_profile_read() returns the summed milliseconds and launch counts since
  * the previous read, then resets. */
-#define WC_STAGE_TRANSFORM 0  /* K1  */
-#define WC_STAGE_COUNT 1      /* unused since the look-back emit (kept for numbering) */
-#define WC_STAGE_SCAN 2       /* unused */
-#define WC_STAGE_OFFSETS 3    /* unused */
-#define WC_STAGE_EMIT 4       /* K2  threshold + ordered pack (k_emit) */
-#define WC_STAGE_DECODE 5     /* K5a-c */
-#define WC_STAGE_INVERSE 6    /* K6  */
-#define WC_STAGE_RMSE 7       /* K7  */
-#define WC_STAGE_PIPE 8       /* pipelined forward kernel (whole wc_forward) */
-#define WC_STAGE_CHUNKED 9    /* chunked forward, first to last launch (whole wc_forward) */
-#define WC_STAGE_HIST 10      /* coefficient-magnitude histogram (wc_forward_stage with d_hist) */
-#define WC_NUM_STAGES 11
+#define WC_STAGE_TRANSFORM 0  /* K1  transform (+ dense re-staging fallback) */
+#define WC_STAGE_EMIT 1       /* K2  threshold + ordered pack (k_emit) */
+#define WC_STAGE_DECODE 2     /* K5  rle_decode */
+#define WC_STAGE_INVERSE 3    /* K6  inverse transform */
+#define WC_STAGE_RMSE 4       /* K7  */
+#define WC_STAGE_HIST 5       /* coefficient-magnitude histogram (wc_forward_stage with d_hist) */
+#define WC_NUM_STAGES 6
 int wc_profile_enable(wc_ctx* ctx, int on);
 int wc_profile_read(wc_ctx* ctx, double* total_ms, uint32_t* launches, int nstages);
 

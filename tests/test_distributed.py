@@ -163,3 +163,28 @@ def test_gloo_global_histogram_threshold(wc, oracle, quantile):
     assert kept == retained >= total - int(np.floor(quantile * total))
     assert merged == {u: oracle.compress_payload_thresh(oracle.narrow(
         oracle.synth_box_f64(oracle.unit_seed(0, 0, u, 0), (0, 0, 0), *d)), thresh) for u, d in enumerate(dims)}
+
+
+def test_bench_spawns_ranks_and_merges_one_line(tmp_path):
+    """bench.py --gpus 2 (no WORLD_SIZE in the environment) starts two ranks
+    itself (torch.distributed.run), shards C5 / C4 over them with plan_shards
+    and prints ONE merged JSON line from rank 0 (gloo on CPU: --plumbing runs
+    the launcher, shards and reductions without kernels)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["WCAMD_NO_TORCH"] = "1"
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--plumbing"], env=env,
+                       capture_output=True, text=True, timeout=300, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["ranks_seen"] == 2
+    assert out["max_seconds"] == pytest.approx(0.002)
+    for name, sh in out["shards"].items():
+        assert sh["cells_total"] == sh["expected_total"], name
+        assert sh["rank0_span"][0] == 0 and 0 < sh["rank0_span"][1] < sh["units_total"], name

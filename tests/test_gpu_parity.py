@@ -8,7 +8,7 @@ in a fixed tree order).
 """
 import numpy as np
 import pytest
-from wavelet_compression_amd.capi import WC_OPT_SPARSE
+from wavelet_compression_amd.capi import WC_OPT_ORDERED, WC_OPT_SPARSE
 
 pytestmark = pytest.mark.gpu
 
@@ -36,17 +36,15 @@ def pack(wc, boxes, dtype=np.float64, offsets=None):
     return units, n, extent, cells
 
 
-def set_path(ctx, path, lag=0, ring=0):
-    """Forward-path options (library defaults: staged, look-back emit tiles)."""
-    ctx.set_pipe(path == "pipe", lag=lag, ring=ring)
-    ctx.set_chunk(16384 if path == "chunked" else 0, slots=2)
-    ctx.set_emit_seg(64 if path == "seg" else 0, 1)
+def set_path(ctx, path):
+    """Library options of a path ("staged" = the defaults)."""
     ctx.set_option(WC_OPT_SPARSE, 0 if path == "dense" else 1)
+    ctx.set_option(WC_OPT_ORDERED, 0 if path == "tickets" else 1)
 
 
-def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None, path="staged", lag=0, ring=0):
+def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None, path="staged"):
     units, n, extent, cells = pack(wc, boxes, dtype, offsets)
-    set_path(ctx, path, lag, ring)
+    set_path(ctx, path)
     try:
         payload, offs, kept = ctx.forward_host(cells, units, n, keep)
     finally:
@@ -59,11 +57,11 @@ def oracle_payload(O, b, keep):
     return O.compress_payload(b32, keep)[0]
 
 
-# Forward paths, all byte-identical: the library default (look-back emit
-# tiles, sparse staging of 32-coefficient segments); "dense" staging (WC_OPT_SPARSE 0); whole-unit emit forced for units of <= 64 tiles, beside look-back
-# tiles for larger units in the same launch; chunked two-stream (16 Ki-cell
-# chunks, 2 coefficient slots); the pipelined single launch.
-PATHS = ["staged", "dense", "seg", "chunked", "pipe"]
+# Forward paths, all byte-identical: the library default (sparse staging of
+# 32-coefficient segments, look-back tile index from the launch order);
+# "dense" staging (WC_OPT_SPARSE 0); "tickets": the look-back tile index from
+# per-unit ticket atomics (WC_OPT_ORDERED 0: no dispatch-order assumption).
+PATHS = ["staged", "dense", "tickets"]
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -208,12 +206,17 @@ def test_empty_and_degenerate_units(wc, ctx, oracle):
             assert got[i] == oracle.compress_payload(b, keep)[0]
 
 
+@pytest.mark.parametrize("path", ["staged", "tickets"])
 @pytest.mark.parametrize("keep", [KEEPS[0], KEEPS[2]])
-def test_inverse_bit_exact(wc, ctx, oracle, keep):
+def test_inverse_bit_exact(wc, ctx, oracle, keep, path):
     boxes = synth(oracle, DIMS, seed0=4)
     units, n, extent, cells = pack(wc, boxes)
     payload, offs, kept = ctx.forward_host(cells, units, n, keep)
-    regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
+    set_path(ctx, path)
+    try:
+        regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
+    finally:
+        set_path(ctx, "staged")
     for i, b in enumerate(boxes):
         o = units[i].cell_offset
         p = wc.capi.unit_payload(payload, offs, kept, i)
@@ -304,11 +307,13 @@ def test_malformed_payload_rejected(wc, ctx, oracle):
         assert ei.value.code == wc.capi.WC_ERR_FORMAT
 
 
-def test_rle_decode_out_of_range_pairs_dropped(wc, ctx, oracle):
-    """rle_decode drops pairs whose index reaches total (src/decompressor.cpp:23)."""
+@pytest.mark.parametrize("runs", [[0, 3, 10, 0], [0] * 40, [2] * 7 + [0] * 30, [15, 0, 0, 4]])
+def test_rle_decode_out_of_range_pairs_dropped(wc, ctx, oracle, runs):
+    """rle_decode drops pairs whose index reaches total (src/decompressor.cpp:20-27),
+    also when the payload holds more pairs than coefficients (nrle > ncoeff)."""
     W, H, D = 4, 2, 2
-    runs = np.array([0, 3, 10, 0], np.int32)
-    vals = np.array([1.5, 2.5, 3.5, 4.5], np.float32)
+    runs = np.array(runs, np.int32)
+    vals = (np.arange(runs.size, dtype=np.float32) + 1.5).astype(np.float32)
     p = oracle.serialize(W, H, D, W * H * D, runs, vals)
     units, n, extent = wc.capi.make_units([(W, H, D)])
     buf = np.zeros(len(p) + 16, np.uint8)
@@ -317,6 +322,41 @@ def test_rle_decode_out_of_range_pairs_dropped(wc, ctx, oracle):
     flat = oracle.rle_decode(runs, vals, W * H * D)
     want = oracle.inverse_wavelet_decompose(flat, W, H, D).ravel()
     assert out.tobytes() == want.tobytes()
+
+
+def test_format_error_survives_later_calls(wc, ctx, oracle):
+    """A malformed payload in an async wc_inverse is reported at the next
+    synchronisation even when a forward (whose emit can raise errors too) runs in
+    between; the error word is cleared once read."""
+    import torch
+    b = synth(oracle, [(8, 8, 8)], seed0=6)[0]
+    p = bytearray(oracle_payload(oracle, b, KEEPS[1]))
+    p[0] = 9  # W mismatch
+    units, n, extent = wc.capi.make_units([(8, 8, 8)])
+    dev = torch.device("cuda", 0)
+    host = np.zeros(len(p) + 16, np.uint8)
+    host[4:4 + len(p)] = np.frombuffer(bytes(p), np.uint8)
+    d_pay = torch.from_numpy(host).to(dev)
+    d_off = torch.tensor([4], dtype=torch.int64, device=dev)
+    d_out = torch.zeros(extent, dtype=torch.float32, device=dev)
+    cells = torch.from_numpy(b.ravel().copy()).to(dev)
+    cap = wc.capi.payload_bound(units, n)
+    d_p2 = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    d_o2 = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    d_k2 = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def fwd():
+        ctx.forward(cells.data_ptr(), wc.capi.WC_F64, units, n, KEEPS[1], d_p2.data_ptr(), cap,
+                    d_o2.data_ptr(), d_k2.data_ptr())
+
+    ctx.inverse(d_pay.data_ptr(), d_off.data_ptr(), units, n, d_out.data_ptr())
+    fwd()
+    with pytest.raises(wc.WaveletError) as ei:
+        ctx.synchronize()
+    assert ei.value.code == wc.capi.WC_ERR_FORMAT
+    fwd()
+    ctx.synchronize()  # cleared once read: the next check is clean
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -343,76 +383,6 @@ def test_128cubed_fp32_and_mixed_sizes(wc, ctx, oracle, path):
     got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, path=path)
     for i, b in enumerate(boxes):
         assert got[i] == oracle.compress_payload(b, keep)[0], dims[i]
-
-
-@pytest.mark.parametrize("lag,ring", [(0, 4096), (1, 8192), (100_000, 40_000), (1, 300_000)])
-def test_pipe_ring_reuse_and_waits(wc, ctx, oracle, lag, ring):
-    """The pipelined kernel with a coefficient ring far smaller than the batch:
-    transform tiles wait for the emit tiles of the units whose ring chunks they
-    overwrite (wait lists), and emit tiles come right after (lag 1) or long
-    after their unit's transform tiles.  Mixed shapes, odd dims, an empty unit
-    and a unit larger than the requested ring (the ring grows to fit it)."""
-    keep = KEEPS[1]
-    dims = [(16, 16, 16), (32, 32, 32), (3, 5, 7), (64, 64, 64), (0, 4, 4), (48, 32, 16), (16, 16, 16),
-            (33, 17, 9), (64, 64, 64), (8, 4, 2), (32, 32, 32), (2, 200, 3)] * 3
-    boxes = synth(oracle, dims, seed0=11)
-    got, kept = gpu_payloads(wc, ctx, boxes, keep, path="pipe", lag=lag, ring=ring)
-    for i, b in enumerate(boxes):
-        assert got[i] == oracle_payload(oracle, b, keep), (i, dims[i])
-
-
-@pytest.mark.parametrize("chunk,slots", [(4096, 2), (100_000, 3), (1 << 20, 2)])
-def test_chunked_slot_reuse(wc, ctx, oracle, chunk, slots):
-    """Chunked forward: a coefficient slot is rewritten only after the emit that read it;
-    chunks smaller than one unit, mixed shapes, odd dims and an empty unit."""
-    keep = KEEPS[1]
-    dims = [(16, 16, 16), (32, 32, 32), (3, 5, 7), (64, 64, 64), (0, 4, 4), (48, 32, 16), (33, 17, 9),
-            (64, 64, 64), (8, 4, 2), (2, 200, 3)] * 2
-    boxes = synth(oracle, dims, seed0=13)
-    units, n, extent, cells = pack(wc, boxes)
-    ctx.set_chunk(chunk, slots)
-    try:
-        payload, offs, kept = ctx.forward_host(cells, units, n, keep)
-    finally:
-        ctx.set_chunk(0)
-    for i, b in enumerate(boxes):
-        assert wc.capi.unit_payload(payload, offs, kept, i) == oracle_payload(oracle, b, keep), (i, dims[i])
-
-
-def test_whole_unit_emit_beside_lookback_tiles(wc, ctx, oracle):
-    """One k_emit launch: units of <= 2 emit tiles packed whole by one workgroup, the larger
-    ones through look-back tiles; empty and single-cell units among them."""
-    keep = KEEPS[0]
-    dims = [(16, 16, 16), (32, 32, 32), (0, 3, 3), (40, 40, 70), (1, 1, 1), (64, 64, 64), (6, 10, 14),
-            (128, 16, 8), (2, 2, 2)]
-    boxes = synth(oracle, dims, seed0=14)
-    units, n, extent, cells = pack(wc, boxes)
-    ctx.set_emit_seg(2, 1)
-    try:
-        payload, offs, kept = ctx.forward_host(cells, units, n, keep)
-    finally:
-        ctx.set_emit_seg()
-    for i, b in enumerate(boxes):
-        assert wc.capi.unit_payload(payload, offs, kept, i) == oracle_payload(oracle, b, keep), (i, dims[i])
-
-
-def test_pipe_stats_counters(wc, ctx, oracle):
-    """WC_OPT_PIPE_STATS: the diagnostics count every work-list item once."""
-    dims = [(64, 64, 64)] * 8 + [(16, 16, 16)] * 4
-    boxes = synth(oracle, dims, seed0=12)
-    units, n, extent, cells = pack(wc, boxes)
-    ctx.set_pipe(True)
-    ctx.set_option(wc.capi.WC_OPT_PIPE_STATS, 1)
-    try:
-        payload, offs, kept = ctx.forward_host(cells, units, n, KEEPS[1])
-        st = ctx.pipe_stats()
-    finally:
-        ctx.set_option(wc.capi.WC_OPT_PIPE_STATS, 0)
-        ctx.set_pipe(False)
-    assert st[6] == 8 * 32 + 4 * 1   # transform tiles: 64^3 -> 32 tiles of 64x2x64, 16^3 -> 1
-    assert st[7] == 8 + 4            # emit items: one whole-unit item per unit
-    for i, b in enumerate(boxes):
-        assert wc.capi.unit_payload(payload, offs, kept, i) == oracle_payload(oracle, b, KEEPS[1])
 
 
 def test_reference_wavelet_decomposition_case(wc):

@@ -2,7 +2,7 @@
 
 usage: python tools/pmc_summary.py <kernel_stats.csv> [--fetch fetch_counter_collection.csv]
                                    [--write write_counter_collection.csv] [--out profiles/x.json]
-                                   [--boxes N --dtype f64]
+                                   [--workload c2 --dtype f64]
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  Per MI355X_MICROARCH.md §HBM,
 on gfx950 FETCH_SIZE reads exactly 1/2 of a wide coalesced stream's bytes, so
@@ -11,12 +11,19 @@ read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE reads the bytes exactly for
 """
 import argparse
 import csv
+import datetime
 import json
-import re
+import subprocess
+import sys
 from collections import defaultdict
+from pathlib import Path
 
-STAGE_OF = [("k_forward_pipe", "pipe"), ("k_transform_fallback", "fallback"), ("k_transform", "transform"), ("k_emit", "flat_emit"),
-            ("k_decode", "decode"), ("k_inverse", "inverse"), ("k_rmse", "rmse")]
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+STAGE_OF = [("k_transform_fallback", "fallback"), ("k_transform", "transform"), ("k_emit", "emit"),
+            ("k_rowindex", "rowindex"), ("k_decode", "decode"), ("k_inverse", "inverse"), ("k_rmse", "rmse"),
+            ("k_hist", "hist")]
 
 
 def stage(name):
@@ -44,9 +51,10 @@ def main():
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--out")
-    ap.add_argument("--boxes", type=int, default=1024)
+    ap.add_argument("--workload", default="c2")
     ap.add_argument("--dtype", default="f64")
     a = ap.parse_args()
+    from bench import kernel_sources_sha  # the bench only trusts counters of the same sources
     kern = {}
     with open(a.stats) as f:
         for row in csv.DictReader(f):
@@ -54,7 +62,9 @@ def main():
             if st:
                 kern[st] = {"name": row["Name"][:80], "calls": int(row["Calls"]),
                             "avg_us": float(row["AverageNs"]) / 1e3, "pct": float(row["Percentage"])}
-    out = {"config": {"boxes": a.boxes, "dtype": a.dtype}, "kernels": kern}
+    git = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True, cwd=ROOT).stdout.strip()
+    out = {"config": {"workload": a.workload, "dtype": a.dtype}, "date": datetime.date.today().isoformat(),
+           "git": git, "kernel_sources_sha": kernel_sources_sha(), "kernels": kern}
     per = {}
     if a.fetch:
         fk = counters(a.fetch, "FETCH_SIZE")

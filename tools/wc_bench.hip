@@ -5,12 +5,10 @@
 // Box-Muller noise), then wc_forward runs `steps` times.  Prints one JSON line.
 //
 // usage: wc_bench [boxes=1024] [dim=64] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1]
-//                 [pipe=1|0] [check=0|1] [lag=0] [ring=0] [claim=1] [prefetch=0] [wgs=0] [stats=0]
-//                 [chunk=0] [slots=2] [seg=0] [segmin=256]
-// check=1: also run the plain staged path (look-back emit only) once and
-// compare every unit's payload bytes with the configured path's
-// ("paths_identical" in the JSON line).
-// lag / ring: WC_OPT_PIPE_LAG / WC_OPT_PIPE_RING (0 = library defaults).
+//                 [check=0|1] [ordered=1] [sparse=1]
+// check=1: also run the conservative configuration (ticket look-back, dense
+// staging) once and compare every unit's payload bytes and, with inverse=1,
+// every reconstructed cell ("paths_identical" in the JSON line).
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -63,18 +61,9 @@ int main(int argc, char** argv) {
     const int steps = argc > 5 ? std::atoi(argv[5]) : 10;
     const int warmup = argc > 6 ? std::atoi(argv[6]) : 2;
     const bool inverse = argc > 7 ? std::atoi(argv[7]) != 0 : false;
-    const bool pipe = argc > 8 ? std::atoi(argv[8]) != 0 : false;  // library default: staged
-    const bool check = argc > 9 ? std::atoi(argv[9]) != 0 : false;
-    const long long lag = argc > 10 ? std::atoll(argv[10]) : 0;
-    const long long ring = argc > 11 ? std::atoll(argv[11]) : 0;
-    const int claim = argc > 12 ? std::atoi(argv[12]) : 1;
-    const int prefetch = argc > 13 ? std::atoi(argv[13]) : 0;
-    const int wgs = argc > 14 ? std::atoi(argv[14]) : 0;
-    const int stats = argc > 15 ? std::atoi(argv[15]) : 0;
-    const long long chunk = argc > 16 ? std::atoll(argv[16]) : 0;
-    const int slots = argc > 17 ? std::atoi(argv[17]) : 2;
-    const int seg = argc > 18 ? std::atoi(argv[18]) : 0;  // library default
-    const int segmin = argc > 19 ? std::atoi(argv[19]) : 256;
+    const bool check = argc > 8 ? std::atoi(argv[8]) != 0 : false;
+    const int ordered = argc > 9 ? std::atoi(argv[9]) : 1;
+    const int sparse = argc > 10 ? std::atoi(argv[10]) : 1;
 
     std::vector<wc_unit> units(boxes);
     const unsigned long long per = (unsigned long long)dim * dim * dim;
@@ -103,16 +92,8 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "wc_ctx_create failed\n");
         return 2;
     }
-    wc_set_option(ctx, WC_OPT_PIPE, pipe ? 1 : 0);
-    wc_set_option(ctx, WC_OPT_PIPE_LAG, lag);
-    wc_set_option(ctx, WC_OPT_PIPE_RING, ring);
-    wc_set_option(ctx, WC_OPT_PIPE_CLAIM, claim);
-    wc_set_option(ctx, WC_OPT_PIPE_PREFETCH, prefetch);
-    wc_set_option(ctx, WC_OPT_PIPE_WGS, wgs);
-    wc_set_option(ctx, WC_OPT_CHUNK, chunk);
-    wc_set_option(ctx, WC_OPT_CHUNK_SLOTS, slots);
-    wc_set_option(ctx, WC_OPT_EMIT_SEG_MAX, seg);
-    wc_set_option(ctx, WC_OPT_EMIT_SEG_MIN_UNITS, segmin);
+    wc_set_option(ctx, WC_OPT_ORDERED, ordered);
+    wc_set_option(ctx, WC_OPT_SPARSE, sparse);
     auto fwd = [&]() {
         int rc = wc_forward(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, keep, payload, cap, offsets, kept);
         if (rc != WC_OK) {
@@ -132,7 +113,6 @@ int main(int argc, char** argv) {
         if (inverse) inv();
     }
     wc_synchronize(ctx);
-    if (stats) wc_set_option(ctx, WC_OPT_PIPE_STATS, 1);
     wc_profile_enable(ctx, 1);
     double ms[WC_NUM_STAGES];
     uint32_t cnt[WC_NUM_STAGES];
@@ -154,39 +134,46 @@ int main(int argc, char** argv) {
         wc_profile_read(ctx, ims, icnt, WC_NUM_STAGES);
     }
     const double step_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() / steps;
-    uint64_t st[8] = {};
-    if (stats) {
-        wc_pipe_stats(ctx, st, 8);
-        wc_set_option(ctx, WC_OPT_PIPE_STATS, 0);
-    }
     int identical = -1;
     if (check) {
-        // Configured path vs the plain staged path: every unit's serialized bytes must match.
+        // Configured path vs the conservative one (ticket look-back, dense
+        // staging): every unit's serialized bytes and reconstructed cells.
         std::vector<uint64_t> off_a(boxes + 1), off_b(boxes + 1);
         std::vector<uint32_t> k_a(boxes), k_b(boxes);
         std::vector<uint8_t> pa(cap), pb(cap);
-        fwd();
-        wc_synchronize(ctx);
-        CK(hipMemcpy(off_a.data(), offsets, 8 * (boxes + 1), hipMemcpyDeviceToHost));
-        CK(hipMemcpy(k_a.data(), kept, 4 * boxes, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(pa.data(), payload, cap, hipMemcpyDeviceToHost));
-        CK(hipMemset(payload, 0xA5, cap));
-        wc_set_option(ctx, WC_OPT_PIPE, 0);
-        wc_set_option(ctx, WC_OPT_CHUNK, 0);
-        wc_set_option(ctx, WC_OPT_EMIT_SEG_MAX, 0);
-        fwd();
-        wc_synchronize(ctx);
-        CK(hipMemcpy(off_b.data(), offsets, 8 * (boxes + 1), hipMemcpyDeviceToHost));
-        CK(hipMemcpy(k_b.data(), kept, 4 * boxes, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(pb.data(), payload, cap, hipMemcpyDeviceToHost));
+        std::vector<float> ra, rb;
+        auto run = [&](std::vector<uint64_t>& off, std::vector<uint32_t>& k, std::vector<uint8_t>& pl,
+                       std::vector<float>& rg) {
+            CK(hipMemset(payload, 0xA5, cap));
+            fwd();
+            if (inverse) {
+                CK(hipMemset(regen, 0xA5, 4 * per * boxes));
+                inv();
+            }
+            if (wc_synchronize(ctx) != WC_OK) {
+                std::fprintf(stderr, "check: %s\n", wc_last_error(ctx));
+                std::exit(2);
+            }
+            CK(hipMemcpy(off.data(), offsets, 8 * (boxes + 1), hipMemcpyDeviceToHost));
+            CK(hipMemcpy(k.data(), kept, 4 * boxes, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(pl.data(), payload, cap, hipMemcpyDeviceToHost));
+            if (inverse) {
+                rg.resize(per * boxes);
+                CK(hipMemcpy(rg.data(), regen, 4 * per * boxes, hipMemcpyDeviceToHost));
+            }
+        };
+        run(off_a, k_a, pa, ra);
+        wc_set_option(ctx, WC_OPT_ORDERED, 0);
+        wc_set_option(ctx, WC_OPT_SPARSE, 0);
+        run(off_b, k_b, pb, rb);
+        wc_set_option(ctx, WC_OPT_ORDERED, ordered);
+        wc_set_option(ctx, WC_OPT_SPARSE, sparse);
         identical = 1;
         for (int i = 0; i < boxes && identical; ++i) {
             if (k_a[i] != k_b[i] || off_a[i] != off_b[i]) identical = 0;
             else if (std::memcmp(pa.data() + off_a[i], pb.data() + off_b[i], 20 + 8ull * k_a[i]) != 0) identical = 0;
         }
-        wc_set_option(ctx, WC_OPT_PIPE, pipe ? 1 : 0);
-        wc_set_option(ctx, WC_OPT_CHUNK, chunk);
-        wc_set_option(ctx, WC_OPT_EMIT_SEG_MAX, seg);
+        if (inverse && identical && std::memcmp(ra.data(), rb.data(), 4 * ra.size()) != 0) identical = 0;
     }
     uint64_t total = 0;
     CK(hipMemcpy(&total, offsets + boxes, 8, hipMemcpyDeviceToHost));
@@ -194,14 +181,12 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(hk.data(), kept, 4 * boxes, hipMemcpyDeviceToHost));
     double ksum = 0;
     for (uint32_t k : hk) ksum += k;
-    const char* names[WC_NUM_STAGES] = {"transform", "flat_count", "unit_scan", "unit_offsets",
-                                        "flat_emit", "decode", "inverse", "rmse", "pipe", "chunked", "hist"};
+    const char* names[WC_NUM_STAGES] = {"transform", "emit", "decode", "inverse", "rmse", "hist"};
     std::printf("{\"boxes\": %d, \"dim\": %d, \"dtype\": \"%s\", \"keep\": %.17g, \"steps\": %d, "
                 "\"ms_per_step\": %.4f, \"cells_per_s\": %.6e, \"kept_fraction\": %.6f, \"payload_bytes\": %llu, "
-                "\"pipe\": %d, \"lag\": %lld, \"ring\": %lld, \"chunk\": %lld, \"slots\": %d, \"seg\": %d, "
-                "\"paths_identical\": %d, \"stage_ms\": {",
+                "\"ordered\": %d, \"sparse\": %d, \"paths_identical\": %d, \"stage_ms\": {",
                 boxes, dim, f64 ? "f64" : "f32", keep, steps, step_ms, per * boxes / (step_ms * 1e-3),
-                ksum / (double)(per * boxes), (unsigned long long)total, pipe ? 1 : 0, lag, ring, chunk, slots, seg, identical);
+                ksum / (double)(per * boxes), (unsigned long long)total, ordered, sparse, identical);
     bool first = true;
     for (int s = 0; s < WC_NUM_STAGES; ++s)
         if (cnt[s]) {
@@ -218,14 +203,6 @@ int main(int argc, char** argv) {
             }
     }
     std::printf("}");
-    if (stats) {
-        // per item averages in microseconds (ticks are 10 ns)
-        const double nT = st[6] ? (double)st[6] : 1.0, nE = st[7] ? (double)st[7] : 1.0;
-        std::printf(", \"pipe_us\": {\"T\": %.2f, \"T_ringwait\": %.2f, \"E\": %.2f, \"E_tdwait\": %.2f, "
-                    "\"E_lookback\": %.2f, \"claim_per_batch\": %.2f, \"nT\": %.0f, \"nE\": %.0f}",
-                    st[0] / nT / 100.0, st[1] / nT / 100.0, st[2] / nE / 100.0, st[3] / nE / 100.0,
-                    st[4] / nE / 100.0, st[5] / ((nT + nE) / claim) / 100.0, nT / steps, nE / steps);
-    }
     std::printf("}\n");
     wc_ctx_destroy(ctx);
     (void)hipFree(cells);

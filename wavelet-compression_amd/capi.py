@@ -27,18 +27,14 @@ EXPORTED = (
     "wc_payload_bound", "wc_cell_count", "wc_forward", "wc_forward_host", "wc_decompose",
     "wc_inverse", "wc_inverse_host", "wc_inverse_flat", "wc_rmse", "wc_version",
     "wc_profile_enable", "wc_profile_read", "wc_set_option", "wc_inverse_flat_host", "wc_rmse_host",
-    "wc_decompose_host", "wc_device_count", "wc_pipe_stats", "wc_forward_stage", "wc_hist_threshold",
+    "wc_decompose_host", "wc_device_count", "wc_forward_stage", "wc_hist_threshold",
     "wc_forward_emit",
 )
-WC_OPT_PIPE, WC_OPT_PIPE_LAG, WC_OPT_PIPE_RING = 1, 2, 3
-WC_OPT_PIPE_CLAIM, WC_OPT_PIPE_PREFETCH, WC_OPT_PIPE_WGS, WC_OPT_PIPE_STATS = 4, 5, 6, 7
-WC_OPT_CHUNK, WC_OPT_CHUNK_SLOTS = 8, 9
-WC_OPT_EMIT_SEG_MAX, WC_OPT_EMIT_SEG_MIN_UNITS = 10, 11
-WC_OPT_SPARSE = 12
+WC_OPT_SPARSE = 12   # sparse coefficient staging in the forward (default 1)
+WC_OPT_ORDERED = 13  # look-back tile index from the launch order (1, default) or per-unit tickets (0)
 
-# Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*), kernel names as rocprof shows them.
-STAGES = ("transform", "flat_count", "unit_scan", "unit_offsets", "flat_emit", "decode", "inverse", "rmse",
-          "pipe", "chunked", "hist")
+# Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*).
+STAGES = ("transform", "emit", "decode", "inverse", "rmse", "hist")
 
 
 class WcUnit(ctypes.Structure):
@@ -91,7 +87,6 @@ def load_library() -> ctypes.CDLL:
         "wc_rmse_host": (i32, [vp, vp, i32, vp, up, i32, vp]),
         "wc_decompose_host": (i32, [vp, vp, i32, up, i32, vp]),
         "wc_profile_read": (i32, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32), i32]),
-        "wc_pipe_stats": (i32, [vp, ctypes.POINTER(ctypes.c_uint64), i32]),
         "wc_forward_stage": (i32, [vp, vp, i32, up, i32, vp]),
         "wc_hist_threshold": (i32, [vp, ctypes.c_double, ctypes.POINTER(ctypes.c_float),
                                     ctypes.POINTER(ctypes.c_uint64)]),
@@ -189,31 +184,6 @@ class Context:
 
     def set_option(self, option: int, value: int):
         self._check(self._L.wc_set_option(self._h, int(option), int(value)))
-
-    def set_pipe(self, on: bool, lag: int = 0, ring: int = 0):
-        """wc_forward as one pipelined launch or as the staged kernels (default);
-        lag / ring tune the pipeline (0 = library defaults)."""
-        self.set_option(WC_OPT_PIPE, 1 if on else 0)
-        self.set_option(WC_OPT_PIPE_LAG, lag)
-        self.set_option(WC_OPT_PIPE_RING, ring)
-
-    def set_chunk(self, cells: int, slots: int = 2):
-        """Chunked forward: one launch per chunk transforms it and packs the previous chunk
-        (cells per chunk; 0 = the whole batch at once)."""
-        self.set_option(WC_OPT_CHUNK, cells)
-        self.set_option(WC_OPT_CHUNK_SLOTS, slots)
-
-    def set_emit_seg(self, max_tiles: int = 0, min_units: int = 256):
-        """Staged emit: units of <= max_tiles 8192-coefficient tiles packed whole by one
-        workgroup when the batch holds >= min_units of them (max_tiles 0: never, the default)."""
-        self.set_option(WC_OPT_EMIT_SEG_MAX, max_tiles)
-        self.set_option(WC_OPT_EMIT_SEG_MIN_UNITS, min_units)
-
-    def pipe_stats(self) -> list:
-        """wc_pipe_stats: pipelined-kernel diagnostics since the last read (8 counters)."""
-        out = (ctypes.c_uint64 * 8)()
-        self._check(self._L.wc_pipe_stats(self._h, out, 8))
-        return list(out)
 
     def profile_enable(self, on: bool = True):
         self._check(self._L.wc_profile_enable(self._h, 1 if on else 0))

@@ -227,6 +227,12 @@ void inverse_batch(const std::vector<std::string>& payloads, const std::vector<w
     uint64_t cur = 4;
     for (size_t i = 0; i < payloads.size(); ++i) {
         if (payloads[i].size() < 20) fatal("Deserialization failed: payload shorter than its header");
+        // wc_inverse_host sizes the device copy from each header's nrle: a truncated
+        // or corrupt stream must not make it read past this buffer
+        int32_t nrle;
+        std::memcpy(&nrle, payloads[i].data() + 16, 4);
+        if (nrle < 0 || 20 + 8 * (uint64_t)nrle > payloads[i].size())
+            fatal("Deserialization failed: payload holds fewer pairs than its header's nrle");
         offs[i] = cur;
         cur += (payloads[i].size() + 4 + 7) / 8 * 8;
     }

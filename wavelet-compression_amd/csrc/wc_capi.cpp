@@ -5,17 +5,12 @@
 // exists: every computing entry point launches HIP kernels and fails with
 // WC_ERR_HIP if the device or code object is absent.
 //
-// Forward path per batch (wc_forward), every unit shape:
-//   WC_OPT_PIPE = 0 (default): staged kernels: k_transform{,_fast} -> flat
-//       coefficients in HBM scratch -> k_emit (threshold + ordered pack:
-//       whole units per workgroup, or emit tiles with decoupled look-back);
-//       WC_OPT_CHUNK > 0 cuts the batch into chunks: one launch per chunk
-//       transforms it and packs the previous one (k_chunk)
-//   WC_OPT_PIPE = 1: k_forward_pipe, one persistent launch: transform
-//       tiles -> coefficient ring (Infinity-Cache resident) -> emit tiles
-//       (threshold + decoupled look-back + pack), interleaved by a host-built
-//       work list (wc_pipe.hip); latency-bound today
-// Both write unit u's serialized bytes at its fixed slot offsets[u].
+// Forward path per batch (wc_forward), every unit shape: K1 k_transform{,_fast}
+// -> flat coefficients in HBM scratch (sparse staging: only the flagged
+// segments) + per-unit max keys -> k_transform_fallback (units whose thresh
+// is < 0 re-staged densely) -> K2 k_emit (threshold + decoupled look-back +
+// ordered pack), writing unit u's serialized bytes at its fixed slot
+// offsets[u].  Inverse: K5 k_decode -> dense flat scratch -> K6 k_inverse{,_fast}.
 #include "wavelet_amd.h"
 #include "wc_internal.h"
 
@@ -30,8 +25,6 @@
 namespace wc {
 size_t transform_lds_bytes(int lbx, int lby, int lbz);
 size_t transform_fast_lds_bytes(int lbx, int lby, int lbz);
-size_t pipe_lds_bytes(size_t tile_lds);
-uint32_t pipe_grid(int dtype, size_t lds, int max_per_cu);
 hipError_t launch_transform(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
                             float*, int, unsigned long long*);
 hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
@@ -40,18 +33,14 @@ hipError_t launch_transform_fallback(hipStream_t, const void*, int, const UnitDe
                                      const unsigned long long*, double);
 hipError_t launch_pack(hipStream_t, const UnitDev*, int, const uint32_t*, const uint8_t*, uint64_t*, uint8_t*);
 hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, const uint8_t*, const uint64_t*,
-                         uint32_t*, unsigned long long*, float*, uint32_t*);
+                         uint32_t*, unsigned long long*, float*, uint32_t*, int);
 hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const XTile*, uint32_t, size_t, uint32_t,
                           size_t, float*);
 hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDev*, int, const FTile*,
                        uint32_t, double*, double*);
-hipError_t launch_forward_pipe(hipStream_t, int, size_t, uint32_t, const PipeParams&);
-hipError_t launch_emit(hipStream_t, const PipeParams&, const float*, uint32_t, uint32_t);
+hipError_t launch_emit(hipStream_t, const EmitParams&, const float*, uint32_t);
 hipError_t launch_hist(hipStream_t, const UnitDev*, const FTile*, uint32_t, const float*, uint32_t,
                        unsigned long long*);
-size_t chunk_lds_bytes(size_t tile_lds);
-hipError_t launch_chunk(hipStream_t, int, size_t, const PipeParams&, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t,
-                        uint32_t);
 }  // namespace wc
 
 using namespace wc;
@@ -64,41 +53,24 @@ struct DevBuf {
 };
 
 // A batch plan: unit descriptors and tile lists, mirrored in HBM.
-//   xtiles = [generic | fast]   transform tiles, unit-major in each part (the
-//                               staged kernels launch each part; the inverse
-//                               and the pipe's work list index all of them)
-//   ftiles                      kFlatTile flat tiles (staged forward, decode, RMSE)
-//   etiles, items, waits        the pipelined forward's emit tiles, work list
-//                               and ring wait lists (built when WC_OPT_PIPE)
+//   xtiles = [generic | fast]   transform tiles, unit-major in each part
+//   ixtiles                     the same, fast tiles in reverse unit order (inverse)
+//   ftiles                      kFlatTile flat tiles (RMSE, histogram)
+//   dtiles                      decode blocks, interleaved by tile index across units
+//   eunits, eidx                emit blocks: unit and tile index, interleaved order
 struct Plan {
     std::vector<wc_unit> key;
-    bool pipe = true;
-    int64_t lag = 0, ring_req = 0;
     std::vector<UnitDev> units;
     std::vector<XTile> xtiles;
     std::vector<XTile> ixtiles;  // inverse launch order (see get_plan)
-    std::vector<FTile> ftiles, etiles, dtiles;
-    std::vector<uint32_t> items, waits, segs, eunits, eidx;
-    int seg_max = 0, seg_min = 0;  // whole-unit emit: WC_OPT_EMIT_SEG_MAX / _MIN_UNITS
-    uint32_t ngen = 0, nfast = 0;
+    std::vector<FTile> ftiles, dtiles;
+    std::vector<uint32_t> eunits, eidx;
+    uint32_t ngen = 0, nfast = 0, netiles = 0;
     bool any_sparse = false;
     uint64_t coef_extent = 0;  // floats of staged coefficient scratch
-    uint64_t ring_floats = 0;  // pipe coefficient ring
-    size_t lds_gen = 0, lds_fast = 0, lds_inverse = 0, lds_pipe = 0;
-    size_t state_bytes = 0;    // pipe per-call state: ticket | key[n] | tdone[n] | edone[n] | status[netiles]
-    // chunked forward (WC_OPT_CHUNK): unit ranges whose coefficients fit one slot
-    struct Chunk {
-        uint32_t u0, u1;            // units [u0, u1)
-        uint32_t gen_b, gen_n;      // generic transform tiles
-        uint32_t fast_b, fast_n;    // fast transform tiles
-        uint32_t et_b, et_n;        // look-back emit tiles
-        uint32_t seg_b, seg_n;      // whole-unit emit entries
-    };
-    int64_t chunk_req = 0;
-    std::vector<Chunk> chunks;
-    uint64_t slot_floats = 0;
-    int nslots = 0;
-    DevBuf d_units, d_xtiles, d_ftiles, d_etiles, d_items, d_waits, d_segs, d_dtiles, d_eunits, d_ixtiles, d_eidx;
+    size_t lds_gen = 0, lds_fast = 0, lds_inverse = 0;
+    size_t state_bytes = 0;    // forward per-call state: 16 | key[n] | tickets[n] | status[netiles]
+    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_eunits, d_ixtiles, d_eidx;
 };
 
 int ceil_log2(int64_t v) {
@@ -116,27 +88,20 @@ struct wc_ctx {
     std::string err;
     Plan plan;
     bool plan_valid = false;
-    bool opt_pipe = false;   // WC_OPT_PIPE default (see include/wavelet_amd.h)
-    int64_t opt_lag = 0;     // WC_OPT_PIPE_LAG (0 = default)
-    int64_t opt_ring = 0;    // WC_OPT_PIPE_RING (0 = default)
-    uint32_t opt_claim = 1;  // WC_OPT_PIPE_CLAIM
-    bool opt_prefetch = false;  // WC_OPT_PIPE_PREFETCH
-    int opt_wgs = 0;         // WC_OPT_PIPE_WGS (0 = occupancy limit)
-    bool opt_stats = false;  // WC_OPT_PIPE_STATS
-    int64_t opt_chunk = 0;   // WC_OPT_CHUNK: cells per chunk (0 = whole batch at once)
-    int opt_slots = 2;       // WC_OPT_CHUNK_SLOTS
-    int opt_seg_max = 0;     // WC_OPT_EMIT_SEG_MAX (0: look-back tiles only, the faster layout measured)
-    int opt_seg_min = 256;   // WC_OPT_EMIT_SEG_MIN_UNITS
+    bool opt_ordered = true;  // WC_OPT_ORDERED (see include/wavelet_amd.h)
+    bool opt_sparse = true;   // WC_OPT_SPARSE
+    // A kernel that may raise error bits ran since the last check.  Kernels
+    // atomicOr into ONE persistent error word (errflag, zeroed at creation and
+    // after each read), so errors of several async calls accumulate until the
+    // next wc_synchronize / _host call reads them.
     bool err_check_pending = false;
-    uint32_t* err_src = nullptr;  // device error word of the pending call (null: errflag)
     // wc_forward_stage left this plan's coefficients + unit keys in coef/state
     // (cleared by set_device, i.e. by every other compute entry point)
     bool staged = false;
     bool sparse_staged = false;  // the last stage_transform used sparse staging
-    bool opt_sparse = true;      // WC_OPT_SPARSE
     uint64_t plan_gen = 0;  // bumped whenever get_plan rebuilds the plan
     // scratch (grow-only)
-    DevBuf coef, part, errflag, ring, state, stats, flags;
+    DevBuf coef, part, errflag, state, flags;
     // host-path staging
     DevBuf h_cells, h_payload, h_packed, h_offsets, h_poff, h_kept, h_out;
     // per-kernel event timing (wc_profile_enable / wc_profile_read)
@@ -246,57 +211,35 @@ void push_tiles(std::vector<XTile>& v, const UnitDev& d, uint32_t u) {
             for (int bx = 0; bx < d.nbx; bx += TX) v.push_back(XTile{u, (uint32_t)bx, (uint32_t)by, (uint32_t)bz});
 }
 
-constexpr int64_t kDefaultLag = int64_t(16) << 20;   // cells of transform work between a unit and its emit work
-constexpr int64_t kDefaultRingExtra = int64_t(8) << 20;  // ring floats beyond the lag (tiles in flight)
-
 uint64_t round_up(uint64_t v, uint64_t m) { return (v + m - 1) / m * m; }
 
-// Emit work of the staged paths.  Units of at most seg_max emit tiles are
-// packed whole, one workgroup each (segs), when the batch holds at least
-// seg_min of them (enough workgroups to fill the device) and is not cut into
-// chunks; every other unit is split into emit tiles of kEmitTile flat
-// coefficients packed with decoupled look-back (at least one per unit: an
-// empty unit's tile writes its header).
+// Emit tiles: every unit is split into emit tiles of kEmitTile flat
+// coefficients (at least one per unit: an empty unit's tile writes its
+// header).  Dispatch order of the emit blocks: interleaved by tile index
+// across the units of a group, so that a tile's look-back predecessors (the
+// lower tile indices of its unit) have lower block ids and the per-unit
+// traffic spreads over the group instead of arriving in one burst.  Groups
+// hold >= 8192 tiles (256 MB of fp32 coefficients, the Infinity Cache's size)
+// and >= 128 x the longest unit's tile chain (a look-back chain advances one
+// tile per status round trip, so long chains need the whole launch to hide
+// in), and run in REVERSE transform order: the first emit blocks read the
+// coefficients K1 wrote last, which may still be in the Infinity Cache.
+// Measured: 1024 x 64^3 emit 0.346 -> 0.327 ms.
 void build_etiles(Plan& P, int n) {
-    P.etiles.clear();
-    P.segs.clear();
-    auto tiles_of = [](const UnitDev& d) {
-        return (uint32_t)std::max<uint64_t>(1, (d.ncells + kEmitTile - 1) / kEmitTile);
-    };
-    int eligible = 0;
-    if (P.seg_max > 0 && !P.pipe && P.chunk_req == 0)
-        for (int i = 0; i < n; ++i) eligible += tiles_of(P.units[i]) <= (uint32_t)P.seg_max;
-    const bool seg = eligible > 0 && eligible >= P.seg_min;
+    uint32_t total = 0;
     for (int i = 0; i < n; ++i) {
         UnitDev& d = P.units[i];
-        d.et_begin = (uint32_t)P.etiles.size();
-        d.net = tiles_of(d);
-        if (seg && d.net <= (uint32_t)P.seg_max) {
-            d.net = 0;
-            P.segs.push_back((uint32_t)i);
-            continue;
-        }
-        for (uint32_t t = 0; t < d.net; ++t) P.etiles.push_back(FTile{(uint32_t)i, t});
+        d.et_begin = total;
+        d.net = (uint32_t)std::max<uint64_t>(1, (d.ncells + kEmitTile - 1) / kEmitTile);
+        total += d.net;
     }
-    P.state_bytes = round_up(16 + 16ull * n + 8ull * P.etiles.size(), 16);
-    // Dispatch order of the look-back blocks: interleaved by tile index across
-    // the units of a group, so the ticket atomics of one unit are spread over
-    // the group instead of arriving in one burst.  Groups hold >= 8192 tiles
-    // (256 MB of fp32 coefficients, the Infinity Cache's size) and >= 128 x the
-    // longest unit's tile chain (a look-back chain advances one tile per
-    // status round trip, so long chains need the whole launch to hide in), and
-    // run in REVERSE transform order: the first emit blocks read the
-    // coefficients K1 wrote last, which may still be in the Infinity Cache.
-    // Measured: 1024 x 64^3 emit 0.346 -> 0.327 ms; batches of
-    // 128^3 units (256-tile chains) stay one group up to 128 units.
+    P.netiles = total;
+    P.state_bytes = round_up(16 + 12ull * n, 8) + 8ull * total;
     P.eunits.clear();
     P.eidx.clear();
     uint32_t maxt = 0;
     for (int i = 0; i < n; ++i) maxt = std::max(maxt, P.units[i].net);
-#ifndef WC_EMIT_GROUP_TILES
-#define WC_EMIT_GROUP_TILES 8192  // tools/sweeps/emit_variants.sh
-#endif
-    const uint64_t group_tiles = std::max<uint64_t>(WC_EMIT_GROUP_TILES, 128ull * maxt);
+    const uint64_t group_tiles = std::max<uint64_t>(8192, 128ull * maxt);
     std::vector<std::pair<int, int>> groups;  // unit ranges [i0, i1)
     for (int i0 = 0; i0 < n;) {
         uint64_t tiles = 0;
@@ -317,160 +260,20 @@ void build_etiles(Plan& P, int n) {
     }
 }
 
-void build_pipe(Plan& P, int n) {
-    P.items.clear();
-    P.waits.clear();
-    uint64_t maxa = kRingChunk, total = 0;
-    for (int i = 0; i < n; ++i) {
-        const UnitDev& d = P.units[i];
-        const uint64_t a = round_up(d.ncells, kRingChunk);
-        maxa = std::max(maxa, a);
-        total += a;
-    }
-    const int64_t lag = P.lag > 0 ? P.lag : kDefaultLag;
-    uint64_t R = P.ring_req > 0 ? round_up((uint64_t)P.ring_req, kRingChunk)
-                                : round_up((uint64_t)lag + kDefaultRingExtra + 2 * maxa, kRingChunk);
-    R = std::max(R, 2 * maxa);
-    R = std::min(R, std::max<uint64_t>(total, kRingChunk));  // no reuse needed: no waits
-    R = std::max(R, maxa);
-    P.ring_floats = R;
-    // Ring regions, chunk aligned; a chunk has one writer per lap, so each
-    // unit waits for the last writers of its chunks (earlier laps follow by
-    // transitivity: that writer's transform waited for them).
-    std::vector<int32_t> last(R / kRingChunk, -1);
-    uint64_t cur = 0;
-    for (int i = 0; i < n; ++i) {
-        UnitDev& d = P.units[i];
-        d.wl_off = (uint32_t)P.waits.size();
-        d.wl_len = 0;
-        d.ring_off = 0;
-        if (d.ncells == 0) continue;
-        const uint64_t a = round_up(d.ncells, kRingChunk);
-        if (cur + a > R) cur = 0;
-        d.ring_off = cur;
-        std::vector<uint32_t> w;
-        for (uint64_t ch = cur / kRingChunk; ch < (cur + a) / kRingChunk; ++ch) {
-            if (last[ch] >= 0 && last[ch] != i) w.push_back((uint32_t)last[ch]);
-            last[ch] = i;
-        }
-        std::sort(w.begin(), w.end());
-        w.erase(std::unique(w.begin(), w.end()), w.end());
-        P.waits.insert(P.waits.end(), w.begin(), w.end());
-        d.wl_len = (uint32_t)w.size();
-        cur += a;
-    }
-    // Work list: transform tiles in unit order; a unit's emit work once `lag`
-    // more cells of transform work have been listed after its last transform
-    // tile, as ONE whole-unit item (no look-back); units whose emit work
-    // comes after the last transform tile (the drain) are split into emit
-    // tiles with look-back instead, so the tail runs wide.  All emit work of
-    // the units a transform waits for comes before it.  Every wait is
-    // therefore on an earlier item.
-    std::vector<int64_t> tend(n);
-    int eu = 0;  // next unit whose emit work is not listed yet
-    int64_t tc = 0;
-    bool t_left = true;
-    auto emit_unit = [&](int v) {
-        UnitDev& d = P.units[v];
-        d.ewant = 1;
-        P.items.push_back(0xC0000000u | (uint32_t)v);
-        (void)t_left;
-    };
-    auto emit_until = [&](int target) {
-        for (; eu < target; ++eu) emit_unit(eu);
-    };
-    auto emit_eligible = [&](int upto_unit) {
-        while (eu <= upto_unit && tend[eu] + lag <= tc) emit_unit(eu++);
-    };
-    int last_t = -1;
-    for (int u = 0; u < n; ++u)
-        if (P.units[u].ntx) last_t = u;
-    for (int u = 0; u < n; ++u) {
-        const UnitDev& d = P.units[u];
-        for (uint32_t k = 0; k < d.wl_len; ++k) emit_until(std::max(eu, (int)P.waits[d.wl_off + k] + 1));
-        const int64_t tcells = (int64_t)8 << (d.lbx + d.lby + d.lbz);
-        for (uint32_t g = 0; g < d.ntx; ++g) {
-            P.items.push_back(d.xt_begin + g);
-            tc += tcells;
-            if (g + 1 == d.ntx) tend[u] = tc;
-            if (u == last_t && g + 1 == d.ntx) t_left = false;
-            emit_eligible(u - 1);
-        }
-        if (d.ntx == 0) tend[u] = tc;
-        emit_eligible(u);
-    }
-    t_left = false;
-    emit_until(n);
-}
-
-// Chunked forward: consecutive units grouped until their coefficients reach
-// chunk_req floats (a larger unit is a chunk of its own); chunk c's
-// coefficients live in slot c % nslots (ring_off), so a slot is rewritten
-// only after the emit launch that read it has finished.
-void build_chunks(Plan& P, int n) {
-    uint32_t gcur = 0, fcur = P.ngen;
-    uint64_t slot = 0;
-    int u = 0;
-    while (u < n) {
-        Plan::Chunk ch{};
-        ch.u0 = (uint32_t)u;
-        ch.gen_b = gcur;
-        ch.fast_b = fcur;
-        ch.et_b = P.units[u].et_begin;
-        uint64_t fl = 0;
-        do {
-            UnitDev& d = P.units[u];
-            d.ring_off = fl;  // relative to the slot for now
-            fl = round_up(fl + d.ncells, 4);
-            if (d.fast)
-                fcur += d.ntx;
-            else
-                gcur += d.ntx;
-            ch.et_n += d.net;
-            ++u;
-        } while (u < n && fl + P.units[u].ncells <= (uint64_t)P.chunk_req);
-        ch.u1 = (uint32_t)u;
-        ch.seg_b = (uint32_t)(std::lower_bound(P.segs.begin(), P.segs.end(), ch.u0) - P.segs.begin());
-        ch.seg_n = (uint32_t)(std::lower_bound(P.segs.begin(), P.segs.end(), ch.u1) - P.segs.begin()) - ch.seg_b;
-        ch.gen_n = gcur - ch.gen_b;
-        ch.fast_n = fcur - ch.fast_b;
-        slot = std::max(slot, fl);
-        P.chunks.push_back(ch);
-    }
-    P.slot_floats = round_up(std::max<uint64_t>(slot, 4), 4);
-    for (size_t c = 0; c < P.chunks.size(); ++c)
-        for (uint32_t v = P.chunks[c].u0; v < P.chunks[c].u1; ++v)
-            P.units[v].ring_off += (c % P.nslots) * P.slot_floats;
-    P.ring_floats = P.slot_floats * P.nslots + kEmitTile;
-}
-
 // Build (or reuse) the plan for this batch and upload it.
 int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     Plan& P = c->plan;
-    if (c->plan_valid && P.pipe == c->opt_pipe && P.lag == c->opt_lag && P.ring_req == c->opt_ring &&
-        P.chunk_req == c->opt_chunk && P.nslots == (c->opt_chunk ? c->opt_slots : 0) &&
-        P.seg_max == c->opt_seg_max && P.seg_min == c->opt_seg_min &&
-        (int)P.key.size() == n && (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0))
+    if (c->plan_valid && (int)P.key.size() == n && (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0))
         return WC_OK;
     c->plan_valid = false;
     ++c->plan_gen;
     P.key.assign(units, units + n);
-    P.pipe = c->opt_pipe;
-    P.items.clear();
-    P.waits.clear();
-    P.lag = c->opt_lag;
-    P.ring_req = c->opt_ring;
-    P.chunk_req = c->opt_chunk;
-    P.nslots = c->opt_chunk ? c->opt_slots : 0;
-    P.seg_max = c->opt_seg_max;
-    P.seg_min = c->opt_seg_min;
-    P.chunks.clear();
     P.units.assign(n, UnitDev{});
     P.xtiles.clear();
     P.ftiles.clear();
     P.ngen = P.nfast = 0;
     P.any_sparse = false;
-    P.lds_gen = P.lds_fast = P.lds_inverse = P.lds_pipe = 0;
+    P.lds_gen = P.lds_fast = P.lds_inverse = 0;
     std::vector<XTile> gen, fast;
     uint64_t coef_cursor = 0, pay_cursor = 4;
     for (int i = 0; i < n; ++i) {
@@ -542,20 +345,11 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     }
     P.coef_extent = coef_cursor ? coef_cursor + kFlatTile : 0;  // slack: flat tiles read whole float4 groups
     build_etiles(P, n);
-    if (!P.pipe && P.chunk_req > 0) build_chunks(P, n);
-    if (P.pipe) {
-        build_pipe(P, n);
-        P.lds_pipe = pipe_lds_bytes(std::max(P.lds_gen, P.lds_fast));
-    }
     int rc;
     if ((rc = upload(c, P.d_units, P.units.data(), sizeof(UnitDev) * P.units.size(), "upload units")) ||
         (rc = upload(c, P.d_xtiles, P.xtiles.data(), sizeof(XTile) * P.xtiles.size(), "upload xtiles")) ||
         (rc = upload(c, P.d_ixtiles, P.ixtiles.data(), sizeof(XTile) * P.ixtiles.size(), "upload ixtiles")) ||
         (rc = upload(c, P.d_ftiles, P.ftiles.data(), sizeof(FTile) * P.ftiles.size(), "upload ftiles")) ||
-        (rc = upload(c, P.d_etiles, P.etiles.data(), sizeof(FTile) * P.etiles.size(), "upload etiles")) ||
-        (rc = upload(c, P.d_items, P.items.data(), sizeof(uint32_t) * P.items.size(), "upload items")) ||
-        (rc = upload(c, P.d_waits, P.waits.data(), sizeof(uint32_t) * P.waits.size(), "upload waits")) ||
-        (rc = upload(c, P.d_segs, P.segs.data(), sizeof(uint32_t) * P.segs.size(), "upload segs")) ||
         (rc = upload(c, P.d_dtiles, P.dtiles.data(), sizeof(FTile) * P.dtiles.size(), "upload dtiles")) ||
         (rc = upload(c, P.d_eunits, P.eunits.data(), sizeof(uint32_t) * P.eunits.size(), "upload eunits")) ||
         (rc = upload(c, P.d_eidx, P.eidx.data(), sizeof(uint32_t) * P.eidx.size(), "upload eidx")))
@@ -577,18 +371,8 @@ int ensure_scratch(wc_ctx* c) {
     int rc;
     if ((rc = ensure(c, c->coef, sizeof(float) * std::max<uint64_t>(P.coef_extent, 1))) ||
         (rc = ensure(c, c->flags, (P.coef_extent >> kSegShift) + kEmitTile)) ||
-        (rc = ensure(c, c->part, sizeof(double) * nft)) || (rc = ensure(c, c->errflag, 16)) ||
+        (rc = ensure(c, c->part, sizeof(double) * nft)) ||
         (rc = ensure(c, c->state, std::max<size_t>(P.state_bytes, decode_state_bytes(P)))))
-        return rc;
-    return WC_OK;
-}
-
-// Scratch of the pipelined forward.
-int ensure_pipe_scratch(wc_ctx* c) {
-    const Plan& P = c->plan;
-    int rc;
-    if ((rc = ensure(c, c->ring, sizeof(float) * P.ring_floats)) || (rc = ensure(c, c->state, P.state_bytes)) ||
-        (rc = ensure(c, c->errflag, 16)))
         return rc;
     return WC_OK;
 }
@@ -600,17 +384,16 @@ int set_device(wc_ctx* c) {
 }
 
 // Surface an error bit a kernel raised (malformed payload in the decode, a
-// dependency wait that timed out) at the next synchronisation point.  The
-// reference exits on a malformed payload (src/decompressor.cpp:228-231);
-// here it is WC_ERR_FORMAT.
+// look-back wait that timed out) at the next synchronisation point, and clear
+// the word.  The reference exits on a malformed payload
+// (src/decompressor.cpp:228-231); here it is WC_ERR_FORMAT.
 int check_kernel_errors(wc_ctx* c) {
     if (!c->err_check_pending) return WC_OK;
     c->err_check_pending = false;
     uint32_t flag = 0;
-    const void* src = c->err_src ? (const void*)c->err_src : c->errflag.p;
-    c->err_src = nullptr;
-    hipError_t e = hipMemcpyAsync(&flag, src, 4, hipMemcpyDeviceToHost, c->stream);
+    hipError_t e = hipMemcpyAsync(&flag, c->errflag.p, 4, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess && flag) e = hipMemsetAsync(c->errflag.p, 0, 4, c->stream);
     if (e != hipSuccess) return hip_fail(c, e, "error flag readback");
     if (flag & (kErrHeader | kErrNegativeRun)) {
         char buf[128];
@@ -618,67 +401,6 @@ int check_kernel_errors(wc_ctx* c) {
         return fail(c, WC_ERR_FORMAT, buf);
     }
     if (flag & kErrTimeout) return fail(c, WC_ERR_HIP, "a dependency wait between workgroups timed out");
-    return WC_OK;
-}
-
-// Parameter block shared by k_forward_pipe and k_emit_lb; the per-call state
-// block [ticket | key[n] | tdone[n] | edone[n] | status[netiles]] is zeroed
-// by one memset.
-PipeParams pipe_params(wc_ctx* c, const void* d_cells, int n, double keep, uint8_t* d_payload,
-                       uint64_t* d_offsets, uint32_t* d_kept) {
-    Plan& P = c->plan;
-    uint8_t* st = (uint8_t*)c->state.p;
-    PipeParams p{};
-    p.cells = d_cells;
-    p.units = (const UnitDev*)P.d_units.p;
-    p.xtiles = (const XTile*)P.d_xtiles.p;
-    p.etiles = (const FTile*)P.d_etiles.p;
-    p.items = (const uint32_t*)P.d_items.p;
-    p.waits = (const uint32_t*)P.d_waits.p;
-    p.ring = (float*)c->ring.p;
-    p.ring_bytes = (uint32_t)(sizeof(float) * P.ring_floats);
-    p.nitems = (uint32_t)P.items.size();
-    p.n = n;
-    p.ticket = (uint32_t*)st;
-    p.key = (unsigned long long*)(st + 16);
-    p.tdone = (uint32_t*)(st + 16 + 8ull * n);
-    p.edone = (uint32_t*)(st + 16 + 12ull * n);
-    p.status = (unsigned long long*)(st + 16 + 16ull * n);
-    p.payload = d_payload;
-    p.offsets = d_offsets;
-    p.kept = d_kept;
-    p.err = (uint32_t*)c->errflag.p;
-    p.keep = keep;
-    p.claim = 1;
-    p.segs = (const uint32_t*)P.d_segs.p;
-    return p;
-}
-
-int forward_pipe(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
-                 uint64_t* d_offsets, uint32_t* d_kept) {
-    Plan& P = c->plan;
-    hipError_t e;
-    if ((e = hipMemsetAsync(c->state.p, 0, P.state_bytes, c->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(c->errflag.p, 0, 4, c->stream)) != hipSuccess)
-        return hip_fail(c, e, "memset pipe state");
-    PipeParams p = pipe_params(c, d_cells, n, keep, d_payload, d_offsets, d_kept);
-    p.claim = c->opt_claim;
-    p.prefetch = c->opt_prefetch ? 1u : 0u;
-    p.stats = nullptr;
-    if (c->opt_stats) {
-        int rc = ensure(c, c->stats, sizeof(unsigned long long) * kPipeStats);
-        if (rc) return rc;
-        p.stats = (unsigned long long*)c->stats.p;
-    }
-    const uint32_t nbatch = (p.nitems + p.claim - 1) / p.claim;
-    const uint32_t grid = std::min<uint32_t>(pipe_grid(dtype, P.lds_pipe, c->opt_wgs), nbatch);
-    {
-        StageTimer t(c, WC_STAGE_PIPE);
-        e = launch_forward_pipe(c->stream, dtype, P.lds_pipe, grid, p);
-    }
-    if (e != hipSuccess) return hip_fail(c, e, "pipe launch");
-    c->err_check_pending = true;
-    c->err_src = nullptr;
     return WC_OK;
 }
 
@@ -710,25 +432,33 @@ int stage_transform(wc_ctx* c, const void* d_cells, int dtype, double keep, bool
 }
 
 // Second half: K2 threshold + ordered pack of the staged coefficients
-// (gthresh: the global-threshold mode's fp32 threshold, or null).
+// (gthresh: the global-threshold mode's fp32 threshold, or null).  Uses the
+// unit keys and the zeroed tickets / look-back granules of the per-call state.
 int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_payload, uint64_t* d_offsets,
                uint32_t* d_kept) {
     Plan& P = c->plan;
-    PipeParams p = pipe_params(c, nullptr, n, keep, d_payload, d_offsets, d_kept);
+    uint8_t* st = (uint8_t*)c->state.p;
+    EmitParams p{};
+    p.units = (const UnitDev*)P.d_units.p;
+    p.eunits = (const uint32_t*)P.d_eunits.p;
+    p.eidx = (const uint32_t*)P.d_eidx.p;
+    p.n = n;
+    p.ordered = c->opt_ordered ? 1u : 0u;
+    p.key = (const unsigned long long*)(st + 16);
+    p.tickets = (uint32_t*)(st + 16 + 8ull * n);
+    p.status = (unsigned long long*)(st + round_up(16 + 12ull * n, 8));
+    p.payload = d_payload;
+    p.offsets = d_offsets;
+    p.kept = d_kept;
+    p.err = (uint32_t*)c->errflag.p;
+    p.keep = keep;
     if (gthresh) {
         p.use_gthresh = 1;
         p.gthresh = *gthresh;
     }
-    p.eunits = (const uint32_t*)P.d_eunits.p;
-    p.eidx = (const uint32_t*)P.d_eidx.p;
-    // error word inside the per-call state header (zeroed with it; the staged
-    // path does not use the pipe's ticket word next to it): no extra memset
-    p.err = (uint32_t*)((uint8_t*)c->state.p + 4);
-    c->err_src = p.err;
     p.flags = (c->sparse_staged && !gthresh) ? (const uint8_t*)c->flags.p : nullptr;
     StageTimer t(c, WC_STAGE_EMIT);
-    hipError_t e = launch_emit(c->stream, p, (const float*)c->coef.p, (uint32_t)P.segs.size(),
-                               (uint32_t)P.etiles.size());
+    hipError_t e = launch_emit(c->stream, p, (const float*)c->coef.p, P.netiles);
     if (e != hipSuccess) return hip_fail(c, e, "emit launch");
     c->err_check_pending = true;  // a look-back wait that timed out surfaces at wc_synchronize
     return WC_OK;
@@ -740,29 +470,6 @@ int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep
     return rc ? rc : stage_emit(c, n, keep, nullptr, d_payload, d_offsets, d_kept);
 }
 
-// Chunked forward: launch k transforms chunk k into slot k % nslots and packs
-// chunk k - 1 (wc_pipe.hip k_chunk), all on the context stream.
-int forward_chunked(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
-                    uint64_t* d_offsets, uint32_t* d_kept) {
-    Plan& P = c->plan;
-    hipError_t e;
-    StageTimer timer(c, WC_STAGE_CHUNKED);
-    if ((e = hipMemsetAsync(c->state.p, 0, P.state_bytes, c->stream)) != hipSuccess)
-        return hip_fail(c, e, "memset state");
-    PipeParams p = pipe_params(c, d_cells, n, keep, d_payload, d_offsets, d_kept);
-    p.ring_coefs = 1;
-    const size_t lds = chunk_lds_bytes(std::max(P.lds_gen, P.lds_fast));
-    const size_t nch = P.chunks.size();
-    for (size_t k = 0; k <= nch; ++k) {
-        const Plan::Chunk* t = k < nch ? &P.chunks[k] : nullptr;
-        const Plan::Chunk* m = k > 0 ? &P.chunks[k - 1] : nullptr;
-        e = launch_chunk(c->stream, dtype, lds, p, t ? t->gen_b : 0, t ? t->gen_n : 0, t ? t->fast_b : 0,
-                         t ? t->fast_n : 0, m ? m->et_b : 0, m ? m->et_n : 0);
-        if (e != hipSuccess) return hip_fail(c, e, "chunk launch");
-    }
-    return WC_OK;
-}
-
 uint64_t cells_extent(const wc_unit* units, int n) {
     uint64_t ext = 0;
     for (int i = 0; i < n; ++i)
@@ -770,9 +477,6 @@ uint64_t cells_extent(const wc_unit* units, int n) {
     return ext;
 }
 
-// Transform-only, inverse and RMSE calls use the plan's tiles and flat
-// scratch, which every plan has (the pipe's work list is only extra).
-int get_plan_staged(wc_ctx* c, const wc_unit* units, int n) { return get_plan(c, units, n); }
 
 }  // namespace
 
@@ -802,6 +506,11 @@ int wc_ctx_create(int device, wc_ctx** out) {
         return WC_ERR_HIP;
     }
     c->stream = c->own;
+    // the persistent error word (check_kernel_errors reads and clears it)
+    if (ensure(c, c->errflag, 16) != WC_OK || hipMemset(c->errflag.p, 0, 16) != hipSuccess) {
+        wc_ctx_destroy(c);
+        return WC_ERR_NOMEM;
+    }
     *out = c;
     return WC_OK;
 }
@@ -810,11 +519,11 @@ void wc_ctx_destroy(wc_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->coef,      &c->part,       &c->errflag,
-                      &c->ring,      &c->state,     &c->stats,      &c->h_cells,    &c->h_payload,
-                      &c->h_packed,  &c->h_offsets, &c->h_poff,    &c->h_kept,     &c->h_out,
-                      &c->plan.d_units, &c->plan.d_xtiles, &c->plan.d_ftiles, &c->plan.d_etiles,
-                      &c->plan.d_items, &c->plan.d_waits, &c->plan.d_segs, &c->plan.d_dtiles, &c->plan.d_eunits, &c->plan.d_ixtiles, &c->plan.d_eidx};
+    DevBuf* bufs[] = {&c->coef,          &c->part,           &c->errflag,        &c->state,
+                      &c->flags,         &c->h_cells,        &c->h_payload,      &c->h_packed,
+                      &c->h_offsets,     &c->h_poff,         &c->h_kept,         &c->h_out,
+                      &c->plan.d_units,  &c->plan.d_xtiles,  &c->plan.d_ftiles,  &c->plan.d_dtiles,
+                      &c->plan.d_eunits, &c->plan.d_ixtiles, &c->plan.d_eidx};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& m : c->marks) {
@@ -837,55 +546,11 @@ int wc_set_stream(wc_ctx* c, void* s) {
 int wc_set_option(wc_ctx* c, int option, int64_t value) {
     if (!c) return WC_ERR_INVALID;
     switch (option) {
-        case WC_OPT_PIPE:
-            c->opt_pipe = value != 0;
-            return WC_OK;
-        case WC_OPT_PIPE_LAG:
-            if (value < 0) return fail(c, WC_ERR_INVALID, "lag < 0");
-            c->opt_lag = value;
-            return WC_OK;
-        case WC_OPT_PIPE_RING:
-            if (value < 0 || value > (int64_t(1) << 28)) return fail(c, WC_ERR_INVALID, "ring floats out of range");
-            c->opt_ring = value;
-            return WC_OK;
-        case WC_OPT_PIPE_CLAIM:
-            if (value < 1 || value > 64) return fail(c, WC_ERR_INVALID, "claim must be 1..64");
-            c->opt_claim = (uint32_t)value;
-            return WC_OK;
-        case WC_OPT_PIPE_PREFETCH:
-            c->opt_prefetch = value != 0;
-            return WC_OK;
-        case WC_OPT_PIPE_WGS:
-            if (value < 0 || value > 64) return fail(c, WC_ERR_INVALID, "workgroups per CU must be 0..64");
-            c->opt_wgs = (int)value;
-            return WC_OK;
-        case WC_OPT_CHUNK:
-            if (value < 0) return fail(c, WC_ERR_INVALID, "chunk cells < 0");
-            c->opt_chunk = value;
-            return WC_OK;
-        case WC_OPT_CHUNK_SLOTS:
-            if (value < 2 || value > 16) return fail(c, WC_ERR_INVALID, "chunk slots must be 2..16");
-            c->opt_slots = (int)value;
-            return WC_OK;
-        case WC_OPT_EMIT_SEG_MAX:
-            if (value < 0 || value > 65536) return fail(c, WC_ERR_INVALID, "seg max tiles must be 0..65536");
-            c->opt_seg_max = (int)value;
-            return WC_OK;
         case WC_OPT_SPARSE:
             c->opt_sparse = value != 0;
             return WC_OK;
-        case WC_OPT_EMIT_SEG_MIN_UNITS:
-            if (value < 1 || value > (int64_t(1) << 30)) return fail(c, WC_ERR_INVALID, "seg min units must be >= 1");
-            c->opt_seg_min = (int)value;
-            return WC_OK;
-        case WC_OPT_PIPE_STATS:
-            c->opt_stats = value != 0;
-            if (c->opt_stats) {
-                int rc = ensure(c, c->stats, sizeof(unsigned long long) * kPipeStats);
-                if (rc) return rc;
-                hipError_t e = hipMemset(c->stats.p, 0, sizeof(unsigned long long) * kPipeStats);
-                if (e != hipSuccess) return hip_fail(c, e, "memset stats");
-            }
+        case WC_OPT_ORDERED:
+            c->opt_ordered = value != 0;
             return WC_OK;
         default:
             return fail(c, WC_ERR_INVALID, "unknown option");
@@ -921,14 +586,6 @@ int wc_forward(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, 
     if (!d_cells || !d_payload || !d_offsets || !d_kept) return fail(c, WC_ERR_INVALID, "null buffer");
     if (cap < wc_payload_bound(units, n)) return fail(c, WC_ERR_INVALID, "payload_capacity < wc_payload_bound");
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
-    if (c->plan.pipe) {
-        if ((rc = ensure_pipe_scratch(c))) return rc;
-        return forward_pipe(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
-    }
-    if (!c->plan.chunks.empty()) {
-        if ((rc = ensure_scratch(c)) || (rc = ensure_pipe_scratch(c))) return rc;
-        return forward_chunked(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
-    }
     if ((rc = ensure_scratch(c))) return rc;
     return forward_staged(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
 }
@@ -941,8 +598,6 @@ int wc_forward_stage(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* u
     if (n == 0) return WC_OK;
     if (!d_cells) return fail(c, WC_ERR_INVALID, "null buffer");
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
-    if (c->plan.pipe || !c->plan.chunks.empty())
-        return fail(c, WC_ERR_INVALID, "wc_forward_stage needs the staged forward (WC_OPT_PIPE / WC_OPT_CHUNK off)");
     // dense staging: the histogram and any later threshold need every coefficient
     if ((rc = ensure_scratch(c)) || (rc = stage_transform(c, d_cells, dtype, 0.0, false))) return rc;
     if (d_hist) {
@@ -1001,7 +656,7 @@ int wc_forward_emit(wc_ctx* c, const wc_unit* units, int n, double keep, const f
     const uint64_t gen = c->plan_gen;
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
     // get_plan keeps the cached plan (and so the staged scratch) only for the same units
-    if (!staged || gen != c->plan_gen || c->plan.pipe || !c->plan.chunks.empty())
+    if (!staged || gen != c->plan_gen)
         return fail(c, WC_ERR_INVALID, "wc_forward_emit: no staged coefficients for these units (wc_forward_stage)");
     // per-unit tile tickets (tdone) and look-back status words are per call:
     // zero everything after the unit keys
@@ -1021,7 +676,7 @@ int wc_decompose(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units
     if (dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
     if (n == 0) return WC_OK;
     if (!d_cells || !d_flat) return fail(c, WC_ERR_INVALID, "null buffer");
-    if ((rc = set_device(c)) || (rc = get_plan_staged(c, units, n))) return rc;
+    if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
     Plan& P = c->plan;
     const UnitDev* du = (const UnitDev*)P.d_units.p;
     const XTile* dxt = (const XTile*)P.d_xtiles.p;
@@ -1040,21 +695,20 @@ int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, c
     if ((rc = validate_units(c, units, n))) return rc;
     if (n == 0) return WC_OK;
     if (!d_payload || !d_offsets || !d_out) return fail(c, WC_ERR_INVALID, "null buffer");
-    if ((rc = set_device(c)) || (rc = get_plan_staged(c, units, n)) || (rc = ensure_scratch(c))) return rc;
+    if ((rc = set_device(c)) || (rc = get_plan(c, units, n)) || (rc = ensure_scratch(c))) return rc;
     Plan& P = c->plan;
     hipError_t e;
     // per-call decode state: ticket[n] | status[flat tiles]; the dense
     // coefficient scratch itself is fully written by the decode (no memset)
     uint8_t* st = (uint8_t*)c->state.p;
-    if ((e = hipMemsetAsync(st, 0, decode_state_bytes(P), c->stream)) != hipSuccess ||
-        (e = hipMemsetAsync(c->errflag.p, 0, 4, c->stream)) != hipSuccess)
+    if ((e = hipMemsetAsync(st, 0, decode_state_bytes(P), c->stream)) != hipSuccess)
         return hip_fail(c, e, "memset");
     {
         StageTimer t(c, WC_STAGE_DECODE);
         e = launch_decode(c->stream, (const UnitDev*)P.d_units.p, (const FTile*)P.d_dtiles.p,
                           (uint32_t)P.dtiles.size(), d_payload, d_offsets, (uint32_t*)st,
                           (unsigned long long*)(st + round_up(4ull * n, 8)), (float*)c->coef.p,
-                          (uint32_t*)c->errflag.p);
+                          (uint32_t*)c->errflag.p, c->opt_ordered ? 1 : 0);
     }
     if (e != hipSuccess) return hip_fail(c, e, "decode launch");
     {
@@ -1065,7 +719,6 @@ int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, c
     if (e != hipSuccess) return hip_fail(c, e, "inverse launch");
     // Malformed payloads surface at the next wc_synchronize (WC_ERR_FORMAT).
     c->err_check_pending = true;
-    c->err_src = nullptr;
     return WC_OK;
 }
 
@@ -1097,19 +750,6 @@ int wc_rmse(wc_ctx* c, const void* d_orig, int dtype, const float* d_regen, cons
     hipError_t e = launch_rmse(c->stream, d_orig, dtype, d_regen, (const UnitDev*)P.d_units.p, n,
                                (const FTile*)P.d_ftiles.p, (uint32_t)P.ftiles.size(), (double*)c->part.p, d_rmse);
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "rmse launch");
-}
-
-int wc_pipe_stats(wc_ctx* c, uint64_t* out, int n) {
-    if (!c || n < 0 || (n > 0 && !out)) return WC_ERR_INVALID;
-    if (!c->opt_stats || !c->stats.p) return fail(c, WC_ERR_INVALID, "WC_OPT_PIPE_STATS is off");
-    unsigned long long h[kPipeStats] = {};
-    hipError_t e;
-    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess ||
-        (e = hipMemcpy(h, c->stats.p, sizeof h, hipMemcpyDeviceToHost)) != hipSuccess ||
-        (e = hipMemset(c->stats.p, 0, sizeof h)) != hipSuccess)
-        return hip_fail(c, e, "pipe stats readback");
-    for (int i = 0; i < n && i < kPipeStats; ++i) out[i] = h[i];
-    return WC_OK;
 }
 
 int wc_profile_enable(wc_ctx* c, int on) {

@@ -1,7 +1,7 @@
 // wc_compact.hip — host-path packing of the forward payload: the slots of
 // wc_forward (fixed worst-case offsets) are packed densely before the copy
-// back (wc_forward_host).  The forward compaction itself is k_emit_lb /
-// k_forward_pipe (wc_pipe.hip).
+// back (wc_forward_host).  The forward compaction itself is k_emit
+// (wc_emit.hip).
 #include "wc_device.h"
 
 namespace wc {

@@ -1,0 +1,269 @@
+// wc_emit.hip — K2: keep threshold + ordered pack of the staged coefficients.
+//
+//   src/compressor.cpp:212-216  signed max, thresh  -> unit key (K1's 64-bit atomicMax) -> fp32 threshold
+//   src/compressor.cpp:222-238  mask + rle_encode   -> emit tiles with decoupled look-back
+//   src/compressor.cpp:55-80    serialize           -> header + pairs written in the unit's slot
+//
+// An emit tile is kEmitTile consecutive flat coefficients of one unit (flat
+// order, x slowest / z fastest, src/compressor.cpp:178-181).  Per tile: load
+// the staged coefficients (only the flagged segments under sparse staging),
+// keep bits |c| > tf, publish (kept count, last kept index + 1) in the tile's
+// 8-B look-back granule, sum the unit's earlier tiles' granules for the pair
+// offset and the previous kept index, and write the (run, value) pairs
+// contiguously (staged per wave in LDS).  The unit's last tile writes the
+// header.
+//
+// Tile index within the unit, two runtime forms (wc_set_option WC_OPT_ORDERED):
+//   1 (default): from the launch order.  Blocks are listed so that a tile's
+//      look-back waits only on tiles of its unit with LOWER block ids; with
+//      in-order dispatch (DESIGN.md §Forward progress) every wait is on a block
+//      that is running or done.  No atomic per block.
+//   0: from a per-unit ticket (atomicAdd): a tile's predecessors have always
+//      started whatever the dispatch order.  One atomic round trip per block.
+// Every spin is bounded (spin_fail) and raises kErrTimeout, never a hang.
+#include "wc_xform.h"
+
+namespace wc {
+
+namespace {
+
+// fp32 keep threshold of a unit: the reference rule from the unit's max key
+// (src/compressor.cpp:212-216), or the one global threshold of the opt-in
+// histogram mode (wc_forward_emit with a threshold).
+__device__ __forceinline__ float unit_thresh(const EmitParams& P, unsigned long long key) {
+    return P.use_gthresh ? P.gthresh : thresh_as_float(key_thresh(key, P.keep));
+}
+
+// Set bits of a 64-lane mask below this lane.
+__device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Emit the kept coefficients of one kEmitTile chunk held in q (thread (w, l)
+// owns elements w*2048 + it*256 + 4l + j; kb bit it*4 + j = kept) as (run,
+// value) pairs: ranks from per-column ballots, run = f - prev - 1.  rank /
+// prev: this wave's first pair index and the unit-relative flat index of the
+// last kept coefficient before this wave's elements (0xffffffff = none, so
+// that run = f).  32-bit arithmetic: flat indices are < 2^31.
+// The pairs of each 256-element block are first placed in this wave's
+// 256-entry LDS stage in rank order, then copied out with contiguous 8-B
+// stores (one full 512-B row per instruction instead of up to four sparse,
+// partial-line scatters).  A wave's LDS operations execute in order, so the
+// stage needs no barrier.
+__device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, uint32_t start, int w, int l,
+                                           uint32_t rank, uint32_t prev, uint2* __restrict__ pairs, uint2* stage) {
+    const unsigned long long lt = (1ull << l) - 1ull;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const uint32_t nib = (kb >> (it * 4)) & 0xfu;
+        const unsigned long long any = __ballot(nib != 0);
+        if (!any) continue;
+        // exclusive prefix of kept counts over lanes: one ballot per column j,
+        // counted below this lane with mbcnt (ballots live in SGPRs)
+        const unsigned long long b0 = __ballot(nib & 1u), b1 = __ballot(nib & 2u), b2 = __ballot(nib & 4u),
+                                 b3 = __ballot(nib & 8u);
+        const uint32_t pre = mbcnt64(b0) + mbcnt64(b1) + mbcnt64(b2) + mbcnt64(b3);
+        const uint32_t itot = (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+        const uint32_t ebase = start + (uint32_t)(w * 2048 + it * 256 + l * 4);
+        const uint32_t lane_last = ebase + (nib ? 31u - (uint32_t)__clz(nib) : 0u);
+        const unsigned long long below = any & lt;
+        const uint32_t from_lane = __shfl(lane_last, below ? 63 - __clzll(below) : l);
+        uint32_t p = below ? from_lane : prev;
+        uint32_t r = pre;
+        if (nib) {
+            const float vv[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (nib & (1u << j)) {
+                    const uint32_t f = ebase + (uint32_t)j;
+                    stage[r] = make_uint2(f - p - 1u, __float_as_uint(vv[j]));
+                    p = f;
+                    ++r;
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t k = (uint32_t)l; k < itot; k += 64) pairs[rank + k] = stage[k];
+        __builtin_amdgcn_wave_barrier();
+        rank += itot;
+        prev = __shfl(lane_last, 63 - __clzll(any));
+    }
+}
+
+// Keep bits of a chunk: bit it*4 + j of element w*2048 + it*256 + 4l + j,
+// |c| > tf for elements below len (src/compressor.cpp:225-226).
+__device__ __forceinline__ uint32_t keep_bits(const float4 (&q)[8], float tf, uint32_t len, int w, int l) {
+    uint32_t kb = 0;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const float e[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t idx = (uint32_t)(w * 2048 + it * 256 + l * 4 + j);
+            kb |= (uint32_t)(idx < len && fabsf(e[j]) > tf) << (it * 4 + j);
+        }
+    }
+    return kb;
+}
+
+// Per-wave kept count and last kept (chunk-relative index + 1, 0 = none).
+__device__ __forceinline__ void wave_totals(uint32_t kb, int w, int l, uint32_t& cnt, uint32_t& last) {
+    cnt = wave_sum((uint32_t)__popc(kb));
+    const int hb = kb ? 31 - __clz(kb) : 0;
+    last = wave_max_u32(kb ? (uint32_t)(w * 2048 + (hb >> 2) * 256 + l * 4 + (hb & 3) + 1) : 0u);
+}
+
+// Unit u's header (src/compressor.cpp:55-80: int32 W, H, D, ncoeff, nrle),
+// kept count and payload offset, once its pair count is known.
+__device__ __forceinline__ void finish_unit(const EmitParams& P, const UnitDev& U, uint32_t u, uint32_t total) {
+    int32_t* hd = reinterpret_cast<int32_t*>(P.payload + U.pay_off);
+    hd[0] = U.nx;
+    hd[1] = U.ny;
+    hd[2] = U.nz;
+    hd[3] = (int32_t)U.ncells;
+    hd[4] = (int32_t)total;
+    P.kept[u] = total;
+    P.offsets[u] = U.pay_off;
+    if ((int)u == P.n - 1) P.offsets[P.n] = U.pay_off + 20 + 8ull * total;
+}
+
+constexpr unsigned long long kMask31 = 0x7fffffffull;
+
+// Threshold + ordered pack of tile `index` of unit `u`.  Thread t = (wave w,
+// lane l) owns elements w*2048 + it*256 + 4l + j, it 0..7.  sm: 16 LDS words.
+__device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __restrict__ coef, uint32_t u,
+                                          uint32_t index, uint32_t* sm, uint2* stage, int tid) {
+    const UnitDev& U = P.units[u];
+    const uint32_t et = U.et_begin + index;
+    const int w = tid >> 6, l = tid & 63;
+    // Sparse staging: this thread's 8 segment flags, loaded before the key.
+    const bool sparse = P.flags && U.sparse;
+    uint32_t segf = 0xffu;  // bit it: group it may hold kept coefficients
+    if (sparse) {
+        // one flag byte per segment of TZ = 2^lbz coefficients (16 or 32)
+        const uint8_t* fl = P.flags + (U.coef_off >> kSegShift) + (((uint64_t)index * kEmitTile) >> U.lbz);
+        const int sh = U.lbz;
+        segf = 0;
+#pragma unroll
+        for (int it = 0; it < 8; ++it) segf |= (uint32_t)(fl[(w * 2048 + it * 256 + 4 * l) >> sh] != 0) << it;
+    }
+    // the unit key: a finished earlier launch wrote it, one uniform load
+    const float tf = unit_thresh(P, P.key[u]);
+    const uint32_t start = index * (uint32_t)kEmitTile;
+    const uint32_t len = (uint32_t)min((uint64_t)kEmitTile, U.ncells - start);
+
+    // 1. coefficients -> keep bits (bit it*4 + j).  The flat scratch is 16-B
+    // aligned per unit with kFlatTile slack past the last unit.  Sparse units
+    // with thresh >= 0 skip unflagged segments (never stored); thresh < 0
+    // units were re-staged densely (k_transform_fallback).
+    const float4* __restrict__ p4 = reinterpret_cast<const float4*>(coef + U.coef_off + start);
+    if (!(tf >= 0.0f)) segf = 0xffu;
+    float4 q[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it)
+        q[it] = ((segf >> it) & 1u) && (uint32_t)(w * 2048 + it * 256 + 4 * l) < len ? p4[w * 512 + it * 64 + l]
+                                                                                      : make_float4(0, 0, 0, 0);
+    const uint32_t kb = keep_bits(q, tf, len, w, l);
+    uint32_t wcnt, wlast;
+    wave_totals(kb, w, l, wcnt, wlast);
+    if (l == 0) {
+        sm[4 + w] = wcnt;
+        sm[8 + w] = wlast;
+    }
+    __syncthreads();
+
+    // 2. publish the aggregate, look back over the unit's earlier tiles (wave 0)
+    if (w == 0) {
+        uint32_t C = 0, L = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            C += sm[4 + i];
+            L = sm[8 + i] > L ? sm[8 + i] : L;
+        }
+        const uint32_t L1 = L ? start + L : 0u;  // unit-relative last kept + 1
+        uint32_t ecnt = 0, elast = 0;            // exclusive: pairs before, last kept + 1 before
+        if (index == 0) {
+            if (l == 0) st_rlx(P.status + et, kFlagIncl | ((unsigned long long)C << 31) | L1);
+        } else {
+            if (l == 0) st_rlx(P.status + et, kFlagAgg | ((unsigned long long)C << 31) | L1);
+            int64_t pos = (int64_t)et - 1;
+            const int64_t first = U.et_begin;
+            // Window of the 64 nearest predecessors (lane l = tile et-1-l; tiles
+            // before the unit read as an inclusive 0).  Lanes up to the nearest
+            // inclusive one are summed once every one of them has published;
+            // a run of published aggregates before the first unpublished tile
+            // is summed and the window slides past it.
+            for (uint32_t spins = 0;;) {
+                const int64_t idx = pos - l;
+                const unsigned long long v = idx >= first ? ld_rlx(P.status + idx) : kFlagIncl;
+                const unsigned long long incl = __ballot((v >> 62) == 2);
+                const unsigned long long zero = __ballot((v >> 62) == 0);
+                const int kI = incl ? __ffsll((long long)incl) - 1 : 64;
+                const int kZ = zero ? __ffsll((long long)zero) - 1 : 64;
+                const int take = kI < kZ ? kI + 1 : kZ;  // lanes [0, take) are summed
+                if (take > 0) {
+                    const bool in = l < take;
+                    ecnt += wave_sum(in ? (uint32_t)((v >> 31) & kMask31) : 0u);
+                    const unsigned long long hasl = __ballot(in && (v & kMask31) != 0);
+                    const uint32_t hl = __shfl((uint32_t)(v & kMask31), hasl ? __ffsll((long long)hasl) - 1 : 0);
+                    if (elast == 0 && hasl) elast = hl;
+                }
+                if (kI < kZ) break;
+                pos -= take;
+                if (take == 0 && spin_fail(spins, P.err)) break;
+            }
+            if (l == 0)
+                st_rlx(P.status + et, kFlagIncl | ((unsigned long long)(ecnt + C) << 31) | (L1 ? L1 : elast));
+        }
+        if (l == 0) {
+            sm[0] = ecnt;
+            sm[1] = elast;
+            if (index + 1 == U.net) finish_unit(P, U, u, ecnt + C);  // last tile
+        }
+    }
+    __syncthreads();
+
+    // 3. emit (run, value) pairs: ranks from wave ballots, run = f - prev - 1.
+    // Flat indices are unit-relative and < 2^31: 32-bit arithmetic, with
+    // "no previous kept" = 0xffffffff so that run = f - prev - 1 = f.
+    uint32_t rank = sm[0];
+    uint32_t prev = sm[1] - 1u;
+    for (int i = 0; i < w; ++i) {
+        rank += sm[4 + i];
+        if (sm[8 + i]) prev = start + sm[8 + i] - 1u;
+    }
+    uint2* __restrict__ pairs = reinterpret_cast<uint2*>(P.payload + U.pay_off + 20);
+    emit_pairs(q, kb, start, w, l, rank, prev, pairs, stage);
+}
+
+}  // namespace
+
+#ifndef WC_EMIT_MINB
+#define WC_EMIT_MINB 4  // workgroups per CU the register budget is sized for
+#endif
+// One block per emit tile.  Block b packs the tile (eunits[b], eidx[b]) in
+// the ordered form, or the next ticket of unit eunits[b] in the ticket form.
+// The plan lists blocks interleaved by tile index across the units of a
+// group, groups in reverse transform order (wc_capi.cpp build_etiles).
+__global__ __launch_bounds__(kThreads, WC_EMIT_MINB) void k_emit(EmitParams P, const float* __restrict__ coef) {
+    __shared__ __attribute__((aligned(16))) uint32_t sm[32];
+    __shared__ uint2 stage_all[kThreads / kWave][256];  // per-wave pair stage (emit_pairs)
+    const int tid = threadIdx.x;
+    uint2* stage = stage_all[tid >> 6];
+    const uint32_t u = P.eunits[blockIdx.x];
+    if (P.ordered) {
+        emit_tile(P, coef, u, P.eidx[blockIdx.x], sm, stage, tid);
+        return;
+    }
+    if (tid == 0) sm[16] = atomicAdd(P.tickets + u, 1u);
+    __syncthreads();
+    const uint32_t index = __builtin_amdgcn_readfirstlane(sm[16]);
+    emit_tile(P, coef, u, index, sm, stage, tid);
+}
+
+hipError_t launch_emit(hipStream_t st, const EmitParams& p, const float* coef, uint32_t netiles) {
+    if (netiles) k_emit<<<netiles, kThreads, 0, st>>>(p, coef);
+    return hipGetLastError();
+}
+
+}  // namespace wc

@@ -28,22 +28,21 @@ namespace wc {
 constexpr int kDecRounds = kFlatTile / kThreads;  // 16 pairs per lane
 constexpr int kDecChunk = 4096;                   // floats per write round (16 KB of LDS)
 
+// Header check: the dims and ncoeff must be the unit's and nrle >= 0.  More
+// pairs than coefficients are accepted: rle_decode drops every pair whose
+// index reaches ncoeff (src/decompressor.cpp:20-27), as here.
 __device__ __forceinline__ bool read_header(const UnitDev& U, const uint8_t* __restrict__ ph, int32_t& nrle) {
     const int32_t* h = reinterpret_cast<const int32_t*>(ph);
     nrle = h[4];
-    return h[0] == U.nx && h[1] == U.ny && h[2] == U.nz && h[3] == (int32_t)U.ncells && nrle >= 0 &&
-           (uint64_t)nrle <= U.ncells;
+    return h[0] == U.nx && h[1] == U.ny && h[2] == U.nz && h[3] == (int32_t)U.ncells && nrle >= 0;
 }
 
-#ifndef WC_DEC_ORDERED
-#define WC_DEC_ORDERED 1  // 0: take the look-back tile index from a per-unit ticket atomic instead
-#endif
 __global__ __launch_bounds__(kThreads) void k_decode(const UnitDev* __restrict__ units,
                                                    const FTile* __restrict__ tiles,
                                                    const uint8_t* __restrict__ payload,
                                                    const uint64_t* __restrict__ offsets, uint32_t* __restrict__ ticket,
                                                    unsigned long long* __restrict__ status, float* __restrict__ flat,
-                                                   uint32_t* __restrict__ err) {
+                                                   uint32_t* __restrict__ err, int ordered) {
     __shared__ __attribute__((aligned(16))) float buf[kDecChunk];
     __shared__ unsigned long long s_w[4];
     __shared__ unsigned long long s_x[2];
@@ -59,18 +58,16 @@ __global__ __launch_bounds__(kThreads) void k_decode(const UnitDev* __restrict__
     // The plan launches ceil(ncoeff / kFlatTile) blocks per unit; those whose
     // plan index is past the payload's pair tiles exit before any atomic.
     if (ft.index >= ntile) return;  // uniform
-#if WC_DEC_ORDERED
-    // Tile = plan index: the plan interleaves tiles by index across units, so a
-    // tile's look-back waits only on lower block ids of its unit, and each XCD
-    // dispatches its blocks in increasing id order (waits stay bounded).
-    (void)ticket;
-    const uint32_t t = ft.index;
-#else
-    // The others take their tile from the unit's ticket.
-    if (tid == 0) s_x[0] = atomicAdd(ticket + u, 1u);
-    __syncthreads();
-    const uint32_t t = (uint32_t)s_x[0];
-#endif
+    // Tile index: ordered form (WC_OPT_ORDERED 1) = plan index: the plan
+    // interleaves tiles by index across units, so a tile's look-back waits
+    // only on lower block ids of its unit (DESIGN.md §Forward progress);
+    // ticket form = the unit's next ticket, whatever the dispatch order.
+    uint32_t t = ft.index;
+    if (!ordered) {
+        if (tid == 0) s_x[0] = atomicAdd(ticket + u, 1u);
+        __syncthreads();
+        t = (uint32_t)s_x[0];
+    }
     if (!hok && t == 0 && tid == 0) atomicOr(err, kErrHeader);
 
     // 1. this lane's pairs and their in-wave inclusive sums of (run + 1)
@@ -423,9 +420,9 @@ __global__ __launch_bounds__(64) void k_rmse_final(const UnitDev* __restrict__ u
 // Launch wrappers
 hipError_t launch_decode(hipStream_t st, const UnitDev* units, const FTile* ftiles, uint32_t nft,
                          const uint8_t* payload, const uint64_t* offsets, uint32_t* ticket,
-                         unsigned long long* status, float* flat, uint32_t* err) {
+                         unsigned long long* status, float* flat, uint32_t* err, int ordered) {
     if (nft == 0) return hipSuccess;
-    k_decode<<<nft, kThreads, 0, st>>>(units, ftiles, payload, offsets, ticket, status, flat, err);
+    k_decode<<<nft, kThreads, 0, st>>>(units, ftiles, payload, offsets, ticket, status, flat, err, ordered);
     return hipGetLastError();
 }
 

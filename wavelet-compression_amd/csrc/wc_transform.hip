@@ -2,7 +2,7 @@
 //   k_transform       generic tiles (any dims, odd tails)     src/compressor.cpp:85-185
 //   k_transform_fast  even dims, D % 8 == 0 (4 z-blocks per thread)
 // Both also reduce the unit's max-|c| key (src/compressor.cpp:212-215).
-// The tile bodies live in wc_xform.h (shared with the pipelined kernel).
+// The tile bodies live in wc_xform.h.
 //
 // Numerics (bit-exact with the reference): the reference
 // pair `(a + b) / 2.0` is a float add, an exact halving in double and one
@@ -15,10 +15,9 @@
 namespace wc {
 
 // Output position of a unit's flat coefficients: 0 the dense flat scratch
-// (coef_off), 1 at the unit's cell offset (wc_decompose), 2 its slot in the
-// chunked forward's coefficient slots (ring_off).
+// (coef_off), 1 at the unit's cell offset (wc_decompose).
 __device__ __forceinline__ uint64_t out_base(const UnitDev& U, int mode) {
-    return mode == 1 ? U.cell_off : mode == 2 ? U.ring_off : U.coef_off;
+    return mode == 1 ? U.cell_off : U.coef_off;
 }
 
 // ---------------------------------------------------------------------------

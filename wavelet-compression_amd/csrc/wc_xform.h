@@ -1,5 +1,5 @@
-// wc_xform.h — the two transform-tile bodies (K1) shared by the staged
-// kernels (wc_transform.hip) and the pipelined forward kernel (wc_pipe.hip).
+// wc_xform.h — the transform-tile bodies (K1) of wc_transform.hip and the
+// helpers the emit and inverse kernels share with them.
 //
 // One-level 3-D Haar, src/compressor.cpp:85-185: a coefficient (I, J, K)
 // depends only on the 2x2x2 input block (I mod hx, J mod hy, K mod hz), so a
