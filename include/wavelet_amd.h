@@ -92,9 +92,14 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  *   progress); 0 takes it from a per-unit ticket atomic instead, which needs no
  *   assumption about dispatch order.  Same bytes out either way.  Every wait
  *   between workgroups is bounded: a wait that never ends is reported as
- *   WC_ERR_HIP at the next wc_synchronize, not a hang. */
+ *   WC_ERR_HIP at the next wc_synchronize, not a hang.
+ * WC_OPT_INVERSE_ROWS (default 1): the inverse of even-dims units (W, H even,
+ *   D % 8 == 0) indexes the payload's pairs by flat row and reconstructs each
+ *   tile straight from the payload; 0 decodes every unit into a dense fp32
+ *   coefficient scratch first (4 B/cell written and read back).  Same cells. */
 #define WC_OPT_SPARSE 12
 #define WC_OPT_ORDERED 13
+#define WC_OPT_INVERSE_ROWS 14
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 
 /* Host-side helpers (no device work). */

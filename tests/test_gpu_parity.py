@@ -8,7 +8,7 @@ in a fixed tree order).
 """
 import numpy as np
 import pytest
-from wavelet_compression_amd.capi import WC_OPT_ORDERED, WC_OPT_SPARSE
+from wavelet_compression_amd.capi import WC_OPT_INVERSE_ROWS, WC_OPT_ORDERED, WC_OPT_SPARSE
 
 pytestmark = pytest.mark.gpu
 
@@ -40,6 +40,7 @@ def set_path(ctx, path):
     """Library options of a path ("staged" = the defaults)."""
     ctx.set_option(WC_OPT_SPARSE, 0 if path == "dense" else 1)
     ctx.set_option(WC_OPT_ORDERED, 0 if path == "tickets" else 1)
+    ctx.set_option(WC_OPT_INVERSE_ROWS, 0 if path == "dense_inverse" else 1)
 
 
 def gpu_payloads(wc, ctx, boxes, keep, dtype=np.float64, offsets=None, path="staged"):
@@ -206,7 +207,7 @@ def test_empty_and_degenerate_units(wc, ctx, oracle):
             assert got[i] == oracle.compress_payload(b, keep)[0]
 
 
-@pytest.mark.parametrize("path", ["staged", "tickets"])
+@pytest.mark.parametrize("path", ["staged", "tickets", "dense_inverse"])
 @pytest.mark.parametrize("keep", [KEEPS[0], KEEPS[2]])
 def test_inverse_bit_exact(wc, ctx, oracle, keep, path):
     boxes = synth(oracle, DIMS, seed0=4)
@@ -307,11 +308,14 @@ def test_malformed_payload_rejected(wc, ctx, oracle):
         assert ei.value.code == wc.capi.WC_ERR_FORMAT
 
 
-@pytest.mark.parametrize("runs", [[0, 3, 10, 0], [0] * 40, [2] * 7 + [0] * 30, [15, 0, 0, 4]])
-def test_rle_decode_out_of_range_pairs_dropped(wc, ctx, oracle, runs):
+@pytest.mark.parametrize("dims", [(4, 2, 2), (4, 2, 8)])  # generic (dense decode) and row-indexed shapes
+@pytest.mark.parametrize("runs", [[0, 3, 10, 0], [0] * 40, [2] * 7 + [0] * 30, [15, 0, 0, 4], [0] * 64,
+                                  [0] * 63 + [5], [70, 0], [], [63], [1] * 31 + [0] * 3])
+def test_rle_decode_out_of_range_pairs_dropped(wc, ctx, oracle, runs, dims):
     """rle_decode drops pairs whose index reaches total (src/decompressor.cpp:20-27),
-    also when the payload holds more pairs than coefficients (nrle > ncoeff)."""
-    W, H, D = 4, 2, 2
+    also when the payload holds more pairs than coefficients (nrle > ncoeff); an
+    empty payload and payloads that end exactly at ncoeff."""
+    W, H, D = dims
     runs = np.array(runs, np.int32)
     vals = (np.arange(runs.size, dtype=np.float32) + 1.5).astype(np.float32)
     p = oracle.serialize(W, H, D, W * H * D, runs, vals)

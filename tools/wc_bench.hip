@@ -5,9 +5,9 @@
 // Box-Muller noise), then wc_forward runs `steps` times.  Prints one JSON line.
 //
 // usage: wc_bench [boxes=1024] [dim=64] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1]
-//                 [check=0|1] [ordered=1] [sparse=1]
+//                 [check=0|1] [ordered=1] [sparse=1] [rows=1]
 // check=1: also run the conservative configuration (ticket look-back, dense
-// staging) once and compare every unit's payload bytes and, with inverse=1,
+// staging, dense inverse decode) once and compare every unit's payload bytes and, with inverse=1,
 // every reconstructed cell ("paths_identical" in the JSON line).
 #include <hip/hip_runtime.h>
 
@@ -64,6 +64,7 @@ int main(int argc, char** argv) {
     const bool check = argc > 8 ? std::atoi(argv[8]) != 0 : false;
     const int ordered = argc > 9 ? std::atoi(argv[9]) : 1;
     const int sparse = argc > 10 ? std::atoi(argv[10]) : 1;
+    const int rows = argc > 11 ? std::atoi(argv[11]) : 1;
 
     std::vector<wc_unit> units(boxes);
     const unsigned long long per = (unsigned long long)dim * dim * dim;
@@ -94,6 +95,7 @@ int main(int argc, char** argv) {
     }
     wc_set_option(ctx, WC_OPT_ORDERED, ordered);
     wc_set_option(ctx, WC_OPT_SPARSE, sparse);
+    wc_set_option(ctx, WC_OPT_INVERSE_ROWS, rows);
     auto fwd = [&]() {
         int rc = wc_forward(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, keep, payload, cap, offsets, kept);
         if (rc != WC_OK) {
@@ -165,9 +167,11 @@ int main(int argc, char** argv) {
         run(off_a, k_a, pa, ra);
         wc_set_option(ctx, WC_OPT_ORDERED, 0);
         wc_set_option(ctx, WC_OPT_SPARSE, 0);
+        wc_set_option(ctx, WC_OPT_INVERSE_ROWS, 0);
         run(off_b, k_b, pb, rb);
         wc_set_option(ctx, WC_OPT_ORDERED, ordered);
         wc_set_option(ctx, WC_OPT_SPARSE, sparse);
+        wc_set_option(ctx, WC_OPT_INVERSE_ROWS, rows);
         identical = 1;
         for (int i = 0; i < boxes && identical; ++i) {
             if (k_a[i] != k_b[i] || off_a[i] != off_b[i]) identical = 0;
@@ -184,9 +188,9 @@ int main(int argc, char** argv) {
     const char* names[WC_NUM_STAGES] = {"transform", "emit", "decode", "inverse", "rmse", "hist"};
     std::printf("{\"boxes\": %d, \"dim\": %d, \"dtype\": \"%s\", \"keep\": %.17g, \"steps\": %d, "
                 "\"ms_per_step\": %.4f, \"cells_per_s\": %.6e, \"kept_fraction\": %.6f, \"payload_bytes\": %llu, "
-                "\"ordered\": %d, \"sparse\": %d, \"paths_identical\": %d, \"stage_ms\": {",
+                "\"ordered\": %d, \"sparse\": %d, \"rows\": %d, \"paths_identical\": %d, \"stage_ms\": {",
                 boxes, dim, f64 ? "f64" : "f32", keep, steps, step_ms, per * boxes / (step_ms * 1e-3),
-                ksum / (double)(per * boxes), (unsigned long long)total, ordered, sparse, identical);
+                ksum / (double)(per * boxes), (unsigned long long)total, ordered, sparse, rows, identical);
     bool first = true;
     for (int s = 0; s < WC_NUM_STAGES; ++s)
         if (cnt[s]) {

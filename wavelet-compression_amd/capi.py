@@ -32,6 +32,7 @@ EXPORTED = (
 )
 WC_OPT_SPARSE = 12   # sparse coefficient staging in the forward (default 1)
 WC_OPT_ORDERED = 13  # look-back tile index from the launch order (1, default) or per-unit tickets (0)
+WC_OPT_INVERSE_ROWS = 14  # row-indexed inverse of even-dims units (1, default) or dense decode (0)
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*).
 STAGES = ("transform", "emit", "decode", "inverse", "rmse", "hist")

@@ -32,8 +32,10 @@ hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, 
 hipError_t launch_transform_fallback(hipStream_t, const void*, int, const UnitDev*, int, const XTile*, size_t, float*,
                                      const unsigned long long*, double);
 hipError_t launch_pack(hipStream_t, const UnitDev*, int, const uint32_t*, const uint8_t*, uint64_t*, uint8_t*);
-hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, const uint8_t*, const uint64_t*,
-                         uint32_t*, unsigned long long*, float*, uint32_t*, int);
+hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, const FTile*, uint32_t, const uint8_t*,
+                         const uint64_t*, uint32_t*, unsigned long long*, float*, uint2*, uint32_t*, int);
+hipError_t launch_inverse_rows(hipStream_t, const RTile*, uint32_t, size_t, const uint8_t*, const uint64_t*,
+                               const uint2*, float*);
 hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const XTile*, uint32_t, size_t, uint32_t,
                           size_t, float*);
 hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDev*, int, const FTile*,
@@ -62,15 +64,20 @@ struct Plan {
     std::vector<wc_unit> key;
     std::vector<UnitDev> units;
     std::vector<XTile> xtiles;
-    std::vector<XTile> ixtiles;  // inverse launch order (see get_plan)
-    std::vector<FTile> ftiles, dtiles;
+    std::vector<XTile> ixtiles;  // dense inverse tiles of the non-row-indexed units: [generic | fast]
+    std::vector<RTile> rtiles;   // K6r tiles of the row-indexed units
+    std::vector<FTile> ftiles, dtiles, rdtiles;  // dtiles: dense decode, rdtiles: row index (K5)
     std::vector<uint32_t> eunits, eidx;
     uint32_t ngen = 0, nfast = 0, netiles = 0;
+    uint32_t ign = 0, ifast = 0;  // ixtiles split
+    bool inv_rows = true;         // WC_OPT_INVERSE_ROWS the plan was built with
+    uint64_t rowinfo_entries = 0;
+    size_t lds_rows = 0;
     bool any_sparse = false;
     uint64_t coef_extent = 0;  // floats of staged coefficient scratch
     size_t lds_gen = 0, lds_fast = 0, lds_inverse = 0;
     size_t state_bytes = 0;    // forward per-call state: 16 | key[n] | tickets[n] | status[netiles]
-    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_eunits, d_ixtiles, d_eidx;
+    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_eunits, d_ixtiles, d_eidx, d_rtiles, d_rdtiles;
 };
 
 int ceil_log2(int64_t v) {
@@ -90,6 +97,7 @@ struct wc_ctx {
     bool plan_valid = false;
     bool opt_ordered = true;  // WC_OPT_ORDERED (see include/wavelet_amd.h)
     bool opt_sparse = true;   // WC_OPT_SPARSE
+    bool opt_inv_rows = true; // WC_OPT_INVERSE_ROWS
     // A kernel that may raise error bits ran since the last check.  Kernels
     // atomicOr into ONE persistent error word (errflag, zeroed at creation and
     // after each read), so errors of several async calls accumulate until the
@@ -101,7 +109,7 @@ struct wc_ctx {
     bool sparse_staged = false;  // the last stage_transform used sparse staging
     uint64_t plan_gen = 0;  // bumped whenever get_plan rebuilds the plan
     // scratch (grow-only)
-    DevBuf coef, part, errflag, state, flags;
+    DevBuf coef, part, errflag, state, flags, rowinfo;
     // host-path staging
     DevBuf h_cells, h_payload, h_packed, h_offsets, h_poff, h_kept, h_out;
     // per-kernel event timing (wc_profile_enable / wc_profile_read)
@@ -260,20 +268,46 @@ void build_etiles(Plan& P, int n) {
     }
 }
 
+// K6r tiling (wc_inverse.hip k_inverse_rows): TX x TY blocks in (x, y), all of
+// z; the tile's LDS is 4 TX ranges of TY*D + 4 floats, at most kRixLds.  TX
+// up to 32 blocks (64-cell output rows), then TY as large as fits.  Units of
+// the fast shape only (even W and H, D % 8 == 0: no odd tails, float4
+// sub-band reads); the others decode densely.
+size_t rix_lds_bytes(const UnitDev& d) { return sizeof(float) * 4 * (size_t)rix_wr(d.ilbx, d.ilby, d.nz); }
+
+bool set_rix_tiling(UnitDev& d) {
+    d.rix = 0;
+    if (!d.fast || d.ncells == 0) return false;
+    auto floats = [&](int tx, int ty) { return (int64_t)4 * (tx * ((int64_t)ty * d.nz + 4) + 16); };
+    int lx = std::min(5, ceil_log2(d.hx));
+    while (lx > 0 && floats(1 << lx, 1) > kRixLds) --lx;
+    if (floats(1 << lx, 1) > kRixLds) return false;
+    int ly = 0;
+    while ((1 << ly) < d.hy && floats(1 << lx, 2 << ly) <= kRixLds) ++ly;
+    d.ilbx = lx;
+    d.ilby = ly;
+    d.rix = 1;
+    return true;
+}
+
 // Build (or reuse) the plan for this batch and upload it.
 int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     Plan& P = c->plan;
-    if (c->plan_valid && (int)P.key.size() == n && (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0))
+    if (c->plan_valid && P.inv_rows == c->opt_inv_rows && (int)P.key.size() == n &&
+        (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0))
         return WC_OK;
     c->plan_valid = false;
     ++c->plan_gen;
     P.key.assign(units, units + n);
+    P.inv_rows = c->opt_inv_rows;
     P.units.assign(n, UnitDev{});
     P.xtiles.clear();
     P.ftiles.clear();
     P.ngen = P.nfast = 0;
     P.any_sparse = false;
-    P.lds_gen = P.lds_fast = P.lds_inverse = 0;
+    P.lds_gen = P.lds_fast = P.lds_inverse = P.lds_rows = 0;
+    P.rtiles.clear();
+    P.rowinfo_entries = 0;
     std::vector<XTile> gen, fast;
     uint64_t coef_cursor = 0, pay_cursor = 4;
     for (int i = 0; i < n; ++i) {
@@ -312,6 +346,32 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         else
             P.lds_gen = std::max(P.lds_gen, transform_lds_bytes(d.lbx, d.lby, d.lbz));
         P.lds_inverse = std::max(P.lds_inverse, transform_lds_bytes(d.lbx, d.lby, d.lbz));
+        if (P.inv_rows && set_rix_tiling(d)) {
+            d.row_off = P.rowinfo_entries;
+            P.rowinfo_entries += (uint64_t)d.nx * d.ny + 1;
+            {  // floor(p / D) = (p * m) >> (31 + l), p < 2^31 (wc_inverse.hip div_rows)
+                const int lg = ceil_log2(d.nz);
+                const uint64_t m = (uint64_t(1) << (31 + lg)) / (uint64_t)d.nz + 1;
+                d.dmagic = m | ((uint64_t)(31 + lg) << 32);
+            }
+            for (int by = 0; by < d.hy; by += 1 << d.ilby)
+                for (int bx = 0; bx < d.hx; bx += 1 << d.ilbx) {
+                    RTile r{};
+                    r.row_off = d.row_off;
+                    r.cell_off = d.cell_off;
+                    r.unit = (uint32_t)i;
+                    r.bx0 = bx;
+                    r.by0 = by;
+                    r.W = d.nx;
+                    r.H = d.ny;
+                    r.D = d.nz;
+                    r.lbx = d.ilbx;
+                    r.lby = d.ilby;
+                    r.tyv = std::min(1 << d.ilby, d.hy - by);
+                    P.rtiles.push_back(r);
+                }
+            P.lds_rows = std::max(P.lds_rows, rix_lds_bytes(d));
+        }
     }
     P.ngen = (uint32_t)gen.size();
     P.nfast = (uint32_t)fast.size();
@@ -319,13 +379,16 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         if (d.fast) d.xt_begin += P.ngen;
     P.xtiles = std::move(gen);
     P.xtiles.insert(P.xtiles.end(), fast.begin(), fast.end());
-    // The inverse runs its fast tiles in reverse unit order: the first blocks
-    // read the coefficients the decode wrote last (Infinity-Cache hits;
-    // measured 1024 x 64^3 K6 0.413-0.429 -> 0.409 ms).  Grouping the
-    // decode's interleave to sharpen this slowed the decode more than it saved.
-    P.ixtiles = P.xtiles;
-    std::stable_sort(P.ixtiles.begin() + P.ngen, P.ixtiles.end(),
-                     [](const XTile& x, const XTile& y) { return x.unit > y.unit; });
+    // Dense inverse tiles of the units that are not row-indexed: generic, then
+    // fast in reverse unit order (the first blocks read the coefficients the
+    // decode wrote last: Infinity-Cache hits).
+    P.ixtiles.clear();
+    for (const XTile& x : P.xtiles)
+        if (!P.units[x.unit].rix && !P.units[x.unit].fast) P.ixtiles.push_back(x);
+    P.ign = (uint32_t)P.ixtiles.size();
+    for (auto it = P.xtiles.rbegin(); it != P.xtiles.rend(); ++it)
+        if (!P.units[it->unit].rix && P.units[it->unit].fast) P.ixtiles.push_back(*it);
+    P.ifast = (uint32_t)P.ixtiles.size() - P.ign;
     for (int i = 0; i < n; ++i) {
         UnitDev& d = P.units[i];
         d.ftile_begin = (uint32_t)P.ftiles.size();
@@ -334,14 +397,22 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     }
     // Decode blocks, interleaved by tile index across units: the pair tiles a
     // payload actually has (the low indices) are dispatched first, the blocks
-    // past a unit's pairs (which exit at once) last.
+    // past a unit's pairs (which exit at once) last.  A row-indexed unit gets
+    // one tile more when kFlatTile divides ncoeff (the virtual pair k = nrle
+    // that closes its row index, wc_inverse.hip).
     P.dtiles.clear();
+    P.rdtiles.clear();
     {
-        uint32_t maxt = 0;
-        for (const UnitDev& d : P.units) maxt = std::max(maxt, d.nftiles);
+        uint32_t maxt = 0, total = 0;
+        for (UnitDev& d : P.units) {
+            d.ndt = d.rix ? (uint32_t)(d.ncells / kFlatTile) + 1 : d.nftiles;
+            d.dt_begin = total;
+            total += d.ndt;
+            maxt = std::max(maxt, d.ndt);
+        }
         for (uint32_t t = 0; t < maxt; ++t)
             for (int i = 0; i < n; ++i)
-                if (t < P.units[i].nftiles) P.dtiles.push_back(FTile{(uint32_t)i, t});
+                if (t < P.units[i].ndt) (P.units[i].rix ? P.rdtiles : P.dtiles).push_back(FTile{(uint32_t)i, t});
     }
     P.coef_extent = coef_cursor ? coef_cursor + kFlatTile : 0;  // slack: flat tiles read whole float4 groups
     build_etiles(P, n);
@@ -352,7 +423,9 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         (rc = upload(c, P.d_ftiles, P.ftiles.data(), sizeof(FTile) * P.ftiles.size(), "upload ftiles")) ||
         (rc = upload(c, P.d_dtiles, P.dtiles.data(), sizeof(FTile) * P.dtiles.size(), "upload dtiles")) ||
         (rc = upload(c, P.d_eunits, P.eunits.data(), sizeof(uint32_t) * P.eunits.size(), "upload eunits")) ||
-        (rc = upload(c, P.d_eidx, P.eidx.data(), sizeof(uint32_t) * P.eidx.size(), "upload eidx")))
+        (rc = upload(c, P.d_eidx, P.eidx.data(), sizeof(uint32_t) * P.eidx.size(), "upload eidx")) ||
+        (rc = upload(c, P.d_rtiles, P.rtiles.data(), sizeof(RTile) * P.rtiles.size(), "upload rtiles")) ||
+        (rc = upload(c, P.d_rdtiles, P.rdtiles.data(), sizeof(FTile) * P.rdtiles.size(), "upload rdtiles")))
         return rc;
     // The host vectors back the async copies: finish them before returning.
     hipError_t e = hipStreamSynchronize(c->stream);
@@ -361,8 +434,10 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     return WC_OK;
 }
 
-// Per-call state of the decode: ticket[n] (8-B aligned) | status[flat tiles].
-size_t decode_state_bytes(const Plan& P) { return round_up(4ull * P.units.size(), 8) + 8ull * P.ftiles.size(); }
+// Per-call state of the decode: ticket[n] (8-B aligned) | status[decode tiles].
+size_t decode_state_bytes(const Plan& P) {
+    return round_up(4ull * P.units.size(), 8) + 8ull * (P.dtiles.size() + P.rdtiles.size());
+}
 
 // Scratch of the staged forward, the inverse and the RMSE (grow-only).
 int ensure_scratch(wc_ctx* c) {
@@ -372,6 +447,7 @@ int ensure_scratch(wc_ctx* c) {
     if ((rc = ensure(c, c->coef, sizeof(float) * std::max<uint64_t>(P.coef_extent, 1))) ||
         (rc = ensure(c, c->flags, (P.coef_extent >> kSegShift) + kEmitTile)) ||
         (rc = ensure(c, c->part, sizeof(double) * nft)) ||
+        (rc = ensure(c, c->rowinfo, sizeof(uint32_t) * 2 * std::max<uint64_t>(P.rowinfo_entries, 1))) ||
         (rc = ensure(c, c->state, std::max<size_t>(P.state_bytes, decode_state_bytes(P)))))
         return rc;
     return WC_OK;
@@ -523,7 +599,8 @@ void wc_ctx_destroy(wc_ctx* c) {
                       &c->flags,         &c->h_cells,        &c->h_payload,      &c->h_packed,
                       &c->h_offsets,     &c->h_poff,         &c->h_kept,         &c->h_out,
                       &c->plan.d_units,  &c->plan.d_xtiles,  &c->plan.d_ftiles,  &c->plan.d_dtiles,
-                      &c->plan.d_eunits, &c->plan.d_ixtiles, &c->plan.d_eidx};
+                      &c->plan.d_eunits, &c->plan.d_ixtiles, &c->plan.d_eidx, &c->plan.d_rtiles,
+                      &c->plan.d_rdtiles, &c->rowinfo};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& m : c->marks) {
@@ -551,6 +628,9 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
             return WC_OK;
         case WC_OPT_ORDERED:
             c->opt_ordered = value != 0;
+            return WC_OK;
+        case WC_OPT_INVERSE_ROWS:
+            c->opt_inv_rows = value != 0;
             return WC_OK;
         default:
             return fail(c, WC_ERR_INVALID, "unknown option");
@@ -706,15 +786,20 @@ int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, c
     {
         StageTimer t(c, WC_STAGE_DECODE);
         e = launch_decode(c->stream, (const UnitDev*)P.d_units.p, (const FTile*)P.d_dtiles.p,
-                          (uint32_t)P.dtiles.size(), d_payload, d_offsets, (uint32_t*)st,
+                          (uint32_t)P.dtiles.size(), (const FTile*)P.d_rdtiles.p, (uint32_t)P.rdtiles.size(),
+                          d_payload, d_offsets, (uint32_t*)st,
                           (unsigned long long*)(st + round_up(4ull * n, 8)), (float*)c->coef.p,
-                          (uint32_t*)c->errflag.p, c->opt_ordered ? 1 : 0);
+                          (uint2*)c->rowinfo.p, (uint32_t*)c->errflag.p, c->opt_ordered ? 1 : 0);
     }
     if (e != hipSuccess) return hip_fail(c, e, "decode launch");
     {
         StageTimer t(c, WC_STAGE_INVERSE);
-        e = launch_inverse(c->stream, (const float*)c->coef.p, 0, (const UnitDev*)P.d_units.p,
-                           (const XTile*)P.d_ixtiles.p, P.ngen, P.lds_inverse, P.nfast, P.lds_fast, d_out);
+        e = launch_inverse_rows(c->stream, (const RTile*)P.d_rtiles.p, (uint32_t)P.rtiles.size(), P.lds_rows,
+                                d_payload, d_offsets,
+                                (const uint2*)c->rowinfo.p, d_out);
+        if (e == hipSuccess)
+            e = launch_inverse(c->stream, (const float*)c->coef.p, 0, (const UnitDev*)P.d_units.p,
+                               (const XTile*)P.d_ixtiles.p, P.ign, P.lds_inverse, P.ifast, P.lds_fast, d_out);
     }
     if (e != hipSuccess) return hip_fail(c, e, "inverse launch");
     // Malformed payloads surface at the next wc_synchronize (WC_ERR_FORMAT).

@@ -36,6 +36,13 @@ struct UnitDev {
     uint32_t et_begin;      // first emit tile (kEmitTile coefficients) of the unit
     uint32_t net;           // emit tiles = max(1, ceil(ncells / kEmitTile))
     uint32_t sparse;        // 1: staged forward stores only flagged 32-coefficient segments (wc_xform.h)
+    // inverse (wc_inverse.hip)
+    uint32_t dt_begin;      // first decode tile (kFlatTile pairs) of the unit: look-back status index
+    uint32_t ndt;           // decode tiles launched for the unit
+    int32_t rix;            // 1: row-indexed inverse (K5 row index + K6r), 0: dense flat scratch
+    int32_t ilbx, ilby;     // log2 of K6r's tile in blocks along x and y (all of z)
+    uint64_t row_off;       // first rowinfo entry of the unit (W*H + 1 entries)
+    uint64_t dmagic;        // floor(2^64 / D) + 1: row = floor(position / D)
 };
 
 // A transform tile: a (1<<lbx) x (1<<lby) x (1<<lbz) box of 2x2x2 blocks.
@@ -43,6 +50,24 @@ struct XTile {
     uint32_t unit;
     uint32_t bx0, by0, bz0;
 };
+
+// A K6r tile (row-indexed inverse, wc_inverse.hip): everything the kernel
+// needs about the tile and its unit in one record (one scalar load batch).
+struct RTile {
+    uint64_t row_off;   // the unit's first rowinfo entry
+    uint64_t cell_off;  // the unit's first output cell
+    uint32_t unit;
+    int32_t bx0, by0;   // first block of the tile along x and y (all of z)
+    int32_t W, H, D;
+    int32_t lbx, lby;   // log2 of the tile's blocks along x and y
+    int32_t tyv;        // blocks along y in this tile (<= 1 << lby at the unit's edge)
+    int32_t pad;
+};
+
+// LDS layout of a K6r tile: 4 wave regions of TX ranges of RS = TY*D + 4
+// floats, regions 16 floats apart (bank offset), 16-B aligned.
+__host__ __device__ inline int rix_rs(int lby, int D) { return (D << lby) + 4; }
+__host__ __device__ inline int rix_wr(int lbx, int lby, int D) { return (rix_rs(lby, D) << lbx) + 16; }
 
 // A flat tile: kFlatTile consecutive coefficients (flat order) of one unit.
 struct FTile {
@@ -81,6 +106,7 @@ struct EmitParams {
     const uint8_t* flags;          // sparse-staging segment flags (null: every unit dense)
 };
 
-constexpr int kSegShift = 4;  // sparse staging: flag index space of 16 coefficients per byte (min segment)
+constexpr int kSegShift = 4;
+constexpr int kRixLds = 9216;  // K6r tile: at most this many floats of LDS (36 KB: 4 workgroups per CU)  // sparse staging: flag index space of 16 coefficients per byte (min segment)
 
 }  // namespace wc

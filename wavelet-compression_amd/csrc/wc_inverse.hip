@@ -1,30 +1,43 @@
 // wc_inverse.hip — decode, inverse transform and RMSE.
-//   K5       k_decode: rle_decode into dense rows    src/decompressor.cpp:14-30
-//   K6       k_inverse{,_fast}: flat -> Box3D        src/decompressor.cpp:79-159
-//   K7       k_rmse_*: per-unit RMSE                 src/calc-loss.cpp:12-43
+//   K5   k_decode: rle_decode                        src/decompressor.cpp:14-30
+//        - row-indexed units: a row index of the payload's pairs
+//        - other units: dense flat coefficients
+//   K6r  k_inverse_rows: pairs -> Box3D, row-indexed  src/decompressor.cpp:14-30, 79-159
+//   K6   k_inverse{,_fast}: dense flat -> Box3D       src/decompressor.cpp:79-159
+//   K7   k_rmse_*: per-unit RMSE                      src/calc-loss.cpp:12-43
 // The inverse pair `avg +/- diff` is evaluated in double and stored as float
 // by the reference; a float add is bit-identical (53 >= 2*24 + 2).
 #include "wc_xform.h"
 
+#include <algorithm>
+
 namespace wc {
 
 // ---------------------------------------------------------------------------
-// K5: rle_decode (src/decompressor.cpp:14-30) straight into the dense flat
-// scratch, in one pass and without a memset.  Pair tile t (kFlatTile pairs)
-// of a unit owns the flat range [S_t, S_t+1): from just after the previous
-// tile's last pair through its own last pair (the unit's last tile: through
-// ncoeff - 1), and writes every element of it — zeros between pairs.  Pair k
-// lands at (sum of run + 1 over pairs <= k) - 1 while that is < ncoeff, which
-// is rle_decode's `idx += run; if (idx < total) out[idx++] = val`; every later
-// pair is dropped.  S_t (the sum over the unit's earlier tiles) comes from a
-// decoupled look-back; a block takes its tile index from a per-unit ticket,
-// so a tile's predecessors have always started, and blocks past the unit's
-// last pair tile exit.
-//
-// Pairs are loaded coalesced: wave w, round r, lane l holds pair
+// K5: rle_decode (src/decompressor.cpp:14-30).  Pair k lands at flat position
+// p_k = (sum of run + 1 over pairs <= k) - 1 while that is < ncoeff, which is
+// rle_decode's `idx += run; if (idx < total) out[idx++] = val`; every later
+// pair is dropped.  Pair tile t (kFlatTile pairs) gets the sum over the unit's
+// earlier tiles from a decoupled look-back (tile index from the launch order
+// or a per-unit ticket, WC_OPT_ORDERED); blocks past the payload's last pair
+// tile exit.  Pairs are loaded coalesced: wave w, round r, lane l holds pair
 // w*1024 + r*64 + l of the tile; positions come from wave scans of run + 1.
-// The range is written in kDecChunk-element rounds: zero an LDS chunk, drop
-// the tile's pairs that fall in it, copy it out with 16-B stores.
+//
+// Two forms:
+//   k_rowindex  row-indexed units (U.rix, the even-dims fast shapes): writes
+//               no coefficient.  For every flat row r = I*H + J (D
+//               coefficients) whose first position r*D lies in (p_{k-1}, p_k]
+//               it writes rowinfo[r] = (k, p_k - r*D): the row's pairs are k ..
+//               rowinfo[r+1].x - 1 and the first lands at p_k.  The virtual
+//               pair k = nrle at position ncoeff closes the table (rows past the
+//               last pair and the sentinel row W*H); a dropped pair counts as
+//               position ncoeff.  K6r then reads each tile's pairs straight
+//               from the payload: the dense fp32 scratch is never materialised.
+//   k_decode    other units: the tile owns the flat range [S_t, S_t+1) from just
+//               after the previous tile's last pair through its own last pair
+//               (the unit's last tile: through ncoeff - 1) and writes every
+//               element of it — zeros between pairs — through LDS in
+//               kDecChunk-element rounds (no memset of the scratch).
 constexpr int kDecRounds = kFlatTile / kThreads;  // 16 pairs per lane
 constexpr int kDecChunk = 4096;                   // floats per write round (16 KB of LDS)
 
@@ -35,6 +48,174 @@ __device__ __forceinline__ bool read_header(const UnitDev& U, const uint8_t* __r
     const int32_t* h = reinterpret_cast<const int32_t*>(ph);
     nrle = h[4];
     return h[0] == U.nx && h[1] == U.ny && h[2] == U.nz && h[3] == (int32_t)U.ncells && nrle >= 0;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_sum32(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
+// The same with saturating adds (v_add_u32 clamp): positions at or past
+// ncoeff (< 2^31) are all "dropped", so sums clamped at 2^32 - 1 decide the
+// same rows as exact ones.
+__device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) { return __builtin_elementwise_add_sat(a, b); }
+
+__device__ __forceinline__ uint32_t wave_incl_sum32_sat(uint32_t v) {
+    v = sat_add(v, __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false));
+    v = sat_add(v, __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false));
+    v = sat_add(v, __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false));
+    v = sat_add(v, __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false));
+    v = sat_add(v, __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));
+    v = sat_add(v, __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+
+// floor(p / D) for p < 2^31 (Granlund-Montgomery, N = 31): dmagic = m |
+// (31 + l) << 32, l = ceil(log2 D), m = floor(2^(31+l) / D) + 1 < 2^32.
+__device__ __forceinline__ uint32_t div_rows(uint32_t p, uint64_t dmagic) {
+    return (uint32_t)(((uint64_t)p * (uint32_t)dmagic) >> (uint32_t)(dmagic >> 32));
+}
+
+// Rows [r_lo, r_lo + cnt) of this lane get (k, p - r * D).  Most lanes write 0
+// or 1 row; a long run of zeros (empty rows) is spread over the whole wave.
+__device__ __forceinline__ void write_rows(uint2* __restrict__ ri, uint32_t r_lo, uint32_t cnt, uint32_t k,
+                                           uint32_t p, uint32_t D, int l) {
+    if (!__ballot(cnt > 1)) {
+        if (cnt) ri[r_lo] = make_uint2(k, p - r_lo * D);
+        return;
+    }
+    const uint32_t incl = wave_incl_sum32(cnt);
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+    const uint32_t excl = incl - cnt;
+    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+        const uint32_t job = j0 + (uint32_t)l;
+        int o = 0;  // first lane whose inclusive count exceeds job
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1)
+            if ((uint32_t)__shfl(incl, o + s - 1) <= job) o += s;
+        o = o > 63 ? 63 : o;
+        const uint32_t orl = __shfl(r_lo, o), oex = __shfl(excl, o), ok = __shfl(k, o), op = __shfl(p, o);
+        if (job < total) {
+            const uint32_t r = orl + (job - oex);
+            ri[r] = make_uint2(ok, op - r * D);
+        }
+    }
+}
+
+// Row index of the row-indexed units.  Only the runs are needed (the values
+// stay in the payload for K6r).  A negative run (malformed; the reference's
+// behaviour is undefined) counts as run 0, so positions never decrease and
+// every row entry is written: K6r never sees a stale or out-of-range entry.
+__global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict__ units,
+                                                     const FTile* __restrict__ tiles,
+                                                     const uint8_t* __restrict__ payload,
+                                                     const uint64_t* __restrict__ offsets,
+                                                     uint32_t* __restrict__ ticket,
+                                                     unsigned long long* __restrict__ status,
+                                                     uint2* __restrict__ rowinfo, uint32_t* __restrict__ err,
+                                                     int ordered) {
+    __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_x[2];
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const FTile ft = tiles[blockIdx.x];
+    const uint32_t u = ft.unit;
+    const UnitDev& U = units[u];
+    const uint8_t* ph = payload + offsets[u];
+    int32_t nrle;
+    const bool hok = read_header(U, ph, nrle);
+    const uint32_t n = hok ? (uint32_t)nrle : 0u;
+    // tiles up to the one holding the virtual pair k = n; the plan launches
+    // floor(ncoeff / kFlatTile) + 1, enough for the first dropped pair
+    const uint32_t ntile = n / kFlatTile + 1u;
+    if (ft.index >= ntile) return;  // uniform
+    uint32_t t = ft.index;
+    if (!ordered) {
+        if (tid == 0) s_x[0] = atomicAdd(ticket + u, 1u);
+        __syncthreads();
+        t = s_x[0];
+    }
+    if (!hok && t == 0 && tid == 0) atomicOr(err, kErrHeader);
+
+    // 1. runs -> v = run + 1 (k < n), 0 (k >= n); saturating in-wave sums
+    const uint32_t* __restrict__ runs = reinterpret_cast<const uint32_t*>(ph + 20);
+    const uint32_t kw = t * (uint32_t)kFlatTile + (uint32_t)w * (kFlatTile / 4);
+    uint32_t v[kDecRounds];
+#pragma unroll
+    for (int r = 0; r < kDecRounds; ++r) {
+        const uint32_t k = kw + r * 64 + l;
+        v[r] = k < n ? runs[2 * k] : 0u;
+    }
+    bool neg = false;
+    uint32_t wsum = 0, x[kDecRounds];
+#pragma unroll
+    for (int r = 0; r < kDecRounds; ++r) {
+        const uint32_t k = kw + r * 64 + l;
+        const int32_t run = (int32_t)v[r];
+        neg |= k < n && run < 0;
+        x[r] = k < n ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
+        const uint32_t s = wave_incl_sum32_sat(x[r]);
+        v[r] = sat_add(wsum, s);  // now: inclusive sum within the wave's pairs
+        wsum = sat_add(wsum, __builtin_amdgcn_readlane(s, 63));
+    }
+    if (neg) atomicOr(err, kErrNegativeRun);
+    if (l == 0) s_w[w] = wsum;
+    __syncthreads();
+    uint32_t wexcl = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        wexcl = i < w ? sat_add(wexcl, s_w[i]) : wexcl;
+        tot = sat_add(tot, s_w[i]);
+    }
+
+    // 2. the sum over the unit's earlier tiles: look-back
+    if (w == 0) {
+        unsigned long long* st = status + U.dt_begin;
+        unsigned long long excl = 0;
+        if (t == 0) {
+            if (l == 0) st_rlx(st, kFlagIncl | tot);
+        } else {
+            if (l == 0) st_rlx(st + t, kFlagAgg | tot);
+            excl = lookback_sum62(st, (int64_t)t, l, err);
+            excl = excl > 0xffffffffull ? 0xffffffffull : excl;
+            if (l == 0) st_rlx(st + t, kFlagIncl | (unsigned long long)sat_add((uint32_t)excl, tot));
+        }
+        if (l == 0) s_x[1] = (uint32_t)excl;
+    }
+    __syncthreads();
+    const uint32_t nc = (uint32_t)U.ncells;
+    const uint32_t A = sat_add(s_x[1], wexcl);
+
+    // 3. row entries.  Per pair k < n: S = p_k + 1 (saturating), x = run + 1,
+    // previous position + 1 = S - x; the virtual pair k == n: S = p_{n-1} + 1
+    // and position ncoeff.  Positions clamp to ncoeff: when S saturates, S - x
+    // >= 2^31 > ncoeff too, so the clamped rows are exact.
+    uint2* __restrict__ ri = rowinfo + U.row_off;
+    const uint32_t D = (uint32_t)U.nz;
+#pragma unroll
+    for (int r = 0; r < kDecRounds; ++r) {
+        const uint32_t k = kw + r * 64 + l;
+        const uint32_t S = sat_add(A, v[r]);
+        uint32_t rlo = 0, cnt = 0, ph = 0;
+        if (k <= n) {
+            uint32_t pl1;  // previous position + 1, in [0, ncoeff + 1]
+            if (k < n) {
+                ph = min(S - 1u, nc);
+                pl1 = min(S - x[r], nc + 1u);
+            } else {
+                ph = nc;
+                pl1 = min(S, nc + 1u);
+            }
+            rlo = pl1 == 0 ? 0u : div_rows(pl1 - 1u, U.dmagic) + 1u;
+            const uint32_t rhi = div_rows(ph, U.dmagic);
+            cnt = rhi >= rlo ? rhi - rlo + 1u : 0u;
+        }
+        write_rows(ri, rlo, cnt, k, ph, D, l);
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void k_decode(const UnitDev* __restrict__ units,
@@ -105,7 +286,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(const UnitDev* __restrict__
 
     // 2. start of this tile's range: look-back over the unit's earlier tiles
     if (w == 0) {
-        unsigned long long* st = status + U.ftile_begin;
+        unsigned long long* st = status + U.dt_begin;
         unsigned long long excl = 0;
         if (t == 0) {
             if (l == 0) st_rlx(st, kFlagIncl | (tot & kMask62));
@@ -152,6 +333,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(const UnitDev* __restrict__
         __syncthreads();
     }
 }
+
 
 // ---------------------------------------------------------------------------
 // K6: inverse transform over the same 2x2x2-block tiles as K1.
@@ -375,6 +557,274 @@ __global__ __launch_bounds__(kThreads) void k_inverse_fast(const float* __restri
 }
 
 // ---------------------------------------------------------------------------
+// K6r: inverse of a row-indexed unit straight from its payload.  A tile is
+// TX x TY blocks in (x, y) and all of z; its coefficients are the 4 TX
+// "ranges" g = (ssx * 2 + ssy) * TX + bxl: I = bx0 + bxl + ssx * hx, flat rows
+// I*H + J for J in [by0, by0 + TY) + ssy * hy — TY*D consecutive flat
+// coefficients (x slowest, z fastest: src/compressor.cpp:178-181), so one
+// contiguous run of pairs, rowinfo[r0].x .. rowinfo[r0 + TY].x - 1, whose
+// first pair lands at rowinfo[r0].y within the range.
+//
+// Wave w owns the ranges g = w + 4j (lane j holds range j's row entries; every
+// sub-band class in every wave) and an LDS region of its own: it zeroes the
+// region, concatenates its ranges' pair runs (a wave scan of the run lengths
+// gives range j's first list index off_j) and walks the list 64 pairs per
+// round.  LDS address of pair i in range j: slot_j + c_j + S_i - S(first_j),
+// S = the inclusive scan of run + 1 over the list (one DPP scan per round);
+// the range of each lane comes from a uniform loop over the range starts that
+// fall in the round (a few per round: SGPR reads, no LDS).  Then one block
+// barrier, and X, Y, Z synthesis per 2x2x2 block (src/decompressor.cpp:89-156)
+// from float4 sub-band reads (4 z-blocks per thread) with 8-B x-pair stores.
+//
+// Persistent: workgroup b runs tiles b, b + G, ...  The latency of the
+// dependent loads (tile record -> row entries + payload offset -> pairs) is
+// hidden by a two-stage prefetch: while tile t is synthesised, the pairs of
+// tile t + G are in flight (up to kRixRounds rounds; more are loaded when
+// scattered) and the row entries of tile t + 2G.
+//
+// The row index of a unit is complete and monotone whatever the payload
+// (k_rowindex), negative runs count as 0 as there, and every LDS address is
+// checked against the wave's region: a malformed payload (reported by K5)
+// gives garbage cells, never an out-of-bounds access.
+constexpr int kRixRounds = 16;  // rounds of 64 pairs prefetched per wave
+
+// Range info of this lane (range g = w + 4l of tile T, lanes l < TX).
+struct RixRange {
+    uint32_t ks, c0, e;  // rowinfo[r0] = (ks, c0), rowinfo[r0 + tyv].x = e
+};
+
+__device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* __restrict__ rowinfo, int w, int l) {
+    RixRange R{0u, 0u, 0u};
+    const int TX = 1 << T.lbx;
+    if (l < TX) {
+        const int g = w + 4 * l, bxl = g & (TX - 1), ssy = (g >> T.lbx) & 1, ssx = g >> (T.lbx + 1);
+        const int bx = T.bx0 + bxl, hx = T.W >> 1, hy = T.H >> 1;
+        if (bx < hx) {
+            const uint64_t r0 = (uint64_t)(bx + ssx * hx) * T.H + T.by0 + ssy * hy;
+            const uint2 a = rowinfo[T.row_off + r0];
+            R.ks = a.x;
+            R.c0 = a.y;
+            R.e = rowinfo[T.row_off + r0 + T.tyv].x;
+        }
+    }
+    return R;
+}
+
+// Lane j's range: list offset (exclusive scan of the run lengths) and the
+// wave's pair count P.
+__device__ __forceinline__ uint32_t rix_offsets(const RTile& T, const RixRange& R, uint32_t& P) {
+    const uint32_t rlen = (uint32_t)(T.tyv * T.D);
+    const uint32_t cnt = R.e > R.ks ? min(R.e - R.ks, rlen) : 0u;
+    const uint32_t incl = wave_incl_sum32(cnt);
+    P = __builtin_amdgcn_readlane(incl, 63);
+    return incl - cnt;
+}
+
+// Payload index base (k - i) of list index i = rb + l: the latest range start
+// <= i.  jn: first range whose start is >= rb (advanced past the round).
+__device__ __forceinline__ uint32_t rix_kbase(uint32_t off, uint32_t ks, uint32_t P, int nr, uint32_t rb, int l,
+                                              int& jn) {
+    const uint32_t i = rb + (uint32_t)l;
+    const int jp = jn > 0 ? jn - 1 : 0;
+    uint32_t kb = (uint32_t)__builtin_amdgcn_readlane(ks, jp) - (uint32_t)__builtin_amdgcn_readlane(off, jp);
+    while (jn < nr) {
+        const uint32_t oj = __builtin_amdgcn_readlane(off, jn);
+        if (oj >= rb + 64 || oj >= P) break;
+        if (i >= oj) kb = (uint32_t)__builtin_amdgcn_readlane(ks, jn) - oj;
+        ++jn;
+    }
+    return kb;
+}
+
+__device__ __forceinline__ uint2 rix_load_pair(const uint2* __restrict__ pr, uint32_t off, uint32_t ks, uint32_t P,
+                                               int nr, uint32_t rb, int l, int& jn) {
+    const uint32_t kb = rix_kbase(off, ks, P, nr, rb, l, jn);
+    const uint32_t i = rb + (uint32_t)l;
+    return i < P ? pr[kb + i] : make_uint2(0u, 0u);
+}
+
+// Scatter one round (list indices rb + l) into the wave's LDS region.
+// carry: scan value before the round; flast: F (slot + c - S(first)) of the
+// latest range started before the round (uniform); jn as in rix_kbase.
+__device__ __forceinline__ void rix_scatter_round(float* __restrict__ reg, uint32_t regn, int RS, uint2 q, uint32_t off,
+                                                  uint32_t c0, uint32_t P, int nr, uint32_t rb, int l, int& jn,
+                                                  uint32_t& carry, uint32_t& flast) {
+    const uint32_t i = rb + (uint32_t)l;
+    const int32_t run = (int32_t)q.x;
+    const uint32_t x = i < P ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
+    const uint32_t S = carry + wave_incl_sum32(x);
+    carry = __builtin_amdgcn_readlane(S, 63);
+    uint32_t fl = flast;
+    while (jn < nr) {
+        const uint32_t oj = __builtin_amdgcn_readlane(off, jn);
+        if (oj >= rb + 64 || oj >= P) break;
+        const uint32_t f = (uint32_t)(jn * RS) + (uint32_t)__builtin_amdgcn_readlane(c0, jn) -
+                           (uint32_t)__builtin_amdgcn_readlane(S, (int)(oj - rb));
+        if (i >= oj) fl = f;
+        flast = f;
+        ++jn;
+    }
+    const uint32_t A = S + fl;
+    if (i < P && A < regn) reg[A] = __uint_as_float(q.y);
+}
+
+__global__ __launch_bounds__(kThreads) void k_inverse_rows(const RTile* __restrict__ tiles, uint32_t ntiles,
+                                                         const uint8_t* __restrict__ payload,
+                                                         const uint64_t* __restrict__ offsets,
+                                                         const uint2* __restrict__ rowinfo, float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const uint32_t G = gridDim.x;
+    uint32_t t = blockIdx.x;
+    if (t >= ntiles) return;
+
+    // prologue: tile t's ranges and pairs in flight, tile t + G's row entries
+    RTile T = tiles[t];
+    const uint2* pr = reinterpret_cast<const uint2*>(payload + offsets[T.unit] + 20);
+    RixRange R = rix_load_range(T, rowinfo, w, l);
+    uint32_t P;
+    uint32_t off = rix_offsets(T, R, P);
+    uint2 q[kRixRounds];
+    {
+        int jn = 0;
+#pragma unroll
+        for (int r = 0; r < kRixRounds; ++r) q[r] = rix_load_pair(pr, off, R.ks, P, 1 << T.lbx, r * 64, l, jn);
+    }
+    uint32_t t1 = t + G;
+    RTile T1 = T;
+    RixRange R1{0u, 0u, 0u};
+    const uint2* pr1 = pr;
+    if (t1 < ntiles) {
+        T1 = tiles[t1];
+        pr1 = reinterpret_cast<const uint2*>(payload + offsets[T1.unit] + 20);
+        R1 = rix_load_range(T1, rowinfo, w, l);
+    }
+
+    for (;;) {
+        const int TX = 1 << T.lbx, RS = rix_rs(T.lby, T.D), nr = TX;
+        const int WR = rix_wr(T.lbx, T.lby, T.D);
+        const uint32_t regn = (uint32_t)(TX * RS);
+        float* reg = lds + w * WR;
+        // 1. zero the wave's region, scatter its pairs
+        {
+            float4* r4 = reinterpret_cast<float4*>(reg);
+            for (uint32_t i = l; i < regn / 4; i += 64) r4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            uint32_t carry = 0, fl = 0;
+            int jn = 0;
+#pragma unroll
+            for (int r = 0; r < kRixRounds; ++r)
+                if ((uint32_t)(r * 64) < P)
+                    rix_scatter_round(reg, regn, RS, q[r], off, R.c0, P, nr, r * 64, l, jn, carry, fl);
+            // rounds past the prefetch window (dense tiles): load and scatter.
+            // Load-side cursor: the first range starting at or after the window.
+            int jl = __popcll(__ballot(l < nr && off < (uint32_t)(kRixRounds * 64) && off < P));
+            for (uint32_t rb = kRixRounds * 64; rb < P; rb += 64) {
+                const uint2 qq = rix_load_pair(pr, off, R.ks, P, nr, rb, l, jl);
+                rix_scatter_round(reg, regn, RS, qq, off, R.c0, P, nr, rb, l, jn, carry, fl);
+            }
+        }
+        __syncthreads();
+
+        // 2. prefetch: tile t1's pairs, tile t2's row entries
+        const uint32_t t2 = t1 + G;
+        RTile T2 = T1;
+        RixRange R2{0u, 0u, 0u};
+        const uint2* pr2 = pr1;
+        uint32_t P1 = 0, off1 = 0;
+        if (t1 < ntiles) {
+            off1 = rix_offsets(T1, R1, P1);
+            int jn = 0;
+#pragma unroll
+            for (int r = 0; r < kRixRounds; ++r) q[r] = rix_load_pair(pr1, off1, R1.ks, P1, 1 << T1.lbx, r * 64, l, jn);
+            if (t2 < ntiles) {
+                T2 = tiles[t2];
+                pr2 = reinterpret_cast<const uint2*>(payload + offsets[T2.unit] + 20);
+                R2 = rix_load_range(T2, rowinfo, w, l);
+            }
+        }
+
+        // 3. synthesis of tile t
+        {
+            const int lbx = T.lbx, TYv = T.tyv;
+            const int W = T.W, H = T.H, D = T.D, hx = W >> 1, hz = D >> 1;
+            float* __restrict__ dst = out + T.cell_off;
+            const int64_t sy = W, sz = (int64_t)W * H;
+            const bool vout = (T.cell_off & 1) == 0;
+            const int ncol = TX * TYv * (hz >> 2);
+            for (int ci = tid; ci < ncol; ci += kThreads) {
+                const int bxl = ci & (TX - 1), rest = ci >> lbx;
+                const int byl = rest % TYv, bq = rest / TYv;
+                const int bx = T.bx0 + bxl, by = T.by0 + byl, bzb = 4 * bq;
+                if (bx >= hx) continue;
+                float c[2][2][2][4];  // [sz][sy][sx][z-block]
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                    for (int t3 = 0; t3 < 2; ++t3)
+#pragma unroll
+                        for (int x = 0; x < 2; ++x) {
+                            const int g = ((x * 2 + t3) << lbx) + bxl;
+                            const float4 v4 = *reinterpret_cast<const float4*>(lds + (g & 3) * WR + (g >> 2) * RS +
+                                                                               byl * D + s2 * hz + bzb);
+                            c[s2][t3][x][0] = v4.x;
+                            c[s2][t3][x][1] = v4.y;
+                            c[s2][t3][x][2] = v4.z;
+                            c[s2][t3][x][3] = v4.w;
+                        }
+#pragma unroll
+                for (int qb = 0; qb < 4; ++qb) {
+                    float X[2][2][2], Y[2][2][2], V[2][2][2];
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                        for (int t3 = 0; t3 < 2; ++t3) {
+                            X[s2][t3][0] = c[s2][t3][0][qb] + c[s2][t3][1][qb];
+                            X[s2][t3][1] = c[s2][t3][0][qb] - c[s2][t3][1][qb];
+                        }
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                        for (int x = 0; x < 2; ++x) {
+                            Y[s2][0][x] = X[s2][0][x] + X[s2][1][x];
+                            Y[s2][1][x] = X[s2][0][x] - X[s2][1][x];
+                        }
+#pragma unroll
+                    for (int t3 = 0; t3 < 2; ++t3)
+#pragma unroll
+                        for (int x = 0; x < 2; ++x) {
+                            V[0][t3][x] = Y[0][t3][x] + Y[1][t3][x];
+                            V[1][t3][x] = Y[0][t3][x] - Y[1][t3][x];
+                        }
+#pragma unroll
+                    for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+                        for (int dy = 0; dy < 2; ++dy) {
+                            float* p = dst + 2 * (int64_t)bx + sy * (2 * by + dy) + sz * (2 * (bzb + qb) + dz);
+                            if (vout) {
+                                *reinterpret_cast<float2*>(p) = make_float2(V[dz][dy][0], V[dz][dy][1]);
+                            } else {
+                                p[0] = V[dz][dy][0];
+                                p[1] = V[dz][dy][1];
+                            }
+                        }
+                }
+            }
+        }
+        __syncthreads();
+        if (t1 >= ntiles) break;
+        T = T1;
+        pr = pr1;
+        R = R1;
+        off = off1;
+        P = P1;
+        t1 = t2;
+        T1 = T2;
+        pr1 = pr2;
+        R1 = R2;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K7: RMSE.  Partial sums per flat tile (cell order), then a fixed-order
 // per-unit reduction so the result is reproducible run to run.
 template <typename T>
@@ -419,10 +869,12 @@ __global__ __launch_bounds__(64) void k_rmse_final(const UnitDev* __restrict__ u
 // ---------------------------------------------------------------------------
 // Launch wrappers
 hipError_t launch_decode(hipStream_t st, const UnitDev* units, const FTile* ftiles, uint32_t nft,
-                         const uint8_t* payload, const uint64_t* offsets, uint32_t* ticket,
-                         unsigned long long* status, float* flat, uint32_t* err, int ordered) {
-    if (nft == 0) return hipSuccess;
-    k_decode<<<nft, kThreads, 0, st>>>(units, ftiles, payload, offsets, ticket, status, flat, err, ordered);
+                         const FTile* rtiles, uint32_t nrt, const uint8_t* payload, const uint64_t* offsets,
+                         uint32_t* ticket, unsigned long long* status, float* flat, uint2* rowinfo, uint32_t* err,
+                         int ordered) {
+    if (nrt)
+        k_rowindex<<<nrt, kThreads, 0, st>>>(units, rtiles, payload, offsets, ticket, status, rowinfo, err, ordered);
+    if (nft) k_decode<<<nft, kThreads, 0, st>>>(units, ftiles, payload, offsets, ticket, status, flat, err, ordered);
     return hipGetLastError();
 }
 
@@ -433,6 +885,33 @@ hipError_t launch_inverse(hipStream_t st, const float* flat, int flat_at_cell_of
                           float* out) {
     if (ngen) k_inverse<<<ngen, kThreads, lds_gen, st>>>(flat, flat_at_cell_off, units, tiles, out);
     if (nfast) k_inverse_fast<<<nfast, kThreads, lds_fast, st>>>(flat, flat_at_cell_off, units, tiles + ngen, out);
+    return hipGetLastError();
+}
+
+// Workgroups of k_inverse_rows resident at once for `lds` bytes (persistent grid).
+static uint32_t rows_grid(size_t lds) {
+    static size_t cached_lds = 0;
+    static uint32_t cached = 0;
+    if (cached_lds != lds || !cached) {
+        int per_cu = 0, ncu = 0, dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_inverse_rows, kThreads, lds) !=
+                hipSuccess ||
+            per_cu < 1)
+            per_cu = 1;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
+            ncu = 256;
+        cached = (uint32_t)per_cu * (uint32_t)ncu;
+        cached_lds = lds;
+    }
+    return cached;
+}
+
+hipError_t launch_inverse_rows(hipStream_t st, const RTile* tiles, uint32_t ntiles, size_t lds, const uint8_t* payload,
+                               const uint64_t* offsets, const uint2* rowinfo, float* out) {
+    if (!ntiles) return hipSuccess;
+    const uint32_t grid = std::min(ntiles, rows_grid(lds));
+    k_inverse_rows<<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out);
     return hipGetLastError();
 }
 
