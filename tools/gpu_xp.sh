@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B of diagnostic libwavelet_amd.so variants (tools/build_variants.sh) on the inverse
-A="1024 64 f64 0.999 20 3 1 0 1 1 1"
-for v in default nostore nopairs neither default; do
+for A in "1024 64 f64 0.999 20 3 1 0 1 1 1" "64 128 f32 0.9999 20 3 1 0 1 1 1"; do
+for v in default bare nostore nopairs bare_noc bare_nosc r24; do
   if [ $v = default ]; then lp=""; else lp="tools/variants/$v"; fi
-  echo "$v: $(LD_LIBRARY_PATH=$lp timeout -k 5 60 tools/bin/wc_bench $A | grep -o '"inverse_stage_ms": {.*}')"
+  echo "$A $v: $(LD_LIBRARY_PATH=$lp timeout -k 5 60 tools/bin/wc_bench $A | grep -o '"inverse_stage_ms": {.*}')"
+done
 done

@@ -270,7 +270,8 @@ void build_etiles(Plan& P, int n) {
 
 // K6r tiling (wc_inverse.hip k_inverse_rows): TX x TY blocks in (x, y), all of
 // z; the tile's LDS is 4 TX ranges of TY*D + 4 floats, at most kRixLds.  TX
-// up to 32 blocks (64-cell output rows), then TY as large as fits.  Units of
+// up to 16 blocks (32-cell = 128-B output rows), then TY as large as fits
+// (fewer, longer ranges per wave).  Units of
 // the fast shape only (even W and H, D % 8 == 0: no odd tails, float4
 // sub-band reads); the others decode densely.
 size_t rix_lds_bytes(const UnitDev& d) { return sizeof(float) * 4 * (size_t)rix_wr(d.ilbx, d.ilby, d.nz); }
@@ -279,7 +280,7 @@ bool set_rix_tiling(UnitDev& d) {
     d.rix = 0;
     if (!d.fast || d.ncells == 0) return false;
     auto floats = [&](int tx, int ty) { return (int64_t)4 * (tx * ((int64_t)ty * d.nz + 4) + 16); };
-    int lx = std::min(5, ceil_log2(d.hx));
+    int lx = std::min(4, ceil_log2(d.hx));  // 16 blocks: 128-B output rows; the rest of the budget to TY
     while (lx > 0 && floats(1 << lx, 1) > kRixLds) --lx;
     if (floats(1 << lx, 1) > kRixLds) return false;
     int ly = 0;

@@ -566,27 +566,30 @@ __global__ __launch_bounds__(kThreads) void k_inverse_fast(const float* __restri
 // first pair lands at rowinfo[r0].y within the range.
 //
 // Wave w owns the ranges g = w + 4j (lane j holds range j's row entries; every
-// sub-band class in every wave) and an LDS region of its own: it zeroes the
-// region, concatenates its ranges' pair runs (a wave scan of the run lengths
-// gives range j's first list index off_j) and walks the list 64 pairs per
-// round.  LDS address of pair i in range j: slot_j + c_j + S_i - S(first_j),
-// S = the inclusive scan of run + 1 over the list (one DPP scan per round);
-// the range of each lane comes from a uniform loop over the range starts that
-// fall in the round (a few per round: SGPR reads, no LDS).  Then one block
-// barrier, and X, Y, Z synthesis per 2x2x2 block (src/decompressor.cpp:89-156)
-// from float4 sub-band reads (4 z-blocks per thread) with 8-B x-pair stores.
+// sub-band class in every wave) and an LDS region of its own.  It zeroes the
+// region and walks its ranges one at a time, 64 pairs per round: round rr
+// belongs to range j = (number of ranges whose rounds end at or before rr) — a
+// ballot and a popcount, uniform — and lane l holds pair m*64 + l of it.
+// Position in the range = first + (inclusive DPP scan of run + 1 over the
+// range's pairs after its first); the value is dropped into LDS.  Then one
+// block barrier, and X, Y, Z synthesis per 2x2x2 block
+// (src/decompressor.cpp:89-156) from float4 sub-band reads (4 z-blocks per
+// thread) with 8-B x-pair stores.
 //
 // Persistent: workgroup b runs tiles b, b + G, ...  The latency of the
 // dependent loads (tile record -> row entries + payload offset -> pairs) is
 // hidden by a two-stage prefetch: while tile t is synthesised, the pairs of
-// tile t + G are in flight (up to kRixRounds rounds; more are loaded when
-// scattered) and the row entries of tile t + 2G.
+// tile t + G are in flight (the first kRixRounds rounds; the rest are loaded
+// when scattered) and the row entries of tile t + 2G.
 //
 // The row index of a unit is complete and monotone whatever the payload
 // (k_rowindex), negative runs count as 0 as there, and every LDS address is
-// checked against the wave's region: a malformed payload (reported by K5)
-// gives garbage cells, never an out-of-bounds access.
-constexpr int kRixRounds = 16;  // rounds of 64 pairs prefetched per wave
+// checked against the range: a malformed payload (reported by K5) gives
+// garbage cells, never an out-of-bounds access.
+#ifndef WC_RIX_ROUNDS
+#define WC_RIX_ROUNDS 24  // 120 VGPRs: still 4 waves per SIMD
+#endif
+constexpr int kRixRounds = WC_RIX_ROUNDS;  // rounds of 64 pairs prefetched per wave
 
 // Range info of this lane (range g = w + 4l of tile T, lanes l < TX).
 struct RixRange {
@@ -610,62 +613,65 @@ __device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* 
     return R;
 }
 
-// Lane j's range: list offset (exclusive scan of the run lengths) and the
-// wave's pair count P.
-__device__ __forceinline__ uint32_t rix_offsets(const RTile& T, const RixRange& R, uint32_t& P) {
+// Per-lane range plan of a wave: pair count, and the inclusive prefix of the
+// ranges' round counts (rin; rounds of range j are [rin_j - rounds_j, rin_j)).
+struct RixPlan {
+    uint32_t cnt, rin, nrounds;
+};
+
+__device__ __forceinline__ RixPlan rix_plan(const RTile& T, const RixRange& R, int l) {
     const uint32_t rlen = (uint32_t)(T.tyv * T.D);
-    const uint32_t cnt = R.e > R.ks ? min(R.e - R.ks, rlen) : 0u;
-    const uint32_t incl = wave_incl_sum32(cnt);
-    P = __builtin_amdgcn_readlane(incl, 63);
-    return incl - cnt;
+    RixPlan p;
+    p.cnt = (l < (1 << T.lbx) && R.e > R.ks) ? min(R.e - R.ks, rlen) : 0u;
+    const uint32_t rounds = (p.cnt + 63) >> 6;
+    p.rin = wave_incl_sum32(rounds);
+    p.nrounds = __builtin_amdgcn_readlane(p.rin, 63);
+    return p;
 }
 
-// Payload index base (k - i) of list index i = rb + l: the latest range start
-// <= i.  jn: first range whose start is >= rb (advanced past the round).
-__device__ __forceinline__ uint32_t rix_kbase(uint32_t off, uint32_t ks, uint32_t P, int nr, uint32_t rb, int l,
-                                              int& jn) {
-    const uint32_t i = rb + (uint32_t)l;
-    const int jp = jn > 0 ? jn - 1 : 0;
-    uint32_t kb = (uint32_t)__builtin_amdgcn_readlane(ks, jp) - (uint32_t)__builtin_amdgcn_readlane(off, jp);
-    while (jn < nr) {
-        const uint32_t oj = __builtin_amdgcn_readlane(off, jn);
-        if (oj >= rb + 64 || oj >= P) break;
-        if (i >= oj) kb = (uint32_t)__builtin_amdgcn_readlane(ks, jn) - oj;
-        ++jn;
-    }
-    return kb;
+// Range j and round m within it of wave round rr (uniform).
+__device__ __forceinline__ void rix_round(const RixPlan& p, int l, uint32_t rr, int& j, uint32_t& m) {
+    (void)l;
+    j = __popcll(__ballot(p.rin <= rr));  // ranges whose rounds all come before rr
+    const uint32_t rin = __builtin_amdgcn_readlane(p.rin, j);
+    const uint32_t cnt = __builtin_amdgcn_readlane(p.cnt, j);
+    m = rr - (rin - ((cnt + 63) >> 6));
 }
 
-__device__ __forceinline__ uint2 rix_load_pair(const uint2* __restrict__ pr, uint32_t off, uint32_t ks, uint32_t P,
-                                               int nr, uint32_t rb, int l, int& jn) {
-    const uint32_t kb = rix_kbase(off, ks, P, nr, rb, l, jn);
-    const uint32_t i = rb + (uint32_t)l;
-    return i < P ? pr[kb + i] : make_uint2(0u, 0u);
+__device__ __forceinline__ uint2 rix_load_round(const uint2* __restrict__ pr, const RixRange& R, const RixPlan& p,
+                                                int l, uint32_t rr) {
+    int j;
+    uint32_t m;
+    rix_round(p, l, rr, j, m);
+    const uint32_t i = m * 64 + (uint32_t)l;
+    const uint32_t cnt = __builtin_amdgcn_readlane(p.cnt, j);
+    const uint32_t ks = __builtin_amdgcn_readlane(R.ks, j);
+#ifdef WC_XP_NOPAIRS
+    return make_uint2(i & 1, ks);
+#endif
+    return i < cnt ? pr[ks + i] : make_uint2(0u, 0u);
 }
 
-// Scatter one round (list indices rb + l) into the wave's LDS region.
-// carry: scan value before the round; flast: F (slot + c - S(first)) of the
-// latest range started before the round (uniform); jn as in rix_kbase.
-__device__ __forceinline__ void rix_scatter_round(float* __restrict__ reg, uint32_t regn, int RS, uint2 q, uint32_t off,
-                                                  uint32_t c0, uint32_t P, int nr, uint32_t rb, int l, int& jn,
-                                                  uint32_t& carry, uint32_t& flast) {
-    const uint32_t i = rb + (uint32_t)l;
+// Scatter wave round rr into the wave's LDS region; carry: the scan through
+// the previous round of the same range (uniform).
+__device__ __forceinline__ void rix_scatter_round(float* __restrict__ reg, int RS, uint32_t rlen, uint2 q,
+                                                  const RixRange& R, const RixPlan& p, int l, uint32_t rr,
+                                                  uint32_t& carry) {
+    int j;
+    uint32_t m;
+    rix_round(p, l, rr, j, m);
+    const uint32_t i = m * 64 + (uint32_t)l;
+    const uint32_t cnt = __builtin_amdgcn_readlane(p.cnt, j);
     const int32_t run = (int32_t)q.x;
-    const uint32_t x = i < P ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
+    const uint32_t x = (i < cnt && i > 0) ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
+    if (m == 0) carry = 0;
     const uint32_t S = carry + wave_incl_sum32(x);
     carry = __builtin_amdgcn_readlane(S, 63);
-    uint32_t fl = flast;
-    while (jn < nr) {
-        const uint32_t oj = __builtin_amdgcn_readlane(off, jn);
-        if (oj >= rb + 64 || oj >= P) break;
-        const uint32_t f = (uint32_t)(jn * RS) + (uint32_t)__builtin_amdgcn_readlane(c0, jn) -
-                           (uint32_t)__builtin_amdgcn_readlane(S, (int)(oj - rb));
-        if (i >= oj) fl = f;
-        flast = f;
-        ++jn;
-    }
-    const uint32_t A = S + fl;
-    if (i < P && A < regn) reg[A] = __uint_as_float(q.y);
+    const uint32_t pos = (uint32_t)__builtin_amdgcn_readlane(R.c0, j) + S;
+#ifdef WC_XP_NOSCATTER
+    if (q.y == 0x12345u)
+#endif
+    if (i < cnt && pos < rlen) reg[j * RS + pos] = __uint_as_float(q.y);
 }
 
 __global__ __launch_bounds__(kThreads) void k_inverse_rows(const RTile* __restrict__ tiles, uint32_t ntiles,
@@ -682,14 +688,11 @@ __global__ __launch_bounds__(kThreads) void k_inverse_rows(const RTile* __restri
     RTile T = tiles[t];
     const uint2* pr = reinterpret_cast<const uint2*>(payload + offsets[T.unit] + 20);
     RixRange R = rix_load_range(T, rowinfo, w, l);
-    uint32_t P;
-    uint32_t off = rix_offsets(T, R, P);
+    RixPlan PL = rix_plan(T, R, l);
     uint2 q[kRixRounds];
-    {
-        int jn = 0;
 #pragma unroll
-        for (int r = 0; r < kRixRounds; ++r) q[r] = rix_load_pair(pr, off, R.ks, P, 1 << T.lbx, r * 64, l, jn);
-    }
+    for (int r = 0; r < kRixRounds; ++r)
+        if ((uint32_t)r < PL.nrounds) q[r] = rix_load_round(pr, R, PL, l, r);
     uint32_t t1 = t + G;
     RTile T1 = T;
     RixRange R1{0u, 0u, 0u};
@@ -701,27 +704,26 @@ __global__ __launch_bounds__(kThreads) void k_inverse_rows(const RTile* __restri
     }
 
     for (;;) {
-        const int TX = 1 << T.lbx, RS = rix_rs(T.lby, T.D), nr = TX;
+        const int TX = 1 << T.lbx, RS = rix_rs(T.lby, T.D);
         const int WR = rix_wr(T.lbx, T.lby, T.D);
-        const uint32_t regn = (uint32_t)(TX * RS);
+        const uint32_t rlen = (uint32_t)(T.tyv * T.D);
         float* reg = lds + w * WR;
         // 1. zero the wave's region, scatter its pairs
         {
             float4* r4 = reinterpret_cast<float4*>(reg);
-            for (uint32_t i = l; i < regn / 4; i += 64) r4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-            uint32_t carry = 0, fl = 0;
-            int jn = 0;
+            const uint32_t n4 = (uint32_t)(TX * RS) >> 2;
+            for (uint32_t i = l; i < n4; i += 64) r4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            uint32_t carry = 0;
+#ifndef WC_XP_NOSCANS
 #pragma unroll
             for (int r = 0; r < kRixRounds; ++r)
-                if ((uint32_t)(r * 64) < P)
-                    rix_scatter_round(reg, regn, RS, q[r], off, R.c0, P, nr, r * 64, l, jn, carry, fl);
-            // rounds past the prefetch window (dense tiles): load and scatter.
-            // Load-side cursor: the first range starting at or after the window.
-            int jl = __popcll(__ballot(l < nr && off < (uint32_t)(kRixRounds * 64) && off < P));
-            for (uint32_t rb = kRixRounds * 64; rb < P; rb += 64) {
-                const uint2 qq = rix_load_pair(pr, off, R.ks, P, nr, rb, l, jl);
-                rix_scatter_round(reg, regn, RS, qq, off, R.c0, P, nr, rb, l, jn, carry, fl);
-            }
+                if ((uint32_t)r < PL.nrounds) rix_scatter_round(reg, RS, rlen, q[r], R, PL, l, r, carry);
+            // rounds past the prefetch window (dense tiles): load and scatter
+            for (uint32_t rr = kRixRounds; rr < PL.nrounds; ++rr)
+                rix_scatter_round(reg, RS, rlen, rix_load_round(pr, R, PL, l, rr), R, PL, l, rr, carry);
+#else
+            if (q[0].x == 77u && q[5].y == 3u) reg[0] = 1.0f;
+#endif
         }
         __syncthreads();
 
@@ -730,12 +732,12 @@ __global__ __launch_bounds__(kThreads) void k_inverse_rows(const RTile* __restri
         RTile T2 = T1;
         RixRange R2{0u, 0u, 0u};
         const uint2* pr2 = pr1;
-        uint32_t P1 = 0, off1 = 0;
+        RixPlan PL1{0u, 0u, 0u};
         if (t1 < ntiles) {
-            off1 = rix_offsets(T1, R1, P1);
-            int jn = 0;
+            PL1 = rix_plan(T1, R1, l);
 #pragma unroll
-            for (int r = 0; r < kRixRounds; ++r) q[r] = rix_load_pair(pr1, off1, R1.ks, P1, 1 << T1.lbx, r * 64, l, jn);
+            for (int r = 0; r < kRixRounds; ++r)
+                if ((uint32_t)r < PL1.nrounds) q[r] = rix_load_round(pr1, R1, PL1, l, r);
             if (t2 < ntiles) {
                 T2 = tiles[t2];
                 pr2 = reinterpret_cast<const uint2*>(payload + offsets[T2.unit] + 20);
@@ -751,6 +753,9 @@ __global__ __launch_bounds__(kThreads) void k_inverse_rows(const RTile* __restri
             const int64_t sy = W, sz = (int64_t)W * H;
             const bool vout = (T.cell_off & 1) == 0;
             const int ncol = TX * TYv * (hz >> 2);
+#ifdef WC_XP_NOPHASEC
+            if (tid < 0)
+#endif
             for (int ci = tid; ci < ncol; ci += kThreads) {
                 const int bxl = ci & (TX - 1), rest = ci >> lbx;
                 const int byl = rest % TYv, bq = rest / TYv;
@@ -800,6 +805,9 @@ __global__ __launch_bounds__(kThreads) void k_inverse_rows(const RTile* __restri
 #pragma unroll
                         for (int dy = 0; dy < 2; ++dy) {
                             float* p = dst + 2 * (int64_t)bx + sy * (2 * by + dy) + sz * (2 * (bzb + qb) + dz);
+#ifdef WC_XP_NOSTORE
+                            if (V[dz][dy][0] == 1.2345f)
+#endif
                             if (vout) {
                                 *reinterpret_cast<float2*>(p) = make_float2(V[dz][dy][0], V[dz][dy][1]);
                             } else {
@@ -815,8 +823,7 @@ __global__ __launch_bounds__(kThreads) void k_inverse_rows(const RTile* __restri
         T = T1;
         pr = pr1;
         R = R1;
-        off = off1;
-        P = P1;
+        PL = PL1;
         t1 = t2;
         T1 = T2;
         pr1 = pr2;
