@@ -177,6 +177,16 @@ def special_boxes():
     out["denormal_f"] = (b, None)
     b = np.full((16, 8, 8), 1.0, np.float32); b[9, 7, 6] = -50.0
     out["neg_max_f"] = (b, None)
+    # negative signed max on sparse-staged shapes (D >= 32, hz % TZ == 0): thresh < 0
+    # keeps every coefficient, including the segments the sparse staging skipped
+    # (a lone negative spike: its block's 8 coefficients tie in |c|, the first in flat
+    # order -- the negative low-pass one -- is the signed max)
+    b = np.zeros((32, 16, 16), np.float32); b[9, 7, 6] = -50.0
+    out["neg_max_sparse"] = (b, 32 * 16 * 16)
+    rng = np.random.default_rng(5)
+    b = (rng.standard_normal((64, 32, 32)) * 0.01).astype(np.float32)
+    b[40:42, 2:4, 16:18] = 0.0; b[40, 3, 17] = -900.0
+    out["neg_max_sparse_tiles"] = (b, 64 * 32 * 32)
     return out
 
 

@@ -1,7 +1,5 @@
 #!/bin/bash
-# SQ counters of the inverse kernels (one --pmc pass each, own time limit)
-W="1024 64 f64 0.999 3 1 1 1 1 1 1"
+# SQ counters of the forward and inverse kernels on C2 (one --pmc pass each, own time limit)
+W="1024 64 f64 0.999 3 1 1"
 exec tools/gpu_run.sh \
- "list:60:rocprofv3 -L > gpurun_out/counters_list.txt 2>&1" \
- "sq1:90:timeout -s KILL 80 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES --output-format csv -d gpurun_out/sq1 -o sq1 -- tools/bin/wc_bench $W" \
- "kt:90:rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt -o kt -- tools/bin/wc_bench $W"
+ "sqc:90:timeout -s KILL 80 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CU_CYCLES SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d gpurun_out/sqc -o sqc -- tools/bin/wc_bench $W"

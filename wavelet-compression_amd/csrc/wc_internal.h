@@ -106,7 +106,7 @@ struct EmitParams {
     const uint8_t* flags;          // sparse-staging segment flags (null: every unit dense)
 };
 
-constexpr int kSegShift = 4;
-constexpr int kRixLds = 9216;  // K6r tile: at most this many floats of LDS (36 KB: 4 workgroups per CU)  // sparse staging: flag index space of 16 coefficients per byte (min segment)
+constexpr int kSegShift = 4;    // sparse staging: flag index space of 16 coefficients per byte (min segment)
+constexpr int kRixLds = 9216;   // K6r tile: at most this many floats of LDS (36 KB: 4 workgroups per CU)
 
 }  // namespace wc

@@ -18,6 +18,10 @@
 
 #include "wc_device.h"
 
+#ifndef WC_K1_NT
+#define WC_K1_NT false
+#endif
+
 namespace wc {
 
 __device__ __forceinline__ unsigned long long coef_key(float c, uint32_t f) {
@@ -192,7 +196,7 @@ __device__ __forceinline__ uint32_t xform_fast_p1(const T* __restrict__ src, con
             for (int zp = 0; zp < 4; ++zp)
 #pragma unroll
                 for (int dy = 0; dy < 2; ++dy)
-                    load_xpair<T>(p0 + sz * (4 * h + zp) + sy * dy, true, vec, v[zp][dy][0], v[zp][dy][1]);
+                    load_xpair<T, WC_K1_NT>(p0 + sz * (4 * h + zp) + sy * dy, true, vec, v[zp][dy][0], v[zp][dy][1]);
 #pragma unroll
             for (int qq = 0; qq < 2; ++qq) {
                 const int q = 2 * h + qq;
