@@ -222,14 +222,41 @@ __device__ __forceinline__ uint64_t wave_incl_sum(uint64_t v) {
     return v;
 }
 
+// Uniform reads of launch-constant tables (plan descriptors, tile lists) through
+// the constant address space: scalar loads even after the kernel has stored to
+// global memory (a vector load's vmcnt wait would also wait for loads in flight).
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* cst(const T* p) {
+    return (const __attribute__((address_space(4))) T*)(uintptr_t)p;
+}
+#else  // host pass of the same source: kernels are not compiled for the host
+template <class T>
+__device__ __forceinline__ const T* cst(const T* p) {
+    return p;
+}
+#endif
+
+// Workgroup barrier for LDS hand-offs only: unlike __syncthreads() it does not
+// wait for this wave's outstanding global loads (a prefetch stays in flight).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // Workgroup max of a 64-bit key folded into *dst with ONE atomicMax per
 // workgroup (all tiles of a unit update the same key word).  s: 4 LDS
 // slots; contains a barrier (call from uniform control flow).
+template <bool LDS_ONLY = false>
 __device__ __forceinline__ void block_key_max(unsigned long long v, unsigned long long* s,
                                               unsigned long long* dst) {
     v = wave_max_u64(v);
     if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
-    __syncthreads();
+    if constexpr (LDS_ONLY)
+        lds_barrier();
+    else
+        __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long m = s[0];
         for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = s[i] > m ? s[i] : m;

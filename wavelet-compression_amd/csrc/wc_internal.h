@@ -42,7 +42,7 @@ struct UnitDev {
     int32_t rix;            // 1: row-indexed inverse (K5 row index + K6r), 0: dense flat scratch
     int32_t ilbx, ilby;     // log2 of K6r's tile in blocks along x and y (all of z)
     uint64_t row_off;       // first rowinfo entry of the unit (W*H + 1 entries)
-    uint64_t dmagic;        // floor(2^64 / D) + 1: row = floor(position / D)
+    uint64_t dmagic;        // m | (31 + l) << 32: row = floor(position / D) = (position * m) >> (31 + l)
 };
 
 // A transform tile: a (1<<lbx) x (1<<lby) x (1<<lbz) box of 2x2x2 blocks.

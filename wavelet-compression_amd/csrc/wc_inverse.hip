@@ -121,11 +121,12 @@ __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict
                                                      int ordered) {
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_x[2];
-    const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const FTile ft = tiles[blockIdx.x];
+    const int tid = threadIdx.x, l = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const FTile ft = cst(tiles)[blockIdx.x];
     const uint32_t u = ft.unit;
-    const UnitDev& U = units[u];
-    const uint8_t* ph = payload + offsets[u];
+    const UnitDev U = cst(units)[u];  // scalar copy: no reloads after the stores below
+    const uint8_t* ph = payload + cst(offsets)[u];
     int32_t nrle;
     const bool hok = read_header(U, ph, nrle);
     const uint32_t n = hok ? (uint32_t)nrle : 0u;
@@ -190,31 +191,29 @@ __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict
     const uint32_t nc = (uint32_t)U.ncells;
     const uint32_t A = sat_add(s_x[1], wexcl);
 
-    // 3. row entries.  Per pair k < n: S = p_k + 1 (saturating), x = run + 1,
-    // previous position + 1 = S - x; the virtual pair k == n: S = p_{n-1} + 1
-    // and position ncoeff.  Positions clamp to ncoeff: when S saturates, S - x
-    // >= 2^31 > ncoeff too, so the clamped rows are exact.
+    // 3. row entries.  Pair k covers rows (rhi_{k-1}, rhi_k], rhi_k =
+    // floor(ph_k / D) with ph_k = min(p_k, ncoeff) (p_k = S - 1, S the
+    // saturating inclusive sum of run + 1; the virtual pair k == n sits at
+    // ncoeff), and rhi_{-1} = -1.  Positions at or past ncoeff (< 2^31) clamp
+    // to it, so saturated sums give the same rows.  rhi_{k-1} comes from the
+    // lane below (DPP), the previous round's lane 63, or for the wave's first
+    // pair from A (= p_{k-1} + 1): one division per pair, none of them 64-bit
+    // shifts of a second operand.
     uint2* __restrict__ ri = rowinfo + U.row_off;
     const uint32_t D = (uint32_t)U.nz;
+    int32_t carry = A == 0 ? -1 : (int32_t)div_rows(min(A - 1u, nc), U.dmagic);  // rhi of the pair before
 #pragma unroll
     for (int r = 0; r < kDecRounds; ++r) {
         const uint32_t k = kw + r * 64 + l;
-        const uint32_t S = sat_add(A, v[r]);
-        uint32_t rlo = 0, cnt = 0, ph = 0;
-        if (k <= n) {
-            uint32_t pl1;  // previous position + 1, in [0, ncoeff + 1]
-            if (k < n) {
-                ph = min(S - 1u, nc);
-                pl1 = min(S - x[r], nc + 1u);
-            } else {
-                ph = nc;
-                pl1 = min(S, nc + 1u);
-            }
-            rlo = pl1 == 0 ? 0u : div_rows(pl1 - 1u, U.dmagic) + 1u;
-            const uint32_t rhi = div_rows(ph, U.dmagic);
-            cnt = rhi >= rlo ? rhi - rlo + 1u : 0u;
-        }
-        write_rows(ri, rlo, cnt, k, ph, D, l);
+        const uint32_t phk = k < n ? min(sat_add(A, v[r]) - 1u, nc) : nc;
+        const int32_t rhi = k <= n ? (int32_t)div_rows(phk, U.dmagic) : -1;
+        // rhi of pair k - 1: lane l - 1, the carry in lane 0 (no wave-wide DPP shift on gfx950)
+        const int32_t from = __builtin_amdgcn_ds_bpermute((l - 1) << 2, rhi);
+        const int32_t rlo = (l == 0 ? carry : from) + 1;
+        const uint32_t cnt = (k <= n && rhi >= rlo) ? (uint32_t)(rhi - rlo + 1) : 0u;
+        write_rows(ri, (uint32_t)rlo, cnt, k, phk, D, l);
+        carry = __builtin_amdgcn_readlane(rhi, 63);
+        if (carry < 0) break;  // uniform: lane 63 is past the virtual pair, so is every later round
     }
 }
 
