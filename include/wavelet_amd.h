@@ -96,10 +96,18 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  * WC_OPT_INVERSE_ROWS (default 1): the inverse of even-dims units (W, H even,
  *   D % 8 == 0) indexes the payload's pairs by flat row and reconstructs each
  *   tile straight from the payload; 0 decodes every unit into a dense fp32
- *   coefficient scratch first (4 B/cell written and read back).  Same cells. */
+ *   coefficient scratch first (4 B/cell written and read back).  Same cells.
+ * WC_OPT_RIX_LDS (default 9216), WC_OPT_RIX_TX (default 4): tile shape of the
+ *   row-indexed inverse: LDS floats per workgroup (1024..16384) and log2 of the
+ *   tile's blocks along x (0..5); y takes the rest of the budget.  Same cells.
+ * WC_OPT_RIX_BLOCKED (default 0): each workgroup of the row-indexed inverse
+ *   runs a contiguous run of tiles (0: tiles b, b + grid, ...).  Same cells. */
 #define WC_OPT_SPARSE 12
 #define WC_OPT_ORDERED 13
 #define WC_OPT_INVERSE_ROWS 14
+#define WC_OPT_RIX_LDS 15
+#define WC_OPT_RIX_TX 16
+#define WC_OPT_RIX_BLOCKED 17
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 
 /* Host-side helpers (no device work). */

@@ -260,6 +260,46 @@ def test_inverse_writes_every_coefficient(wc, ctx, oracle, sparse):
         assert regen[o:o + b.size].tobytes() == want.tobytes(), i
 
 
+def test_inverse_repeated_calls_epoch_granules(wc, ctx, oracle):
+    """The row index keeps its work items and look-back granules across calls,
+    tagged with the call's epoch instead of zeroed: a big batch, then a smaller
+    one (the big call's items past its end are stale), a malformed payload, the
+    ticket form, and more than 256 units (the item workgroups' own look-back)
+    must each decode exactly, on one context."""
+    big_dims = [(64, 64, 64)] * 3 + [(32, 32, 32)] * 5 + [(16, 16, 16)] * 8
+    small_dims = [(16, 16, 16), (8, 8, 8)]
+    many_dims = [(8, 4, 8)] * 300 + [(32, 16, 64)] * 4
+    batches = [(big_dims, 21), (small_dims, 22), (big_dims, 23), (many_dims, 24), (small_dims, 25)]
+
+    def run(dims, seed, path="staged"):
+        boxes = synth(oracle, dims, seed0=seed)
+        units, n, extent, cells = pack(wc, boxes)
+        payload, offs, kept = ctx.forward_host(cells, units, n, KEEPS[1])
+        set_path(ctx, path)
+        try:
+            regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
+        finally:
+            set_path(ctx, "staged")
+        for i, b in enumerate(boxes):
+            o = units[i].cell_offset
+            want = oracle.decompress_payload(wc.capi.unit_payload(payload, offs, kept, i)).ravel()
+            assert regen[o:o + b.size].tobytes() == want.tobytes(), (dims[i], i, path)
+
+    for dims, seed in batches:
+        run(dims, seed)
+    run(big_dims, 26, path="tickets")
+    b = synth(oracle, [(8, 8, 8)], seed0=6)[0]
+    p = bytearray(oracle_payload(oracle, b, KEEPS[1]))
+    p[0] = 9
+    units, n, extent = wc.capi.make_units([(8, 8, 8)])
+    buf = np.zeros(len(p) + 16, np.uint8)
+    buf[4:4 + len(p)] = np.frombuffer(bytes(p), np.uint8)
+    with pytest.raises(wc.WaveletError):
+        ctx.inverse_host(buf, np.array([4], np.uint64), units, n, extent)
+    run(small_dims, 27)
+    run(big_dims, 28)
+
+
 def test_inverse_flat_random(wc, ctx, oracle):
     import torch
     rng = np.random.default_rng(11)

@@ -5,7 +5,7 @@
 // Box-Muller noise), then wc_forward runs `steps` times.  Prints one JSON line.
 //
 // usage: wc_bench [boxes=1024] [dim=64] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1]
-//                 [check=0|1] [ordered=1] [sparse=1] [rows=1]
+//                 [check=0|1] [ordered=1] [sparse=1] [rows=1] [rix_lds=9216] [rix_tx=4] [rix_blocked=0]
 // check=1: also run the conservative configuration (ticket look-back, dense
 // staging, dense inverse decode) once and compare every unit's payload bytes and, with inverse=1,
 // every reconstructed cell ("paths_identical" in the JSON line).
@@ -65,6 +65,9 @@ int main(int argc, char** argv) {
     const int ordered = argc > 9 ? std::atoi(argv[9]) : 1;
     const int sparse = argc > 10 ? std::atoi(argv[10]) : 1;
     const int rows = argc > 11 ? std::atoi(argv[11]) : 1;
+    const int rix_lds = argc > 12 ? std::atoi(argv[12]) : 9216;
+    const int rix_tx = argc > 13 ? std::atoi(argv[13]) : 4;
+    const int rix_blocked = argc > 14 ? std::atoi(argv[14]) : 0;
 
     std::vector<wc_unit> units(boxes);
     const unsigned long long per = (unsigned long long)dim * dim * dim;
@@ -96,6 +99,11 @@ int main(int argc, char** argv) {
     wc_set_option(ctx, WC_OPT_ORDERED, ordered);
     wc_set_option(ctx, WC_OPT_SPARSE, sparse);
     wc_set_option(ctx, WC_OPT_INVERSE_ROWS, rows);
+    if (wc_set_option(ctx, WC_OPT_RIX_LDS, rix_lds) != WC_OK || wc_set_option(ctx, WC_OPT_RIX_TX, rix_tx) != WC_OK ||
+        wc_set_option(ctx, WC_OPT_RIX_BLOCKED, rix_blocked) != WC_OK) {
+        std::fprintf(stderr, "options: %s\n", wc_last_error(ctx));
+        return 2;
+    }
     auto fwd = [&]() {
         int rc = wc_forward(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, keep, payload, cap, offsets, kept);
         if (rc != WC_OK) {
@@ -188,9 +196,9 @@ int main(int argc, char** argv) {
     const char* names[WC_NUM_STAGES] = {"transform", "emit", "decode", "inverse", "rmse", "hist"};
     std::printf("{\"boxes\": %d, \"dim\": %d, \"dtype\": \"%s\", \"keep\": %.17g, \"steps\": %d, "
                 "\"ms_per_step\": %.4f, \"cells_per_s\": %.6e, \"kept_fraction\": %.6f, \"payload_bytes\": %llu, "
-                "\"ordered\": %d, \"sparse\": %d, \"rows\": %d, \"paths_identical\": %d, \"stage_ms\": {",
+                "\"ordered\": %d, \"sparse\": %d, \"rows\": %d, \"rix\": [%d, %d, %d], \"paths_identical\": %d, \"stage_ms\": {",
                 boxes, dim, f64 ? "f64" : "f32", keep, steps, step_ms, per * boxes / (step_ms * 1e-3),
-                ksum / (double)(per * boxes), (unsigned long long)total, ordered, sparse, rows, identical);
+                ksum / (double)(per * boxes), (unsigned long long)total, ordered, sparse, rows, rix_lds, rix_tx, rix_blocked, identical);
     bool first = true;
     for (int s = 0; s < WC_NUM_STAGES; ++s)
         if (cnt[s]) {

@@ -32,10 +32,11 @@ hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, 
 hipError_t launch_transform_fallback(hipStream_t, const void*, int, const UnitDev*, int, const XTile*, size_t, float*,
                                      const unsigned long long*, double);
 hipError_t launch_pack(hipStream_t, const UnitDev*, int, const uint32_t*, const uint8_t*, uint64_t*, uint8_t*);
-hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, const FTile*, uint32_t, const uint8_t*,
-                         const uint64_t*, uint32_t*, unsigned long long*, float*, uint2*, uint32_t*, int);
+hipError_t launch_decode(hipStream_t, const UnitDev*, int, const FTile*, uint32_t, uint32_t, RixItem*,
+                         unsigned long long*, uint32_t, const uint8_t*, const uint64_t*, uint32_t*,
+                         unsigned long long*, float*, uint2*, uint32_t*, int);
 hipError_t launch_inverse_rows(hipStream_t, const RTile*, uint32_t, size_t, const uint8_t*, const uint64_t*,
-                               const uint2*, float*);
+                               const uint2*, float*, int);
 hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const XTile*, uint32_t, size_t, uint32_t,
                           size_t, float*);
 hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDev*, int, const FTile*,
@@ -66,7 +67,10 @@ struct Plan {
     std::vector<XTile> xtiles;
     std::vector<XTile> ixtiles;  // dense inverse tiles of the non-row-indexed units: [generic | fast]
     std::vector<RTile> rtiles;   // K6r tiles of the row-indexed units
-    std::vector<FTile> ftiles, dtiles, rdtiles;  // dtiles: dense decode, rdtiles: row index (K5)
+    std::vector<FTile> ftiles, dtiles;  // dtiles: dense decode blocks
+    uint32_t nrix_items = 0;            // row-index work items at most (sum of ndt over row-indexed units)
+    int rix_lds = kRixLds;              // WC_OPT_RIX_LDS the plan was built with
+    int rix_lx = 4;                     // WC_OPT_RIX_TX the plan was built with
     std::vector<uint32_t> eunits, eidx;
     uint32_t ngen = 0, nfast = 0, netiles = 0;
     uint32_t ign = 0, ifast = 0;  // ixtiles split
@@ -77,7 +81,7 @@ struct Plan {
     uint64_t coef_extent = 0;  // floats of staged coefficient scratch
     size_t lds_gen = 0, lds_fast = 0, lds_inverse = 0;
     size_t state_bytes = 0;    // forward per-call state: 16 | key[n] | tickets[n] | status[netiles]
-    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_eunits, d_ixtiles, d_eidx, d_rtiles, d_rdtiles;
+    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_eunits, d_ixtiles, d_eidx, d_rtiles;
 };
 
 int ceil_log2(int64_t v) {
@@ -98,6 +102,9 @@ struct wc_ctx {
     bool opt_ordered = true;  // WC_OPT_ORDERED (see include/wavelet_amd.h)
     bool opt_sparse = true;   // WC_OPT_SPARSE
     bool opt_inv_rows = true; // WC_OPT_INVERSE_ROWS
+    int opt_rix_lds = kRixLds; // WC_OPT_RIX_LDS
+    int opt_rix_lx = 4;        // WC_OPT_RIX_TX
+    bool opt_rix_blocked = false; // WC_OPT_RIX_BLOCKED
     // A kernel that may raise error bits ran since the last check.  Kernels
     // atomicOr into ONE persistent error word (errflag, zeroed at creation and
     // after each read), so errors of several async calls accumulate until the
@@ -110,6 +117,11 @@ struct wc_ctx {
     uint64_t plan_gen = 0;  // bumped whenever get_plan rebuilds the plan
     // scratch (grow-only)
     DevBuf coef, part, errflag, state, flags, rowinfo;
+    // row index (wc_inverse): work items and epoch-tagged look-back granules,
+    // zeroed when allocated and never again (a granule of an earlier call reads
+    // as unpublished); epoch: the call counter they are tagged with
+    DevBuf ritems, istate;
+    uint32_t epoch = 0;
     // host-path staging
     DevBuf h_cells, h_payload, h_packed, h_offsets, h_poff, h_kept, h_out;
     // per-kernel event timing (wc_profile_enable / wc_profile_read)
@@ -276,15 +288,15 @@ void build_etiles(Plan& P, int n) {
 // sub-band reads); the others decode densely.
 size_t rix_lds_bytes(const UnitDev& d) { return sizeof(float) * 4 * (size_t)rix_wr(d.ilbx, d.ilby, d.nz); }
 
-bool set_rix_tiling(UnitDev& d) {
+bool set_rix_tiling(UnitDev& d, int budget, int max_lx) {
     d.rix = 0;
     if (!d.fast || d.ncells == 0) return false;
     auto floats = [&](int tx, int ty) { return (int64_t)4 * (tx * ((int64_t)ty * d.nz + 4) + 16); };
-    int lx = std::min(4, ceil_log2(d.hx));  // 16 blocks: 128-B output rows; the rest of the budget to TY
-    while (lx > 0 && floats(1 << lx, 1) > kRixLds) --lx;
-    if (floats(1 << lx, 1) > kRixLds) return false;
+    int lx = std::min(max_lx, ceil_log2(d.hx));  // 16 blocks: 128-B output rows; the rest of the budget to TY
+    while (lx > 0 && floats(1 << lx, 1) > budget) --lx;
+    if (floats(1 << lx, 1) > budget) return false;
     int ly = 0;
-    while ((1 << ly) < d.hy && floats(1 << lx, 2 << ly) <= kRixLds) ++ly;
+    while ((1 << ly) < d.hy && floats(1 << lx, 2 << ly) <= budget) ++ly;
     d.ilbx = lx;
     d.ilby = ly;
     d.rix = 1;
@@ -294,13 +306,16 @@ bool set_rix_tiling(UnitDev& d) {
 // Build (or reuse) the plan for this batch and upload it.
 int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     Plan& P = c->plan;
-    if (c->plan_valid && P.inv_rows == c->opt_inv_rows && (int)P.key.size() == n &&
+    if (c->plan_valid && P.inv_rows == c->opt_inv_rows && P.rix_lds == c->opt_rix_lds &&
+        P.rix_lx == c->opt_rix_lx && (int)P.key.size() == n &&
         (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0))
         return WC_OK;
     c->plan_valid = false;
     ++c->plan_gen;
     P.key.assign(units, units + n);
     P.inv_rows = c->opt_inv_rows;
+    P.rix_lds = c->opt_rix_lds;
+    P.rix_lx = c->opt_rix_lx;
     P.units.assign(n, UnitDev{});
     P.xtiles.clear();
     P.ftiles.clear();
@@ -347,7 +362,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         else
             P.lds_gen = std::max(P.lds_gen, transform_lds_bytes(d.lbx, d.lby, d.lbz));
         P.lds_inverse = std::max(P.lds_inverse, transform_lds_bytes(d.lbx, d.lby, d.lbz));
-        if (P.inv_rows && set_rix_tiling(d)) {
+        if (P.inv_rows && set_rix_tiling(d, P.rix_lds, P.rix_lx)) {
             d.row_off = P.rowinfo_entries;
             P.rowinfo_entries += (uint64_t)d.nx * d.ny + 1;
             {  // floor(p / D) = (p * m) >> (31 + l), p < 2^31 (wc_inverse.hip div_rows)
@@ -402,18 +417,20 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     // one tile more when kFlatTile divides ncoeff (the virtual pair k = nrle
     // that closes its row index, wc_inverse.hip).
     P.dtiles.clear();
-    P.rdtiles.clear();
+    P.nrix_items = 0;
     {
         uint32_t maxt = 0, total = 0;
         for (UnitDev& d : P.units) {
-            d.ndt = d.rix ? (uint32_t)(d.ncells / kFlatTile) + 1 : d.nftiles;
+            d.ndt = d.rix ? (uint32_t)(d.ncells / kRixTile) + 1 : d.nftiles;
             d.dt_begin = total;
             total += d.ndt;
             maxt = std::max(maxt, d.ndt);
         }
         for (uint32_t t = 0; t < maxt; ++t)
             for (int i = 0; i < n; ++i)
-                if (t < P.units[i].ndt) (P.units[i].rix ? P.rdtiles : P.dtiles).push_back(FTile{(uint32_t)i, t});
+                if (t < P.units[i].ndt && !P.units[i].rix) P.dtiles.push_back(FTile{(uint32_t)i, t});
+        for (const UnitDev& d : P.units)
+            if (d.rix) P.nrix_items += d.ndt;
     }
     P.coef_extent = coef_cursor ? coef_cursor + kFlatTile : 0;  // slack: flat tiles read whole float4 groups
     build_etiles(P, n);
@@ -425,8 +442,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         (rc = upload(c, P.d_dtiles, P.dtiles.data(), sizeof(FTile) * P.dtiles.size(), "upload dtiles")) ||
         (rc = upload(c, P.d_eunits, P.eunits.data(), sizeof(uint32_t) * P.eunits.size(), "upload eunits")) ||
         (rc = upload(c, P.d_eidx, P.eidx.data(), sizeof(uint32_t) * P.eidx.size(), "upload eidx")) ||
-        (rc = upload(c, P.d_rtiles, P.rtiles.data(), sizeof(RTile) * P.rtiles.size(), "upload rtiles")) ||
-        (rc = upload(c, P.d_rdtiles, P.rdtiles.data(), sizeof(FTile) * P.rdtiles.size(), "upload rdtiles")))
+        (rc = upload(c, P.d_rtiles, P.rtiles.data(), sizeof(RTile) * P.rtiles.size(), "upload rtiles")))
         return rc;
     // The host vectors back the async copies: finish them before returning.
     hipError_t e = hipStreamSynchronize(c->stream);
@@ -435,9 +451,26 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     return WC_OK;
 }
 
-// Per-call state of the decode: ticket[n] (8-B aligned) | status[decode tiles].
-size_t decode_state_bytes(const Plan& P) {
-    return round_up(4ull * P.units.size(), 8) + 8ull * (P.dtiles.size() + P.rdtiles.size());
+uint64_t decode_tiles(const Plan& P) {
+    uint64_t tiles = 0;
+    for (const UnitDev& d : P.units) tiles += d.ndt;
+    return tiles;
+}
+
+// Per-call state of the dense decode: ticket[n] (8-B aligned) | status[decode
+// tiles of every unit] (zeroed per call).
+size_t decode_state_bytes(const Plan& P) { return round_up(4ull * P.units.size(), 8) + 8ull * decode_tiles(P); }
+
+// Row-index granules: item workgroups' totals | the tiles' sums (at dt_begin).
+size_t istate_bytes(const Plan& P) { return 8ull * ((P.units.size() + kThreads - 1) / kThreads + decode_tiles(P)); }
+
+// ensure() for buffers whose contents must start zeroed.
+int ensure_zeroed(wc_ctx* c, DevBuf& b, size_t bytes) {
+    const void* before = b.p;
+    int rc = ensure(c, b, bytes);
+    if (rc || b.p == before) return rc;
+    hipError_t e = hipMemsetAsync(b.p, 0, b.bytes, c->stream);
+    return e == hipSuccess ? WC_OK : hip_fail(c, e, "memset");
 }
 
 // Scratch of the staged forward, the inverse and the RMSE (grow-only).
@@ -449,6 +482,8 @@ int ensure_scratch(wc_ctx* c) {
         (rc = ensure(c, c->flags, (P.coef_extent >> kSegShift) + kEmitTile)) ||
         (rc = ensure(c, c->part, sizeof(double) * nft)) ||
         (rc = ensure(c, c->rowinfo, sizeof(uint32_t) * 2 * std::max<uint64_t>(P.rowinfo_entries, 1))) ||
+        (rc = ensure_zeroed(c, c->ritems, sizeof(RixItem) * std::max<uint64_t>(P.nrix_items, 1))) ||
+        (rc = ensure_zeroed(c, c->istate, istate_bytes(P))) ||
         (rc = ensure(c, c->state, std::max<size_t>(P.state_bytes, decode_state_bytes(P)))))
         return rc;
     return WC_OK;
@@ -601,7 +636,7 @@ void wc_ctx_destroy(wc_ctx* c) {
                       &c->h_offsets,     &c->h_poff,         &c->h_kept,         &c->h_out,
                       &c->plan.d_units,  &c->plan.d_xtiles,  &c->plan.d_ftiles,  &c->plan.d_dtiles,
                       &c->plan.d_eunits, &c->plan.d_ixtiles, &c->plan.d_eidx, &c->plan.d_rtiles,
-                      &c->plan.d_rdtiles, &c->rowinfo};
+                      &c->rowinfo, &c->ritems, &c->istate};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& m : c->marks) {
@@ -632,6 +667,17 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
             return WC_OK;
         case WC_OPT_INVERSE_ROWS:
             c->opt_inv_rows = value != 0;
+            return WC_OK;
+        case WC_OPT_RIX_LDS:
+            if (value < 1024 || value > 16384) return fail(c, WC_ERR_INVALID, "WC_OPT_RIX_LDS: 1024..16384 floats");
+            c->opt_rix_lds = (int)value;
+            return WC_OK;
+        case WC_OPT_RIX_BLOCKED:
+            c->opt_rix_blocked = value != 0;
+            return WC_OK;
+        case WC_OPT_RIX_TX:
+            if (value < 0 || value > 5) return fail(c, WC_ERR_INVALID, "WC_OPT_RIX_TX: log2 of 1..32 blocks");
+            c->opt_rix_lx = (int)value;
             return WC_OK;
         default:
             return fail(c, WC_ERR_INVALID, "unknown option");
@@ -779,25 +825,35 @@ int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, c
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n)) || (rc = ensure_scratch(c))) return rc;
     Plan& P = c->plan;
     hipError_t e;
-    // per-call decode state: ticket[n] | status[flat tiles]; the dense
-    // coefficient scratch itself is fully written by the decode (no memset)
+    // per-call state of the dense decode and of the ticket form: ticket[n] |
+    // status[decode tiles] (zeroed).  The row index needs none: its granules
+    // carry the call's epoch.  The dense coefficient scratch is fully written
+    // by the decode (no memset).
     uint8_t* st = (uint8_t*)c->state.p;
-    if ((e = hipMemsetAsync(st, 0, decode_state_bytes(P), c->stream)) != hipSuccess)
+    if ((!P.dtiles.empty() || !c->opt_ordered) &&
+        (e = hipMemsetAsync(st, 0, decode_state_bytes(P), c->stream)) != hipSuccess)
         return hip_fail(c, e, "memset");
+    c->epoch = (c->epoch + 1) & kEpochMask;
+    if (c->epoch == 0) {  // wrapped: granules of 2^30 calls ago could look current
+        if ((e = hipMemsetAsync(c->istate.p, 0, c->istate.bytes, c->stream)) != hipSuccess ||
+            (e = hipMemsetAsync(c->ritems.p, 0, c->ritems.bytes, c->stream)) != hipSuccess)
+            return hip_fail(c, e, "memset");
+        c->epoch = 1;
+    }
     {
         StageTimer t(c, WC_STAGE_DECODE);
-        e = launch_decode(c->stream, (const UnitDev*)P.d_units.p, (const FTile*)P.d_dtiles.p,
-                          (uint32_t)P.dtiles.size(), (const FTile*)P.d_rdtiles.p, (uint32_t)P.rdtiles.size(),
-                          d_payload, d_offsets, (uint32_t*)st,
-                          (unsigned long long*)(st + round_up(4ull * n, 8)), (float*)c->coef.p,
-                          (uint2*)c->rowinfo.p, (uint32_t*)c->errflag.p, c->opt_ordered ? 1 : 0);
+        e = launch_decode(c->stream, (const UnitDev*)P.d_units.p, n, (const FTile*)P.d_dtiles.p,
+                          (uint32_t)P.dtiles.size(), P.nrix_items, (RixItem*)c->ritems.p,
+                          (unsigned long long*)c->istate.p, c->epoch, d_payload, d_offsets, (uint32_t*)st,
+                          (unsigned long long*)(st + round_up(4ull * n, 8)), (float*)c->coef.p, (uint2*)c->rowinfo.p,
+                          (uint32_t*)c->errflag.p, c->opt_ordered ? 1 : 0);
     }
     if (e != hipSuccess) return hip_fail(c, e, "decode launch");
     {
         StageTimer t(c, WC_STAGE_INVERSE);
         e = launch_inverse_rows(c->stream, (const RTile*)P.d_rtiles.p, (uint32_t)P.rtiles.size(), P.lds_rows,
                                 d_payload, d_offsets,
-                                (const uint2*)c->rowinfo.p, d_out);
+                                (const uint2*)c->rowinfo.p, d_out, c->opt_rix_blocked ? 1 : 0);
         if (e == hipSuccess)
             e = launch_inverse(c->stream, (const float*)c->coef.p, 0, (const UnitDev*)P.d_units.p,
                                (const XTile*)P.d_ixtiles.p, P.ign, P.lds_inverse, P.ifast, P.lds_fast, d_out);

@@ -202,6 +202,36 @@ __device__ __forceinline__ unsigned long long lookback_sum62(const unsigned long
     return excl & kMask62;
 }
 
+// Epoch-tagged granules: flag (2 bits) | epoch (30 bits) | 32-bit saturated
+// sum.  A granule of another epoch (an earlier call) reads as unpublished, so
+// a buffer of such granules needs zeroing only once, when it is allocated.
+__device__ __forceinline__ unsigned long long granule_e(unsigned long long flag, uint32_t epoch, uint32_t sum) {
+    return flag | ((unsigned long long)(epoch & kEpochMask) << 32) | sum;
+}
+
+// lookback_sum62 over epoch-tagged granules; the result saturates at 2^32 - 1.
+__device__ __forceinline__ uint32_t lookback_sum32e(const unsigned long long* st, int64_t t, int l, uint32_t* err,
+                                                    uint32_t epoch) {
+    unsigned long long excl = 0;
+    int64_t pos = t - 1;
+    const uint32_t ep = epoch & kEpochMask;
+    for (uint32_t spins = 0;;) {
+        const int64_t idx = pos - l;
+        unsigned long long v = idx >= 0 ? ld_rlx(st + idx) : granule_e(kFlagIncl, ep, 0u);
+        if ((uint32_t)(v >> 32 & kEpochMask) != ep) v = 0;  // an earlier call's granule: unpublished
+        const unsigned long long incl = __ballot((v >> 62) == 2);
+        const unsigned long long zero = __ballot((v >> 62) == 0);
+        const int kI = incl ? __ffsll((long long)incl) - 1 : 64;
+        const int kZ = zero ? __ffsll((long long)zero) - 1 : 64;
+        const int take = kI < kZ ? kI + 1 : kZ;  // lanes [0, take) are summed
+        if (take > 0) excl += wave_sum(l < take ? (v & 0xffffffffull) : 0ull);
+        if (kI < kZ) break;
+        pos -= take;
+        if (take == 0 && spin_fail(spins, err)) break;
+    }
+    return excl > 0xffffffffull ? 0xffffffffu : (uint32_t)excl;
+}
+
 // Wave-wide inclusive sum (64 lanes) on DPP lane moves, GFX9 pattern:
 // row_shr 1/2/4/8 within 16-lane rows, then row_bcast:15 and row_bcast:31
 // carry into the next rows.  Lanes whose source is out of range read 0.

@@ -83,6 +83,9 @@ __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, ui
             }
         }
         __builtin_amdgcn_wave_barrier();
+#ifdef WC_XP_E_NOSTORE
+        if (itot == 0x7fffffffu)
+#endif
         for (uint32_t k = (uint32_t)l; k < itot; k += 64) pairs[rank + k] = stage[k];
         __builtin_amdgcn_wave_barrier();
         rank += itot;
@@ -193,6 +196,9 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
             // inclusive one are summed once every one of them has published;
             // a run of published aggregates before the first unpublished tile
             // is summed and the window slides past it.
+#ifdef WC_XP_E_NOLB
+            if (pos == -7)
+#endif
             for (uint32_t spins = 0;;) {
                 const int64_t idx = pos - l;
                 const unsigned long long v = idx >= first ? ld_rlx(P.status + idx) : kFlagIncl;

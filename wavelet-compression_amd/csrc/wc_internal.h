@@ -64,6 +64,19 @@ struct RTile {
     int32_t pad;
 };
 
+// Work item of the row index (K5, wc_inverse.hip k_rowindex): pair tile t of
+// a row-indexed unit, written on the device by k_rix_items from the unit's
+// payload header (a unit's tiles are consecutive items, ascending).
+struct RixItem {
+    uint64_t pay;    // byte offset of the unit's payload (offsets[unit])
+    uint32_t unit;
+    uint32_t t;      // pair tile (kRixTile pairs) within the unit
+    uint32_t n;      // pairs of the payload (nrle; 0 when the header is bad)
+    uint32_t bad;    // 1: the header disagrees with the unit (raised by tile 0)
+    uint32_t epoch;  // the wc_inverse call that wrote the item (older items are stale)
+    uint32_t pad;
+};
+
 // LDS layout of a K6r tile: 4 wave regions of TX ranges of RS = TY*D + 4
 // floats, regions 16 floats apart (bank offset), 16-B aligned.
 __host__ __device__ inline int rix_rs(int lby, int D) { return (D << lby) + 4; }
@@ -83,6 +96,8 @@ constexpr unsigned long long kKeyNaNFirst = ~0ull;
 constexpr uint32_t kErrHeader = 1u;      // payload header disagrees with the unit
 constexpr uint32_t kErrNegativeRun = 2u; // a run length < 0 (reference: UB)
 constexpr uint32_t kErrTimeout = 8u;     // a look-back wait between workgroups hit its bound
+
+constexpr uint32_t kEpochMask = 0x3fffffffu;  // epoch bits of a look-back granule (wc_device.h granule_e)
 
 constexpr int kEmitTile = 8192;          // coefficients per emit tile (32 per thread)
 
@@ -107,6 +122,11 @@ struct EmitParams {
 };
 
 constexpr int kSegShift = 4;    // sparse staging: flag index space of 16 coefficients per byte (min segment)
-constexpr int kRixLds = 9216;   // K6r tile: at most this many floats of LDS (36 KB: 4 workgroups per CU)
+#ifndef WC_RIX_TILE
+#define WC_RIX_TILE 4096
+#endif
+constexpr int kRixTile = WC_RIX_TILE;   // pairs per row-index (K5) tile
+constexpr int kRixRounds5 = kRixTile / kThreads;
+constexpr int kRixLds = 9216;   // K6r tile: default LDS budget in floats (36 KB: 4 workgroups per CU)
 
 }  // namespace wc

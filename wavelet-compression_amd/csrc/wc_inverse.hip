@@ -107,60 +107,126 @@ __device__ __forceinline__ void write_rows(uint2* __restrict__ ri, uint32_t r_lo
     }
 }
 
+// Work list of the row index: unit u's pair tiles t < min(nrle / kRixTile + 1,
+// ndt) (the tile holding the virtual pair k = nrle closes the table; tiles
+// past floor(ncoeff / kRixTile) hold only dropped pairs) as consecutive items.
+//
+// Workgroup b covers units [256b, 256b + 256): a block scan of the tile
+// counts, a look-back over the earlier workgroups' totals (epoch-tagged
+// granules ist[], no zeroing per call) for the first item, then the items
+// are written cooperatively (consecutive lanes, consecutive items).
+__global__ __launch_bounds__(kThreads) void k_rix_items(const UnitDev* __restrict__ units, int nunits,
+                                                      const uint8_t* __restrict__ payload,
+                                                      const uint64_t* __restrict__ offsets, RixItem* __restrict__ items,
+                                                      unsigned long long* __restrict__ ist, uint32_t* __restrict__ err,
+                                                      uint32_t epoch) {
+    __shared__ uint32_t s_sum[4];
+    __shared__ uint32_t s_max[4];
+    __shared__ uint32_t s_base;
+    __shared__ uint32_t s_excl[kThreads + 1];
+    __shared__ uint32_t s_n[kThreads];
+    __shared__ uint64_t s_off[kThreads];
+    const int tid = threadIdx.x, l = tid & 63;
+    const int u = blockIdx.x * kThreads + tid;
+    uint32_t nt = 0, n = 0;
+    uint64_t off = 0;
+    bool hok = true;
+    if (u < nunits && units[u].rix) {
+        const UnitDev& U = units[u];
+        off = offsets[u];
+        int32_t nrle;
+        hok = read_header(U, payload + off, nrle);
+        n = hok ? (uint32_t)nrle : 0u;
+        nt = min(n / (uint32_t)kRixTile + 1u, U.ndt);
+    }
+    const ScanOut sc = block_scan_sum_max<uint32_t>(nt, 0u, s_sum, s_max);
+    s_excl[tid] = (uint32_t)sc.excl_sum;
+    s_n[tid] = n | (hok ? 0u : 0x80000000u);  // nrle >= 0 fits in 31 bits
+    s_off[tid] = off;
+    const uint32_t T = (uint32_t)sc.total_sum;
+    if (tid == 0) s_excl[kThreads] = T;
+    if (tid < 64) {
+        uint32_t excl = 0;
+        if (blockIdx.x == 0) {
+            if (l == 0) st_rlx(ist, granule_e(kFlagIncl, epoch, T));
+        } else {
+            if (l == 0) st_rlx(ist + blockIdx.x, granule_e(kFlagAgg, epoch, T));
+            excl = lookback_sum32e(ist, (int64_t)blockIdx.x, l, err, epoch);
+            if (l == 0) st_rlx(ist + blockIdx.x, granule_e(kFlagIncl, epoch, excl + T));
+        }
+        if (l == 0) s_base = excl;
+    }
+    __syncthreads();
+    const uint32_t base = s_base;
+    for (uint32_t i = tid; i < T; i += kThreads) {
+        // the LAST thread whose range starts at or before i: its range is the
+        // one holding i (empty ranges before it share its start)
+        int lo = 0;
+#pragma unroll
+        for (int step = kThreads / 2; step >= 1; step >>= 1)
+            if (s_excl[lo + step] <= i) lo += step;
+        const uint32_t nn = s_n[lo];
+        items[base + i] = RixItem{s_off[lo], blockIdx.x * (uint32_t)kThreads + (uint32_t)lo, i - s_excl[lo],
+                                  nn & 0x7fffffffu, nn >> 31, epoch & kEpochMask, 0u};
+    }
+}
+
 // Row index of the row-indexed units.  Only the runs are needed (the values
 // stay in the payload for K6r).  A negative run (malformed; the reference's
 // behaviour is undefined) counts as run 0, so positions never decrease and
 // every row entry is written: K6r never sees a stale or out-of-range entry.
+//
+// One block per item slot: block b works on item b (slots this call did not
+// write hold an earlier epoch: the block exits); tile index from the item (ordered:
+// a unit's items are consecutive, so a tile's look-back waits only on lower
+// block ids, DESIGN.md §Forward progress) or from a per-unit ticket.
+__device__ __forceinline__ void rix_load_runs(const uint8_t* __restrict__ payload, const RixItem& it, int w, int l,
+                                              uint32_t (&v)[kRixRounds5]) {
+    const uint32_t* __restrict__ runs = reinterpret_cast<const uint32_t*>(payload + it.pay + 20);
+    const uint32_t kw = it.t * (uint32_t)kRixTile + (uint32_t)w * (kRixTile / 4);
+#pragma unroll
+    for (int r = 0; r < kRixRounds5; ++r) {
+        const uint32_t k = kw + r * 64 + l;
+        v[r] = k < it.n ? runs[2 * k] : 0u;
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict__ units,
-                                                     const FTile* __restrict__ tiles,
-                                                     const uint8_t* __restrict__ payload,
-                                                     const uint64_t* __restrict__ offsets,
+                                                     const RixItem* __restrict__ items,
                                                      uint32_t* __restrict__ ticket,
+                                                     const uint8_t* __restrict__ payload,
                                                      unsigned long long* __restrict__ status,
                                                      uint2* __restrict__ rowinfo, uint32_t* __restrict__ err,
-                                                     int ordered) {
+                                                     int ordered, uint32_t epoch) {
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_x[2];
     const int tid = threadIdx.x, l = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const FTile ft = cst(tiles)[blockIdx.x];
-    const uint32_t u = ft.unit;
-    const UnitDev U = cst(units)[u];  // scalar copy: no reloads after the stores below
-    const uint8_t* ph = payload + cst(offsets)[u];
-    int32_t nrle;
-    const bool hok = read_header(U, ph, nrle);
-    const uint32_t n = hok ? (uint32_t)nrle : 0u;
-    // tiles up to the one holding the virtual pair k = n; the plan launches
-    // floor(ncoeff / kFlatTile) + 1, enough for the first dropped pair
-    const uint32_t ntile = n / kFlatTile + 1u;
-    if (ft.index >= ntile) return;  // uniform
-    uint32_t t = ft.index;
+    RixItem it = cst(items)[blockIdx.x];
+    if (it.epoch != (epoch & kEpochMask)) return;  // uniform: no item of this call
     if (!ordered) {
-        if (tid == 0) s_x[0] = atomicAdd(ticket + u, 1u);
+        if (tid == 0) s_x[0] = atomicAdd(ticket + it.unit, 1u);
         __syncthreads();
-        t = s_x[0];
+        it.t = s_x[0];
     }
-    if (!hok && t == 0 && tid == 0) atomicOr(err, kErrHeader);
+    const uint32_t u = it.unit, t = it.t, n = it.n;
+    uint32_t v[kRixRounds5];
+    rix_load_runs(payload, it, w, l, v);
+    const UnitDev U = cst(units)[u];  // scalar copy: no reloads after the stores below
+    if (it.bad && t == 0 && tid == 0) atomicOr(err, kErrHeader);
 
-    // 1. runs -> v = run + 1 (k < n), 0 (k >= n); saturating in-wave sums
-    const uint32_t* __restrict__ runs = reinterpret_cast<const uint32_t*>(ph + 20);
-    const uint32_t kw = t * (uint32_t)kFlatTile + (uint32_t)w * (kFlatTile / 4);
-    uint32_t v[kDecRounds];
-#pragma unroll
-    for (int r = 0; r < kDecRounds; ++r) {
-        const uint32_t k = kw + r * 64 + l;
-        v[r] = k < n ? runs[2 * k] : 0u;
-    }
+    // 1. v = run + 1 (k < n), 0 (k >= n) -> saturating in-wave inclusive sums
+    const uint32_t kw = t * (uint32_t)kRixTile + (uint32_t)w * (kRixTile / 4);
     bool neg = false;
-    uint32_t wsum = 0, x[kDecRounds];
+    uint32_t wsum = 0;
 #pragma unroll
-    for (int r = 0; r < kDecRounds; ++r) {
+    for (int r = 0; r < kRixRounds5; ++r) {
         const uint32_t k = kw + r * 64 + l;
         const int32_t run = (int32_t)v[r];
         neg |= k < n && run < 0;
-        x[r] = k < n ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
-        const uint32_t s = wave_incl_sum32_sat(x[r]);
-        v[r] = sat_add(wsum, s);  // now: inclusive sum within the wave's pairs
+        const uint32_t x = k < n ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
+        const uint32_t s = wave_incl_sum32_sat(x);
+        v[r] = sat_add(wsum, s);
         wsum = sat_add(wsum, __builtin_amdgcn_readlane(s, 63));
     }
     if (neg) atomicOr(err, kErrNegativeRun);
@@ -176,14 +242,15 @@ __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict
     // 2. the sum over the unit's earlier tiles: look-back
     if (w == 0) {
         unsigned long long* st = status + U.dt_begin;
-        unsigned long long excl = 0;
+        uint32_t excl = 0;
         if (t == 0) {
-            if (l == 0) st_rlx(st, kFlagIncl | tot);
+            if (l == 0) st_rlx(st, granule_e(kFlagIncl, epoch, tot));
         } else {
-            if (l == 0) st_rlx(st + t, kFlagAgg | tot);
-            excl = lookback_sum62(st, (int64_t)t, l, err);
-            excl = excl > 0xffffffffull ? 0xffffffffull : excl;
-            if (l == 0) st_rlx(st + t, kFlagIncl | (unsigned long long)sat_add((uint32_t)excl, tot));
+            if (l == 0) st_rlx(st + t, granule_e(kFlagAgg, epoch, tot));
+#ifndef WC_XP_NOLB
+            excl = lookback_sum32e(st, (int64_t)t, l, err, epoch);
+#endif
+            if (l == 0) st_rlx(st + t, granule_e(kFlagIncl, epoch, sat_add(excl, tot)));
         }
         if (l == 0) s_x[1] = (uint32_t)excl;
     }
@@ -196,21 +263,23 @@ __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict
     // saturating inclusive sum of run + 1; the virtual pair k == n sits at
     // ncoeff), and rhi_{-1} = -1.  Positions at or past ncoeff (< 2^31) clamp
     // to it, so saturated sums give the same rows.  rhi_{k-1} comes from the
-    // lane below (DPP), the previous round's lane 63, or for the wave's first
-    // pair from A (= p_{k-1} + 1): one division per pair, none of them 64-bit
-    // shifts of a second operand.
+    // lane below, the previous round's lane 63, or for the wave's first pair
+    // from A (= p_{k-1} + 1): one division per pair.
     uint2* __restrict__ ri = rowinfo + U.row_off;
     const uint32_t D = (uint32_t)U.nz;
     int32_t carry = A == 0 ? -1 : (int32_t)div_rows(min(A - 1u, nc), U.dmagic);  // rhi of the pair before
 #pragma unroll
-    for (int r = 0; r < kDecRounds; ++r) {
+    for (int r = 0; r < kRixRounds5; ++r) {
         const uint32_t k = kw + r * 64 + l;
         const uint32_t phk = k < n ? min(sat_add(A, v[r]) - 1u, nc) : nc;
         const int32_t rhi = k <= n ? (int32_t)div_rows(phk, U.dmagic) : -1;
-        // rhi of pair k - 1: lane l - 1, the carry in lane 0 (no wave-wide DPP shift on gfx950)
+        // rhi of pair k - 1: lane l - 1, the carry in lane 0
         const int32_t from = __builtin_amdgcn_ds_bpermute((l - 1) << 2, rhi);
         const int32_t rlo = (l == 0 ? carry : from) + 1;
         const uint32_t cnt = (k <= n && rhi >= rlo) ? (uint32_t)(rhi - rlo + 1) : 0u;
+#ifdef WC_XP_NOROWS
+        if (cnt == 12345u)
+#endif
         write_rows(ri, (uint32_t)rlo, cnt, k, phk, D, l);
         carry = __builtin_amdgcn_readlane(rhi, 63);
         if (carry < 0) break;  // uniform: lane 63 is past the virtual pair, so is every later round
@@ -586,7 +655,10 @@ __global__ __launch_bounds__(kThreads) void k_inverse_fast(const float* __restri
 // checked against the range: a malformed payload (reported by K5) gives
 // garbage cells, never an out-of-bounds access.
 #ifndef WC_RIX_ROUNDS
-#define WC_RIX_ROUNDS 24  // 120 VGPRs: still 4 waves per SIMD
+#define WC_RIX_ROUNDS 20  // 128 VGPRs with the x-quad synthesis: 4 waves per SIMD, no spills
+#endif
+#ifndef WC_RIX_F4
+#define WC_RIX_F4 1  // x-quad (16-B) stores where the output allows them
 #endif
 constexpr int kRixRounds = WC_RIX_ROUNDS;  // rounds of 64 pairs prefetched per wave
 
@@ -673,15 +745,51 @@ __device__ __forceinline__ void rix_scatter_round(float* __restrict__ reg, int R
     if (i < cnt && pos < rlen) reg[j * RS + pos] = __uint_as_float(q.y);
 }
 
-__global__ __launch_bounds__(kThreads) void k_inverse_rows(const RTile* __restrict__ tiles, uint32_t ntiles,
+// Inverse of one 2x2x2 block (src/decompressor.cpp:89-156: X, then Y, then Z
+// pairs avg +/- diff): c[sz][sy][sx] -> V[dz][dy][dx].
+__device__ __forceinline__ void synth_block(const float (&c)[2][2][2], float (&V)[2][2][2]) {
+    float X[2][2][2], Y[2][2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            X[s][t][0] = c[s][t][0] + c[s][t][1];
+            X[s][t][1] = c[s][t][0] - c[s][t][1];
+        }
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            Y[s][0][x] = X[s][0][x] + X[s][1][x];
+            Y[s][1][x] = X[s][0][x] - X[s][1][x];
+        }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            V[0][t][x] = Y[0][t][x] + Y[1][t][x];
+            V[1][t][x] = Y[0][t][x] - Y[1][t][x];
+        }
+}
+
+// Tiles of workgroup b: blocked (a contiguous run of ceil(ntiles / G) tiles:
+// consecutive tiles share the payload lines at their range boundaries and the
+// unit's row entries) or strided (b, b + G, ...).
+__global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __restrict__ tiles, uint32_t ntiles,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ offsets,
-                                                         const uint2* __restrict__ rowinfo, float* __restrict__ out) {
+                                                         const uint2* __restrict__ rowinfo, float* __restrict__ out,
+                                                         int blocked) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const uint32_t G = gridDim.x;
-    uint32_t t = blockIdx.x;
-    if (t >= ntiles) return;
+    uint32_t G = gridDim.x, t = blockIdx.x, tend = ntiles;
+    if (blocked) {
+        const uint32_t per = (ntiles + gridDim.x - 1) / gridDim.x;
+        t = blockIdx.x * per;
+        tend = min(ntiles, t + per);
+        G = 1;
+    }
+    if (t >= tend) return;
 
     // prologue: tile t's ranges and pairs in flight, tile t + G's row entries
     RTile T = tiles[t];
@@ -696,7 +804,7 @@ __global__ __launch_bounds__(kThreads) void k_inverse_rows(const RTile* __restri
     RTile T1 = T;
     RixRange R1{0u, 0u, 0u};
     const uint2* pr1 = pr;
-    if (t1 < ntiles) {
+    if (t1 < tend) {
         T1 = tiles[t1];
         pr1 = reinterpret_cast<const uint2*>(payload + offsets[T1.unit] + 20);
         R1 = rix_load_range(T1, rowinfo, w, l);
@@ -732,12 +840,12 @@ __global__ __launch_bounds__(kThreads) void k_inverse_rows(const RTile* __restri
         RixRange R2{0u, 0u, 0u};
         const uint2* pr2 = pr1;
         RixPlan PL1{0u, 0u, 0u};
-        if (t1 < ntiles) {
+        if (t1 < tend) {
             PL1 = rix_plan(T1, R1, l);
 #pragma unroll
             for (int r = 0; r < kRixRounds; ++r)
                 if ((uint32_t)r < PL1.nrounds) q[r] = rix_load_round(pr1, R1, PL1, l, r);
-            if (t2 < ntiles) {
+            if (t2 < tend) {
                 T2 = tiles[t2];
                 pr2 = reinterpret_cast<const uint2*>(payload + offsets[T2.unit] + 20);
                 R2 = rix_load_range(T2, rowinfo, w, l);
@@ -750,75 +858,111 @@ __global__ __launch_bounds__(kThreads) void k_inverse_rows(const RTile* __restri
             const int W = T.W, H = T.H, D = T.D, hx = W >> 1, hz = D >> 1;
             float* __restrict__ dst = out + T.cell_off;
             const int64_t sy = W, sz = (int64_t)W * H;
-            const bool vout = (T.cell_off & 1) == 0;
-            const int ncol = TX * TYv * (hz >> 2);
+            const int64_t lo = (int64_t)(T.bx0 * 2);
 #ifdef WC_XP_NOPHASEC
             if (tid < 0)
 #endif
-            for (int ci = tid; ci < ncol; ci += kThreads) {
-                const int bxl = ci & (TX - 1), rest = ci >> lbx;
-                const int byl = rest % TYv, bq = rest / TYv;
-                const int bx = T.bx0 + bxl, by = T.by0 + byl, bzb = 4 * bq;
-                if (bx >= hx) continue;
-                float c[2][2][2][4];  // [sz][sy][sx][z-block]
+            if (WC_RIX_F4 && TX >= 2 && ((T.cell_off & 3) == 0) && ((W & 3) == 0)) {
+                // two x-blocks x two z-blocks per thread: 16-B x-quad stores
+                const int nq = (TX >> 1) * TYv * (hz >> 1);
+                for (int ci = tid; ci < nq; ci += kThreads) {
+                    const int bp = ci & ((TX >> 1) - 1), rest = ci >> (lbx - 1);
+                    const int byl = rest % TYv, bq = rest / TYv;
+                    const int bxl = 2 * bp, by = T.by0 + byl, bzb = 2 * bq;
+                    if (T.bx0 + bxl >= hx) continue;
+                    float c[2][2][2][2][2];  // [x-block][sz][sy][sx][z-block]
 #pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2)
+                    for (int e = 0; e < 2; ++e)
 #pragma unroll
-                    for (int t3 = 0; t3 < 2; ++t3)
+                        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-                        for (int x = 0; x < 2; ++x) {
-                            const int g = ((x * 2 + t3) << lbx) + bxl;
-                            const float4 v4 = *reinterpret_cast<const float4*>(lds + (g & 3) * WR + (g >> 2) * RS +
-                                                                               byl * D + s2 * hz + bzb);
-                            c[s2][t3][x][0] = v4.x;
-                            c[s2][t3][x][1] = v4.y;
-                            c[s2][t3][x][2] = v4.z;
-                            c[s2][t3][x][3] = v4.w;
+                            for (int t3 = 0; t3 < 2; ++t3)
+#pragma unroll
+                                for (int x = 0; x < 2; ++x) {
+                                    const int g = ((x * 2 + t3) << lbx) + bxl + e;
+                                    const float2 v2 = *reinterpret_cast<const float2*>(
+                                        lds + (g & 3) * WR + (g >> 2) * RS + byl * D + s2 * hz + bzb);
+                                    c[e][s2][t3][x][0] = v2.x;
+                                    c[e][s2][t3][x][1] = v2.y;
+                                }
+#pragma unroll
+                    for (int qb = 0; qb < 2; ++qb) {
+                        float V[2][2][2][2];  // [x-block][dz][dy][dx]
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            float cb[2][2][2];
+#pragma unroll
+                            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                                for (int t3 = 0; t3 < 2; ++t3)
+#pragma unroll
+                                    for (int x = 0; x < 2; ++x) cb[s2][t3][x] = c[e][s2][t3][x][qb];
+                            synth_block(cb, V[e]);
                         }
 #pragma unroll
-                for (int qb = 0; qb < 4; ++qb) {
-                    float X[2][2][2], Y[2][2][2], V[2][2][2];
+                        for (int dz = 0; dz < 2; ++dz)
 #pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                        for (int t3 = 0; t3 < 2; ++t3) {
-                            X[s2][t3][0] = c[s2][t3][0][qb] + c[s2][t3][1][qb];
-                            X[s2][t3][1] = c[s2][t3][0][qb] - c[s2][t3][1][qb];
-                        }
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                        for (int x = 0; x < 2; ++x) {
-                            Y[s2][0][x] = X[s2][0][x] + X[s2][1][x];
-                            Y[s2][1][x] = X[s2][0][x] - X[s2][1][x];
-                        }
-#pragma unroll
-                    for (int t3 = 0; t3 < 2; ++t3)
-#pragma unroll
-                        for (int x = 0; x < 2; ++x) {
-                            V[0][t3][x] = Y[0][t3][x] + Y[1][t3][x];
-                            V[1][t3][x] = Y[0][t3][x] - Y[1][t3][x];
-                        }
-#pragma unroll
-                    for (int dz = 0; dz < 2; ++dz)
-#pragma unroll
-                        for (int dy = 0; dy < 2; ++dy) {
-                            float* p = dst + 2 * (int64_t)bx + sy * (2 * by + dy) + sz * (2 * (bzb + qb) + dz);
+                            for (int dy = 0; dy < 2; ++dy) {
+                                float* p = dst + lo + 2 * bxl + sy * (2 * by + dy) + sz * (2 * (bzb + qb) + dz);
 #ifdef WC_XP_NOSTORE
-                            if (V[dz][dy][0] == 1.2345f)
+                                if (V[0][dz][dy][0] == 1.2345f)
 #endif
-                            if (vout) {
-                                *reinterpret_cast<float2*>(p) = make_float2(V[dz][dy][0], V[dz][dy][1]);
-                            } else {
-                                p[0] = V[dz][dy][0];
-                                p[1] = V[dz][dy][1];
+                                *reinterpret_cast<float4*>(p) =
+                                    make_float4(V[0][dz][dy][0], V[0][dz][dy][1], V[1][dz][dy][0], V[1][dz][dy][1]);
                             }
-                        }
+                    }
+                }
+            } else {
+                const bool vout = (T.cell_off & 1) == 0;
+                const int ncol = TX * TYv * (hz >> 2);
+                for (int ci = tid; ci < ncol; ci += kThreads) {
+                    const int bxl = ci & (TX - 1), rest = ci >> lbx;
+                    const int byl = rest % TYv, bq = rest / TYv;
+                    const int bx = T.bx0 + bxl, by = T.by0 + byl, bzb = 4 * bq;
+                    if (bx >= hx) continue;
+                    float c[2][2][2][4];  // [sz][sy][sx][z-block]
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                        for (int t3 = 0; t3 < 2; ++t3)
+#pragma unroll
+                            for (int x = 0; x < 2; ++x) {
+                                const int g = ((x * 2 + t3) << lbx) + bxl;
+                                const float4 v4 = *reinterpret_cast<const float4*>(lds + (g & 3) * WR + (g >> 2) * RS +
+                                                                                   byl * D + s2 * hz + bzb);
+                                c[s2][t3][x][0] = v4.x;
+                                c[s2][t3][x][1] = v4.y;
+                                c[s2][t3][x][2] = v4.z;
+                                c[s2][t3][x][3] = v4.w;
+                            }
+#pragma unroll
+                    for (int qb = 0; qb < 4; ++qb) {
+                        float cb[2][2][2], V[2][2][2];
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                            for (int t3 = 0; t3 < 2; ++t3)
+#pragma unroll
+                                for (int x = 0; x < 2; ++x) cb[s2][t3][x] = c[s2][t3][x][qb];
+                        synth_block(cb, V);
+#pragma unroll
+                        for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+                            for (int dy = 0; dy < 2; ++dy) {
+                                float* p = dst + 2 * (int64_t)bx + sy * (2 * by + dy) + sz * (2 * (bzb + qb) + dz);
+                                if (vout) {
+                                    *reinterpret_cast<float2*>(p) = make_float2(V[dz][dy][0], V[dz][dy][1]);
+                                } else {
+                                    p[0] = V[dz][dy][0];
+                                    p[1] = V[dz][dy][1];
+                                }
+                            }
+                    }
                 }
             }
         }
         __syncthreads();
-        if (t1 >= ntiles) break;
+        if (t1 >= tend) break;
         T = T1;
         pr = pr1;
         R = R1;
@@ -874,12 +1018,30 @@ __global__ __launch_bounds__(64) void k_rmse_final(const UnitDev* __restrict__ u
 
 // ---------------------------------------------------------------------------
 // Launch wrappers
-hipError_t launch_decode(hipStream_t st, const UnitDev* units, const FTile* ftiles, uint32_t nft,
-                         const FTile* rtiles, uint32_t nrt, const uint8_t* payload, const uint64_t* offsets,
-                         uint32_t* ticket, unsigned long long* status, float* flat, uint2* rowinfo, uint32_t* err,
-                         int ordered) {
-    if (nrt)
-        k_rowindex<<<nrt, kThreads, 0, st>>>(units, rtiles, payload, offsets, ticket, status, rowinfo, err, ordered);
+// Workgroups of a kernel resident at once (persistent grids).
+static uint32_t resident_grid(const void* fn, size_t lds) {
+    int per_cu = 0, ncu = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kThreads, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+    return (uint32_t)per_cu * (uint32_t)ncu;
+}
+
+// K5.  Row-indexed units: the work list (k_rix_items) then the row index over
+// at most nrix_max item slots; both use epoch-tagged granules (istate: the
+// item workgroups' totals, then the row-index tiles' sums at dt_begin).
+// Other units: the dense decode (zeroed ticket / status).
+hipError_t launch_decode(hipStream_t st, const UnitDev* units, int nunits, const FTile* ftiles, uint32_t nft,
+                         uint32_t nrix_max, RixItem* ritems, unsigned long long* istate, uint32_t epoch,
+                         const uint8_t* payload, const uint64_t* offsets, uint32_t* ticket,
+                         unsigned long long* status, float* flat, uint2* rowinfo, uint32_t* err, int ordered) {
+    if (nrix_max) {
+        const uint32_t nb = (uint32_t)(nunits + kThreads - 1) / kThreads;
+        k_rix_items<<<nb, kThreads, 0, st>>>(units, nunits, payload, offsets, ritems, istate, err, epoch);
+        k_rowindex<<<nrix_max, kThreads, 0, st>>>(units, ritems, ticket, payload, istate + nb, rowinfo, err, ordered,
+                                                  epoch);
+    }
     if (nft) k_decode<<<nft, kThreads, 0, st>>>(units, ftiles, payload, offsets, ticket, status, flat, err, ordered);
     return hipGetLastError();
 }
@@ -899,25 +1061,17 @@ static uint32_t rows_grid(size_t lds) {
     static size_t cached_lds = 0;
     static uint32_t cached = 0;
     if (cached_lds != lds || !cached) {
-        int per_cu = 0, ncu = 0, dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_inverse_rows, kThreads, lds) !=
-                hipSuccess ||
-            per_cu < 1)
-            per_cu = 1;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
-            ncu = 256;
-        cached = (uint32_t)per_cu * (uint32_t)ncu;
+        cached = resident_grid((const void*)k_inverse_rows, lds);
         cached_lds = lds;
     }
     return cached;
 }
 
 hipError_t launch_inverse_rows(hipStream_t st, const RTile* tiles, uint32_t ntiles, size_t lds, const uint8_t* payload,
-                               const uint64_t* offsets, const uint2* rowinfo, float* out) {
+                               const uint64_t* offsets, const uint2* rowinfo, float* out, int blocked) {
     if (!ntiles) return hipSuccess;
     const uint32_t grid = std::min(ntiles, rows_grid(lds));
-    k_inverse_rows<<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out);
+    k_inverse_rows<<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out, blocked);
     return hipGetLastError();
 }
 
