@@ -32,7 +32,7 @@ hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, 
 hipError_t launch_transform_fallback(hipStream_t, const void*, int, const UnitDev*, int, const XTile*, size_t, float*,
                                      const unsigned long long*, double);
 hipError_t launch_pack(hipStream_t, const UnitDev*, int, const uint32_t*, const uint8_t*, uint64_t*, uint8_t*);
-hipError_t launch_decode(hipStream_t, const UnitDev*, int, const FTile*, uint32_t, uint32_t, RixItem*,
+hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, const FTile*, uint32_t,
                          unsigned long long*, uint32_t, const uint8_t*, const uint64_t*, uint32_t*,
                          unsigned long long*, float*, uint2*, uint32_t*, int);
 hipError_t launch_inverse_rows(hipStream_t, const RTile*, uint32_t, size_t, const uint8_t*, const uint64_t*,
@@ -67,8 +67,7 @@ struct Plan {
     std::vector<XTile> xtiles;
     std::vector<XTile> ixtiles;  // dense inverse tiles of the non-row-indexed units: [generic | fast]
     std::vector<RTile> rtiles;   // K6r tiles of the row-indexed units
-    std::vector<FTile> ftiles, dtiles;  // dtiles: dense decode blocks
-    uint32_t nrix_items = 0;            // row-index work items at most (sum of ndt over row-indexed units)
+    std::vector<FTile> ftiles, dtiles, rdtiles;  // dtiles: dense decode, rdtiles: row index (K5)
     int rix_lds = kRixLds;              // WC_OPT_RIX_LDS the plan was built with
     int rix_lx = 4;                     // WC_OPT_RIX_TX the plan was built with
     std::vector<uint32_t> eunits, eidx;
@@ -81,7 +80,7 @@ struct Plan {
     uint64_t coef_extent = 0;  // floats of staged coefficient scratch
     size_t lds_gen = 0, lds_fast = 0, lds_inverse = 0;
     size_t state_bytes = 0;    // forward per-call state: 16 | key[n] | tickets[n] | status[netiles]
-    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_eunits, d_ixtiles, d_eidx, d_rtiles;
+    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_eunits, d_ixtiles, d_eidx, d_rtiles, d_rdtiles;
 };
 
 int ceil_log2(int64_t v) {
@@ -117,10 +116,10 @@ struct wc_ctx {
     uint64_t plan_gen = 0;  // bumped whenever get_plan rebuilds the plan
     // scratch (grow-only)
     DevBuf coef, part, errflag, state, flags, rowinfo;
-    // row index (wc_inverse): work items and epoch-tagged look-back granules,
-    // zeroed when allocated and never again (a granule of an earlier call reads
-    // as unpublished); epoch: the call counter they are tagged with
-    DevBuf ritems, istate;
+    // row index (wc_inverse): epoch-tagged look-back granules, zeroed when
+    // allocated and never again (a granule of an earlier call reads as
+    // unpublished); epoch: the call counter they are tagged with
+    DevBuf istate;
     uint32_t epoch = 0;
     // host-path staging
     DevBuf h_cells, h_payload, h_packed, h_offsets, h_poff, h_kept, h_out;
@@ -417,7 +416,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     // one tile more when kFlatTile divides ncoeff (the virtual pair k = nrle
     // that closes its row index, wc_inverse.hip).
     P.dtiles.clear();
-    P.nrix_items = 0;
+    P.rdtiles.clear();
     {
         uint32_t maxt = 0, total = 0;
         for (UnitDev& d : P.units) {
@@ -428,9 +427,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         }
         for (uint32_t t = 0; t < maxt; ++t)
             for (int i = 0; i < n; ++i)
-                if (t < P.units[i].ndt && !P.units[i].rix) P.dtiles.push_back(FTile{(uint32_t)i, t});
-        for (const UnitDev& d : P.units)
-            if (d.rix) P.nrix_items += d.ndt;
+                if (t < P.units[i].ndt) (P.units[i].rix ? P.rdtiles : P.dtiles).push_back(FTile{(uint32_t)i, t});
     }
     P.coef_extent = coef_cursor ? coef_cursor + kFlatTile : 0;  // slack: flat tiles read whole float4 groups
     build_etiles(P, n);
@@ -442,7 +439,8 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         (rc = upload(c, P.d_dtiles, P.dtiles.data(), sizeof(FTile) * P.dtiles.size(), "upload dtiles")) ||
         (rc = upload(c, P.d_eunits, P.eunits.data(), sizeof(uint32_t) * P.eunits.size(), "upload eunits")) ||
         (rc = upload(c, P.d_eidx, P.eidx.data(), sizeof(uint32_t) * P.eidx.size(), "upload eidx")) ||
-        (rc = upload(c, P.d_rtiles, P.rtiles.data(), sizeof(RTile) * P.rtiles.size(), "upload rtiles")))
+        (rc = upload(c, P.d_rtiles, P.rtiles.data(), sizeof(RTile) * P.rtiles.size(), "upload rtiles")) ||
+        (rc = upload(c, P.d_rdtiles, P.rdtiles.data(), sizeof(FTile) * P.rdtiles.size(), "upload rdtiles")))
         return rc;
     // The host vectors back the async copies: finish them before returning.
     hipError_t e = hipStreamSynchronize(c->stream);
@@ -461,8 +459,8 @@ uint64_t decode_tiles(const Plan& P) {
 // tiles of every unit] (zeroed per call).
 size_t decode_state_bytes(const Plan& P) { return round_up(4ull * P.units.size(), 8) + 8ull * decode_tiles(P); }
 
-// Row-index granules: item workgroups' totals | the tiles' sums (at dt_begin).
-size_t istate_bytes(const Plan& P) { return 8ull * ((P.units.size() + kThreads - 1) / kThreads + decode_tiles(P)); }
+// Row-index granules: the tiles' sums (at dt_begin).
+size_t istate_bytes(const Plan& P) { return 8ull * decode_tiles(P); }
 
 // ensure() for buffers whose contents must start zeroed.
 int ensure_zeroed(wc_ctx* c, DevBuf& b, size_t bytes) {
@@ -482,7 +480,6 @@ int ensure_scratch(wc_ctx* c) {
         (rc = ensure(c, c->flags, (P.coef_extent >> kSegShift) + kEmitTile)) ||
         (rc = ensure(c, c->part, sizeof(double) * nft)) ||
         (rc = ensure(c, c->rowinfo, sizeof(uint32_t) * 2 * std::max<uint64_t>(P.rowinfo_entries, 1))) ||
-        (rc = ensure_zeroed(c, c->ritems, sizeof(RixItem) * std::max<uint64_t>(P.nrix_items, 1))) ||
         (rc = ensure_zeroed(c, c->istate, istate_bytes(P))) ||
         (rc = ensure(c, c->state, std::max<size_t>(P.state_bytes, decode_state_bytes(P)))))
         return rc;
@@ -636,7 +633,7 @@ void wc_ctx_destroy(wc_ctx* c) {
                       &c->h_offsets,     &c->h_poff,         &c->h_kept,         &c->h_out,
                       &c->plan.d_units,  &c->plan.d_xtiles,  &c->plan.d_ftiles,  &c->plan.d_dtiles,
                       &c->plan.d_eunits, &c->plan.d_ixtiles, &c->plan.d_eidx, &c->plan.d_rtiles,
-                      &c->rowinfo, &c->ritems, &c->istate};
+                      &c->plan.d_rdtiles, &c->rowinfo, &c->istate};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto& m : c->marks) {
@@ -835,15 +832,14 @@ int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, c
         return hip_fail(c, e, "memset");
     c->epoch = (c->epoch + 1) & kEpochMask;
     if (c->epoch == 0) {  // wrapped: granules of 2^30 calls ago could look current
-        if ((e = hipMemsetAsync(c->istate.p, 0, c->istate.bytes, c->stream)) != hipSuccess ||
-            (e = hipMemsetAsync(c->ritems.p, 0, c->ritems.bytes, c->stream)) != hipSuccess)
+        if ((e = hipMemsetAsync(c->istate.p, 0, c->istate.bytes, c->stream)) != hipSuccess)
             return hip_fail(c, e, "memset");
         c->epoch = 1;
     }
     {
         StageTimer t(c, WC_STAGE_DECODE);
-        e = launch_decode(c->stream, (const UnitDev*)P.d_units.p, n, (const FTile*)P.d_dtiles.p,
-                          (uint32_t)P.dtiles.size(), P.nrix_items, (RixItem*)c->ritems.p,
+        e = launch_decode(c->stream, (const UnitDev*)P.d_units.p, (const FTile*)P.d_dtiles.p,
+                          (uint32_t)P.dtiles.size(), (const FTile*)P.d_rdtiles.p, (uint32_t)P.rdtiles.size(),
                           (unsigned long long*)c->istate.p, c->epoch, d_payload, d_offsets, (uint32_t*)st,
                           (unsigned long long*)(st + round_up(4ull * n, 8)), (float*)c->coef.p, (uint2*)c->rowinfo.p,
                           (uint32_t*)c->errflag.p, c->opt_ordered ? 1 : 0);

@@ -64,19 +64,6 @@ struct RTile {
     int32_t pad;
 };
 
-// Work item of the row index (K5, wc_inverse.hip k_rowindex): pair tile t of
-// a row-indexed unit, written on the device by k_rix_items from the unit's
-// payload header (a unit's tiles are consecutive items, ascending).
-struct RixItem {
-    uint64_t pay;    // byte offset of the unit's payload (offsets[unit])
-    uint32_t unit;
-    uint32_t t;      // pair tile (kRixTile pairs) within the unit
-    uint32_t n;      // pairs of the payload (nrle; 0 when the header is bad)
-    uint32_t bad;    // 1: the header disagrees with the unit (raised by tile 0)
-    uint32_t epoch;  // the wc_inverse call that wrote the item (older items are stale)
-    uint32_t pad;
-};
-
 // LDS layout of a K6r tile: 4 wave regions of TX ranges of RS = TY*D + 4
 // floats, regions 16 floats apart (bank offset), 16-B aligned.
 __host__ __device__ inline int rix_rs(int lby, int D) { return (D << lby) + 4; }

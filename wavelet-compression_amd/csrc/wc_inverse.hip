@@ -107,94 +107,21 @@ __device__ __forceinline__ void write_rows(uint2* __restrict__ ri, uint32_t r_lo
     }
 }
 
-// Work list of the row index: unit u's pair tiles t < min(nrle / kRixTile + 1,
-// ndt) (the tile holding the virtual pair k = nrle closes the table; tiles
-// past floor(ncoeff / kRixTile) hold only dropped pairs) as consecutive items.
-//
-// Workgroup b covers units [256b, 256b + 256): a block scan of the tile
-// counts, a look-back over the earlier workgroups' totals (epoch-tagged
-// granules ist[], no zeroing per call) for the first item, then the items
-// are written cooperatively (consecutive lanes, consecutive items).
-__global__ __launch_bounds__(kThreads) void k_rix_items(const UnitDev* __restrict__ units, int nunits,
-                                                      const uint8_t* __restrict__ payload,
-                                                      const uint64_t* __restrict__ offsets, RixItem* __restrict__ items,
-                                                      unsigned long long* __restrict__ ist, uint32_t* __restrict__ err,
-                                                      uint32_t epoch) {
-    __shared__ uint32_t s_sum[4];
-    __shared__ uint32_t s_max[4];
-    __shared__ uint32_t s_base;
-    __shared__ uint32_t s_excl[kThreads + 1];
-    __shared__ uint32_t s_n[kThreads];
-    __shared__ uint64_t s_off[kThreads];
-    const int tid = threadIdx.x, l = tid & 63;
-    const int u = blockIdx.x * kThreads + tid;
-    uint32_t nt = 0, n = 0;
-    uint64_t off = 0;
-    bool hok = true;
-    if (u < nunits && units[u].rix) {
-        const UnitDev& U = units[u];
-        off = offsets[u];
-        int32_t nrle;
-        hok = read_header(U, payload + off, nrle);
-        n = hok ? (uint32_t)nrle : 0u;
-        nt = min(n / (uint32_t)kRixTile + 1u, U.ndt);
-    }
-    const ScanOut sc = block_scan_sum_max<uint32_t>(nt, 0u, s_sum, s_max);
-    s_excl[tid] = (uint32_t)sc.excl_sum;
-    s_n[tid] = n | (hok ? 0u : 0x80000000u);  // nrle >= 0 fits in 31 bits
-    s_off[tid] = off;
-    const uint32_t T = (uint32_t)sc.total_sum;
-    if (tid == 0) s_excl[kThreads] = T;
-    if (tid < 64) {
-        uint32_t excl = 0;
-        if (blockIdx.x == 0) {
-            if (l == 0) st_rlx(ist, granule_e(kFlagIncl, epoch, T));
-        } else {
-            if (l == 0) st_rlx(ist + blockIdx.x, granule_e(kFlagAgg, epoch, T));
-            excl = lookback_sum32e(ist, (int64_t)blockIdx.x, l, err, epoch);
-            if (l == 0) st_rlx(ist + blockIdx.x, granule_e(kFlagIncl, epoch, excl + T));
-        }
-        if (l == 0) s_base = excl;
-    }
-    __syncthreads();
-    const uint32_t base = s_base;
-    for (uint32_t i = tid; i < T; i += kThreads) {
-        // the LAST thread whose range starts at or before i: its range is the
-        // one holding i (empty ranges before it share its start)
-        int lo = 0;
-#pragma unroll
-        for (int step = kThreads / 2; step >= 1; step >>= 1)
-            if (s_excl[lo + step] <= i) lo += step;
-        const uint32_t nn = s_n[lo];
-        items[base + i] = RixItem{s_off[lo], blockIdx.x * (uint32_t)kThreads + (uint32_t)lo, i - s_excl[lo],
-                                  nn & 0x7fffffffu, nn >> 31, epoch & kEpochMask, 0u};
-    }
-}
-
 // Row index of the row-indexed units.  Only the runs are needed (the values
 // stay in the payload for K6r).  A negative run (malformed; the reference's
 // behaviour is undefined) counts as run 0, so positions never decrease and
 // every row entry is written: K6r never sees a stale or out-of-range entry.
 //
-// One block per item slot: block b works on item b (slots this call did not
-// write hold an earlier epoch: the block exits); tile index from the item (ordered:
-// a unit's items are consecutive, so a tile's look-back waits only on lower
-// block ids, DESIGN.md §Forward progress) or from a per-unit ticket.
-__device__ __forceinline__ void rix_load_runs(const uint8_t* __restrict__ payload, const RixItem& it, int w, int l,
-                                              uint32_t (&v)[kRixRounds5]) {
-    const uint32_t* __restrict__ runs = reinterpret_cast<const uint32_t*>(payload + it.pay + 20);
-    const uint32_t kw = it.t * (uint32_t)kRixTile + (uint32_t)w * (kRixTile / 4);
-#pragma unroll
-    for (int r = 0; r < kRixRounds5; ++r) {
-        const uint32_t k = kw + r * 64 + l;
-        v[r] = k < it.n ? runs[2 * k] : 0u;
-    }
-}
+// One block per pair tile of the plan (rdtiles: interleaved by tile index
+// across units, so a tile's look-back waits only on lower block ids, DESIGN.md
+// §Forward progress; or the tile index from a per-unit ticket); blocks past
+// the payload's pair tiles exit after the header.  The look-back granules are
+// epoch-tagged: no zeroing between calls.
 
 __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict__ units,
-                                                     const RixItem* __restrict__ items,
-                                                     uint32_t* __restrict__ ticket,
+                                                     const FTile* __restrict__ tiles, uint32_t* __restrict__ ticket,
                                                      const uint8_t* __restrict__ payload,
+                                                     const uint64_t* __restrict__ offsets,
                                                      unsigned long long* __restrict__ status,
                                                      uint2* __restrict__ rowinfo, uint32_t* __restrict__ err,
                                                      int ordered, uint32_t epoch) {
@@ -202,18 +129,33 @@ __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict
     __shared__ uint32_t s_x[2];
     const int tid = threadIdx.x, l = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    RixItem it = cst(items)[blockIdx.x];
-    if (it.epoch != (epoch & kEpochMask)) return;  // uniform: no item of this call
-    if (!ordered) {
-        if (tid == 0) s_x[0] = atomicAdd(ticket + it.unit, 1u);
-        __syncthreads();
-        it.t = s_x[0];
-    }
-    const uint32_t u = it.unit, t = it.t, n = it.n;
-    uint32_t v[kRixRounds5];
-    rix_load_runs(payload, it, w, l, v);
+    const FTile ft = cst(tiles)[blockIdx.x];
+    const uint32_t u = ft.unit;
     const UnitDev U = cst(units)[u];  // scalar copy: no reloads after the stores below
-    if (it.bad && t == 0 && tid == 0) atomicOr(err, kErrHeader);
+    const uint8_t* ph = payload + cst(offsets)[u];
+    int32_t nrle;
+    const bool hok = read_header(U, ph, nrle);
+    const uint32_t n = hok ? (uint32_t)nrle : 0u;
+    // tiles up to the one holding the virtual pair k = n (the plan launches
+    // floor(ncoeff / kRixTile) + 1, enough for the first dropped pair)
+    if (ft.index > n / (uint32_t)kRixTile) return;  // uniform
+    uint32_t t = ft.index;
+    if (!ordered) {
+        if (tid == 0) s_x[0] = atomicAdd(ticket + u, 1u);
+        __syncthreads();
+        t = s_x[0];
+    }
+    uint32_t v[kRixRounds5];
+    {
+        const uint32_t* __restrict__ runs = reinterpret_cast<const uint32_t*>(ph + 20);
+        const uint32_t kw = t * (uint32_t)kRixTile + (uint32_t)w * (kRixTile / 4);
+#pragma unroll
+        for (int r = 0; r < kRixRounds5; ++r) {
+            const uint32_t k = kw + r * 64 + l;
+            v[r] = k < n ? runs[2 * k] : 0u;
+        }
+    }
+    if (!hok && t == 0 && tid == 0) atomicOr(err, kErrHeader);
 
     // 1. v = run + 1 (k < n), 0 (k >= n) -> saturating in-wave inclusive sums
     const uint32_t kw = t * (uint32_t)kRixTile + (uint32_t)w * (kRixTile / 4);
@@ -1028,20 +970,16 @@ static uint32_t resident_grid(const void* fn, size_t lds) {
     return (uint32_t)per_cu * (uint32_t)ncu;
 }
 
-// K5.  Row-indexed units: the work list (k_rix_items) then the row index over
-// at most nrix_max item slots; both use epoch-tagged granules (istate: the
-// item workgroups' totals, then the row-index tiles' sums at dt_begin).
-// Other units: the dense decode (zeroed ticket / status).
-hipError_t launch_decode(hipStream_t st, const UnitDev* units, int nunits, const FTile* ftiles, uint32_t nft,
-                         uint32_t nrix_max, RixItem* ritems, unsigned long long* istate, uint32_t epoch,
+// K5.  Row-indexed units: the row index (epoch-tagged granules istate at
+// dt_begin, never zeroed per call).  Other units: the dense decode (zeroed
+// ticket / status).
+hipError_t launch_decode(hipStream_t st, const UnitDev* units, const FTile* ftiles, uint32_t nft,
+                         const FTile* rtiles, uint32_t nrt, unsigned long long* istate, uint32_t epoch,
                          const uint8_t* payload, const uint64_t* offsets, uint32_t* ticket,
                          unsigned long long* status, float* flat, uint2* rowinfo, uint32_t* err, int ordered) {
-    if (nrix_max) {
-        const uint32_t nb = (uint32_t)(nunits + kThreads - 1) / kThreads;
-        k_rix_items<<<nb, kThreads, 0, st>>>(units, nunits, payload, offsets, ritems, istate, err, epoch);
-        k_rowindex<<<nrix_max, kThreads, 0, st>>>(units, ritems, ticket, payload, istate + nb, rowinfo, err, ordered,
-                                                  epoch);
-    }
+    if (nrt)
+        k_rowindex<<<nrt, kThreads, 0, st>>>(units, rtiles, ticket, payload, offsets, istate, rowinfo, err, ordered,
+                                             epoch);
     if (nft) k_decode<<<nft, kThreads, 0, st>>>(units, ftiles, payload, offsets, ticket, status, flat, err, ordered);
     return hipGetLastError();
 }
