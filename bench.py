@@ -67,6 +67,9 @@ def parse(argv=None):
                          "was measured on the same kernel sources")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU/gloo run of the launcher, sharding and reductions (no kernels, no numbers)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="multi-rank rehearsal on a one-GPU box: every rank on device 0, gloo instead of RCCL "
+                         "(the kernels, shards and reductions of --gpus N; the numbers are not a scaling result)")
     return ap.parse_args(argv)
 
 
@@ -116,22 +119,35 @@ def alg_bytes_inverse(cells, kept, nunits):
 class Dist:
     """The rank's view of the job: world, rank, device, barrier, reductions."""
 
-    def __init__(self, plumbing: bool):
+    def __init__(self, plumbing: bool, rehearse: bool = False):
         import torch
         import torch.distributed as dist
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.plumbing = plumbing
+        self.coll_dev = None  # device of the reduction tensors (None: self.dev)
         if plumbing:
             self.dev = torch.device("cpu")
             if self.world > 1:
                 dist.init_process_group("gloo")
+        elif rehearse:
+            if self.world > 1:
+                dist.init_process_group("gloo")
+            torch.cuda.set_device(0)
+            self.dev = torch.device("cuda", 0)
+            self.local = 0
+            self.coll_dev = torch.device("cpu")
         else:
             if self.world > 1:
                 dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
             torch.cuda.set_device(self.local)
             self.dev = torch.device("cuda", self.local)
+
+    def backend(self):
+        import torch.distributed as dist
+        b = dist.get_backend()
+        return "RCCL over xGMI" if b == "nccl" else b
 
     def barrier(self):
         if self.world > 1:
@@ -142,7 +158,7 @@ class Dist:
         if self.world == 1:
             return dict(metrics)
         from wavelet_compression_amd.shard import reduce_metrics
-        return reduce_metrics(metrics, device=self.dev)
+        return reduce_metrics(metrics, device=self.coll_dev or self.dev)
 
     def close(self):
         if self.world > 1:
@@ -447,7 +463,7 @@ def global_hist_leg(args, d: Dist, ctx, b: Batch):
             "quantile": args.hist_quantile, "threshold": res["thresh"], "retained": res["retained"],
             "kept_check": int(m["kept"]) == res["retained"], "kept_fraction": m["kept"] / m["cells"],
             "value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
-            "allreduce": f"{b.capi.HIST_BINS} x u64 over {d.world} rank(s)" + (" (RCCL)" if d.world > 1 else " (none)")}
+            "allreduce": f"{b.capi.HIST_BINS} x u64 over {d.world} rank(s)" + (f" ({d.backend()})" if d.world > 1 else " (none)")}
 
 
 # ---------------------------------------------------------------------------
@@ -566,7 +582,7 @@ def main():
     args.legs_set = set() if args.legs in ("none", "") else set(args.legs.split(","))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
-    d = Dist(args.plumbing)
+    d = Dist(args.plumbing, args.rehearse)
     if args.plumbing:
         out = plumbing_run(args, d)
         if d.rank == 0:

@@ -8,7 +8,7 @@ Reported: wall seconds per mode, input GB/s of -c, units/s, and the CPU
 baseline = oracle transform/threshold/RLE/serialize + xz preset 6 (what the
 reference's compress() does per unit, single thread) on a sample of units.
 
-usage: python tools/bench_cli.py [--scale 1.0] [--ncomp 4] [--out profiles/r01/cli_e2e.json]
+usage: python tools/bench_cli.py [--scale 1.0] [--ncomp 4] [--out profiles/r02/cli_e2e.json]
 """
 from __future__ import annotations
 
@@ -68,8 +68,9 @@ def main():
     ap.add_argument("--ncomp", type=int, default=4)
     ap.add_argument("--keep", type=float, default=0.999)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
-    ap.add_argument("--out", default=str(ROOT / "profiles" / "r01" / "cli_e2e.json"))
+    ap.add_argument("--out", default=str(ROOT / "profiles" / "r02" / "cli_e2e.json"))
     args = ap.parse_args()
+    import wcamd  # noqa: F401  (registers the package as wavelet_compression_amd)
     from oracle import oracle as O
     from wavelet_compression_amd import plotfile as pf
 
