@@ -188,3 +188,28 @@ def test_bench_spawns_ranks_and_merges_one_line(tmp_path):
     for name, sh in out["shards"].items():
         assert sh["cells_total"] == sh["expected_total"], name
         assert sh["rank0_span"][0] == 0 and 0 < sh["rank0_span"][1] < sh["units_total"], name
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_one_gpu(tmp_path):
+    """The driver's multi-GPU bench path on a one-GPU box: `bench.py --gpus 2
+    --rehearse` starts two ranks (gloo, both on device 0) that run the real
+    kernels on their own shards (C5 split by plan_shards) and merge ONE line
+    whose totals cover both ranks."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--rehearse", "--steps", "2",
+                        "--warmup", "1", "--leg-steps", "1", "--legs", "c5", "--no-cpu-baseline"], env=env,
+                       capture_output=True, text=True, timeout=240, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 2048
+    assert out["value"] > 0 and 0.25 < out["kept_fraction"] < 0.35
+    c5 = out["c5"]
+    assert c5["units_total"] == 512 and c5["units_this_rank"] == 256 and c5["cells_total"] == 512 * 128 ** 3
