@@ -33,6 +33,9 @@ EXPORTED = (
 WC_OPT_SPARSE = 12   # sparse coefficient staging in the forward (default 1)
 WC_OPT_ORDERED = 13  # look-back tile index from the launch order (1, default) or per-unit tickets (0)
 WC_OPT_INVERSE_ROWS = 14  # row-indexed inverse of even-dims units (1, default) or dense decode (0)
+WC_OPT_RIX_LDS = 15  # row-indexed inverse: LDS floats per workgroup (default 9216)
+WC_OPT_RIX_TX = 16  # row-indexed inverse: log2 of the tile's x blocks (default 4)
+WC_OPT_RIX_BLOCKED = 17  # row-indexed inverse: contiguous tile runs per workgroup (default 0)
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*).
 STAGES = ("transform", "emit", "decode", "inverse", "rmse", "hist")
