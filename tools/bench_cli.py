@@ -57,7 +57,8 @@ def place(boxes):
 
 
 def digit_free_dir() -> Path:
-    p = Path(tempfile.gettempdir()) / ("wcamd_e2e_" + "".join(random.choice(string.ascii_lowercase) for _ in range(8)))
+    p = Path(tempfile.gettempdir()) / ("wcamd_etoe_" + "".join(random.choice(string.ascii_lowercase) for _ in range(8)))
+    assert not any(ch.isdigit() for ch in str(p)), p  # format_files reads the digits of the WHOLE path
     p.mkdir()
     return p
 
@@ -95,16 +96,22 @@ def main():
         common = [f"datadir={base}/data/", "minfile=plt00100", "maxfile=plt00100", "minlevel=0",
                   f"maxlevel={len(levels) - 1}", f"components={comp}", f"keep={args.keep}"]
 
+        logs = {}
+
         def run(argv):
             t = time.perf_counter()
             r = subprocess.run([str(CLI), *argv], capture_output=True, text=True, timeout=1800)
             dt = time.perf_counter() - t
-            if r.returncode != 0 or "[error]" in r.stderr:
-                raise SystemExit(r.stdout + r.stderr)
-            return dt, r.stdout
+            out = r.stdout + r.stderr
+            logs[argv[-1]] = out[-1500:]
+            if r.returncode != 0 or "[error]" in out:
+                raise SystemExit(out)
+            return dt, out
 
         t_c, _ = run(common + [f"compresseddir={base}/comp/", "-c"])
         xz_bytes = sum(f.stat().st_size for f in (base / "comp").glob("*.xz"))
+        if xz_bytes == 0:
+            raise SystemExit("no .xz files written:\n" + logs["-c"])
         t_d, _ = run([f"compresseddir={base}/comp/", f"out={base}/regen/", "-d"])
         t_e, est = run([*common[:3], "minlevel=0", "maxlevel=0", f"components={comp}", f"keep={args.keep}",
                         f"compresseddir={base}/x/", "-estimate"])
@@ -143,6 +150,7 @@ def main():
             "speedup_vs_cpu_compress": (ncells / t_c) / cpu_cells_s,
             "generate_s": t_gen,
             "estimate_output": [ln for ln in est.splitlines() if "Predicted" in ln],
+            "cli_logs": logs,
         }
         Path(args.out).parent.mkdir(parents=True, exist_ok=True)
         Path(args.out).write_text(json.dumps(res, indent=1) + "\n")
