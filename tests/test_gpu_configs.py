@@ -5,7 +5,9 @@ C1 (configs[0]): the reference's own fixtures tests/plt00074 -> plt00075
     tests/test_host_io.py proves byte-identical to the reference's files, so
     nothing reads /root/reference), level 0, component temp, keep 0.999,
     -estimate through the CLI (src/modes.cpp:209-327): RMSE 0, adjusted loss 0,
-    compressed size = sum of the .xz bytes / the level's raw size per component.
+    compressed size = sum of the .xz bytes / the level's raw size per component;
+    then -c and -d over both fixtures, both levels and components: the
+    regenerated plotfiles are the fixture files byte for byte.
 C3 (configs[2]): the 4-level AMR layout x 4 components (bench_workloads.py,
     SURVEY.md §8(d)), wc_forward -> wc_inverse -> wc_rmse on one GPU through
     the C-ABI; payload bytes and reconstructions bit-exact against the oracle
@@ -79,6 +81,26 @@ def test_c1_estimate_on_reference_fixtures(digit_free_dir):
     assert raw == 262913.5  # the reference fixture's Level_0 (Cell_D_00000 + Cell_H) per component
     assert size == pytest.approx(xz / raw * 100, rel=1e-12)
     assert size == pytest.approx(0.0974, abs=0.002)  # SURVEY §6 (liblzma-version dependent)
+
+    # -c then -d over both fixtures, both levels, both components: the boxes are
+    # constant (3902.4f, 16.0), so the Haar round trip is exact and the
+    # regenerated plotfiles must be the reference's own fixture files byte for
+    # byte (the writer's byte identity: tests/test_host_io.py)
+    import filecmp
+    full = base / "full"
+    _cli(f"datadir={base}/data/", "minfile=plt00074", "maxfile=plt00075", "minlevel=0", "maxlevel=1",
+         "components=temp pressure", "keep=0.999", f"compresseddir={full}/", "-c")
+    _cli(f"compresseddir={full}/", f"out={base}/regen/", "-d")
+    for name in ("plt00074", "plt00075"):
+        want = base / "data" / name
+        n = 0
+        for root, _, files in os.walk(want):
+            for f in files:
+                a = Path(root) / f
+                b = base / "regen" / name / a.relative_to(want)
+                assert filecmp.cmp(a, b, shallow=False), b
+                n += 1
+        assert n == 5  # Header, Level_{0,1}/Cell_H and Level_{0,1}/Cell_D_00000
 
 
 @pytest.fixture(scope="module")
