@@ -13,6 +13,9 @@ the slowest rank's time.
 Legs (sub-objects of the same JSON line):
   inverse  C2's payloads back to cells (rle_decode + inverse transform) and
            the per-box RMSE (calc_rmse_per_box) of the reconstruction
+  host     C2 through the host-buffer boundary (wc_forward_host: pinned host
+           cells over PCIe, packed payloads back to host memory): the
+           PCIe-inclusive rate, reported beside `value`, never as it
   c3       BASELINE configs[2]: 4-level AMR layout x 4 components, fwd + inv +
            RMSE round trip on one GPU (world == 1)
   c5       configs[4]: 512 x 128^3 fp32, keep 0.9999, units split over ranks
@@ -44,7 +47,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-ALL_LEGS = ("inverse", "c3", "c5", "c4")
+ALL_LEGS = ("inverse", "host", "c3", "c5", "c4")
 
 
 def parse(argv=None):
@@ -466,6 +469,28 @@ def global_hist_leg(args, d: Dist, ctx, b: Batch):
             "allreduce": f"{b.capi.HIST_BINS} x u64 over {d.world} rank(s)" + (f" ({d.backend()})" if d.world > 1 else " (none)")}
 
 
+def host_leg(args, d: Dist, ctx, b: Batch):
+    """C2 through wc_forward_host: the cells start in pinned host memory, the
+    packed payloads end in (pageable) host memory; includes both PCIe copies."""
+    import torch
+    pinned = torch.empty(b.cells_dev.numel(), dtype=b.cells_dev.dtype, pin_memory=True)
+    pinned.copy_(b.cells_dev)
+    torch.cuda.synchronize()
+    arr = pinned.numpy()
+    _, offs, _ = ctx.forward_host(arr, b.tab, b.n, b.keep)  # warm-up: host staging buffers
+    steps = max(1, min(args.leg_steps, 5))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        _, offs, _ = ctx.forward_host(arr, b.tab, b.n, b.keep)
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    h2d = arr.nbytes
+    d2h = int(offs[b.n])
+    return {"value": b.ncells / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
+            "h2d_bytes": h2d, "d2h_bytes": d2h, "host_GBps": (h2d + d2h) / (ms * 1e-3) / 1e9,
+            "note": "PCIe-inclusive (pinned host cells in, packed payloads out to host memory), one rank; "
+                    "`value` above is the HBM-resident rate"}
+
+
 # ---------------------------------------------------------------------------
 # CPU baseline (the oracle: checker + reported baseline only)
 
@@ -595,6 +620,8 @@ def main():
     out, b = headline(args, d, ctx)
     if "inverse" in args.legs_set:
         out["inverse"] = inverse_leg(args, d, ctx, b)
+    if "host" in args.legs_set and d.world == 1:
+        out["host"] = host_leg(args, d, ctx, b)
     out["cpu_baseline"] = None
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, b, b.rmse)
