@@ -538,7 +538,7 @@ def test_sparse_staging_special_values(wc, ctx, oracle):
         for idx, v in edits:
             b[idx] = v
         return b
-    s1, s2 = (32, 4, 4), (64, 4, 8)
+    s1, s2, s3 = (32, 4, 4), (64, 4, 8), (64, 16, 64)
     boxes = [
         box(s1, 2.0, [((slice(0, 2), slice(0, 2), slice(0, 2)), np.nan)]),
         box(s1, 2.0, [((31, 3, 3), np.nan)]),
@@ -549,6 +549,12 @@ def test_sparse_staging_special_values(wc, ctx, oracle):
         box(s2, 0.0, [((3, 2, 2), 3.0), ((3, 2, 3), -3.0), ((60, 3, 1), -3.0)]),
         box(s1, np.float32(1e-40), [((9, 1, 1), np.float32(3e-39))]),
         box(s2, 300.0, [((17, 1, 6), -1.0e5)]),
+        # multi-tile units (8 z-tiles of 32 blocks): a negative field whose tiles all
+        # stage densely, with all-NaN segments (stored too: thresh < 0 reads them
+        # all); a positive field with one negative spike (mixed: re-staged)
+        box(s3, -5.0, [((slice(None), slice(0, 2), slice(2, 4)), np.nan)]),
+        box(s3, 7.0, [((slice(None), slice(0, 2), slice(2, 4)), np.nan), ((50, 12, 40), -2.0e4)]),
+        box(s3, -7.0, [((20, 9, 33), 3.0e4)]),
     ]
     for keep in (KEEPS[1], 1.0):
         for path in ("staged", "dense"):

@@ -28,9 +28,9 @@ size_t transform_fast_lds_bytes(int lbx, int lby, int lbz);
 hipError_t launch_transform(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
                             float*, int, unsigned long long*);
 hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
-                                 float*, int, unsigned long long*, uint8_t*, double);
+                                 float*, int, unsigned long long*, uint8_t*, uint32_t*, double);
 hipError_t launch_transform_fallback(hipStream_t, const void*, int, const UnitDev*, int, const XTile*, size_t, float*,
-                                     const unsigned long long*, double);
+                                     const unsigned long long*, const uint32_t*, uint32_t*, uint32_t*, double);
 hipError_t launch_pack(hipStream_t, const UnitDev*, int, const uint32_t*, const uint8_t*, uint64_t*, uint8_t*);
 hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, const FTile*, uint32_t,
                          unsigned long long*, uint32_t, const uint8_t*, const uint64_t*, uint32_t*,
@@ -253,7 +253,9 @@ void build_etiles(Plan& P, int n) {
         total += d.net;
     }
     P.netiles = total;
-    P.state_bytes = round_up(16 + 12ull * n, 8) + 8ull * total;
+    // per-call state: 16 (needy count) | key[n] (u64) | tickets[n] | spos[n] | needy[n] (u32) |
+    // status[tiles] (u64)
+    P.state_bytes = round_up(16 + 20ull * n, 8) + 8ull * total;
     P.eunits.clear();
     P.eidx.clear();
     uint32_t maxt = 0;
@@ -523,6 +525,9 @@ int stage_transform(wc_ctx* c, const void* d_cells, int dtype, double keep, bool
     if ((e = hipMemsetAsync(c->state.p, 0, P.state_bytes, c->stream)) != hipSuccess)
         return hip_fail(c, e, "memset state");
     unsigned long long* key = (unsigned long long*)((uint8_t*)c->state.p + 16);
+    const size_t n = P.units.size();
+    uint32_t* spos = (uint32_t*)((uint8_t*)c->state.p + 16 + 12 * n);
+    uint32_t* needy = (uint32_t*)((uint8_t*)c->state.p + 16 + 16 * n);  // needy[-4 B .. ]: state word 0 counts
     float* coef = (float*)c->coef.p;
     uint8_t* flags = sparse && P.any_sparse ? (uint8_t*)c->flags.p : nullptr;
     {
@@ -530,11 +535,11 @@ int stage_transform(wc_ctx* c, const void* d_cells, int dtype, double keep, bool
         e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, coef, 0, key);
         if (e == hipSuccess)
             e = launch_transform_fast(c->stream, d_cells, dtype, du, dxt + P.ngen, P.nfast, P.lds_fast, coef, 0,
-                                      key, flags, keep);
+                                      key, flags, spos, keep);
         // units whose thresh came out < 0 need every coefficient (rare: negative signed max)
         if (e == hipSuccess && flags)
             e = launch_transform_fallback(c->stream, d_cells, dtype, du, (int)P.units.size(), dxt, P.lds_fast, coef,
-                                          key, keep);
+                                          key, spos, (uint32_t*)c->state.p, needy, keep);
     }
     c->sparse_staged = flags != nullptr;
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "transform launch");
@@ -555,7 +560,7 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
     p.ordered = c->opt_ordered ? 1u : 0u;
     p.key = (const unsigned long long*)(st + 16);
     p.tickets = (uint32_t*)(st + 16 + 8ull * n);
-    p.status = (unsigned long long*)(st + round_up(16 + 12ull * n, 8));
+    p.status = (unsigned long long*)(st + round_up(16 + 20ull * n, 8));
     p.payload = d_payload;
     p.offsets = d_offsets;
     p.kept = d_kept;
@@ -808,7 +813,7 @@ int wc_decompose(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units
     hipError_t e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, d_flat, 1, nullptr);
     if (e == hipSuccess)
         e = launch_transform_fast(c->stream, d_cells, dtype, du, dxt + P.ngen, P.nfast, P.lds_fast, d_flat, 1,
-                                  nullptr, nullptr, 0.0);
+                                  nullptr, nullptr, nullptr, 0.0);
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "transform launch");
 }
 

@@ -767,9 +767,17 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
 #pragma unroll
             for (int r = 0; r < kRixRounds; ++r)
                 if ((uint32_t)r < PL.nrounds) rix_scatter_round(reg, RS, rlen, q[r], R, PL, l, r, carry);
-            // rounds past the prefetch window (dense tiles): load and scatter
-            for (uint32_t rr = kRixRounds; rr < PL.nrounds; ++rr)
-                rix_scatter_round(reg, RS, rlen, rix_load_round(pr, R, PL, l, rr), R, PL, l, rr, carry);
+            // rounds past the prefetch window (dense tiles): batches of
+            // kRixRounds loads in flight together, then their scatters (q is
+            // free until the next tile's prefetch below)
+            for (uint32_t r0 = kRixRounds; r0 < PL.nrounds; r0 += kRixRounds) {
+#pragma unroll
+                for (int r = 0; r < kRixRounds; ++r)
+                    if (r0 + r < PL.nrounds) q[r] = rix_load_round(pr, R, PL, l, r0 + r);
+#pragma unroll
+                for (int r = 0; r < kRixRounds; ++r)
+                    if (r0 + r < PL.nrounds) rix_scatter_round(reg, RS, rlen, q[r], R, PL, l, r0 + r, carry);
+            }
 #else
             if (q[0].x == 77u && q[5].y == 3u) reg[0] = 1.0f;
 #endif

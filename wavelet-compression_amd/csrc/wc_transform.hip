@@ -48,7 +48,7 @@ template <typename T, bool KEYS>
 __global__ __launch_bounds__(kThreads) void k_transform_fast(
     const T* __restrict__ cells, const UnitDev* __restrict__ units, const XTile* __restrict__ tiles,
     float* __restrict__ out, int out_mode, unsigned long long* __restrict__ unit_key,
-    uint8_t* __restrict__ flags, double keep) {
+    uint8_t* __restrict__ flags, uint32_t* __restrict__ spos, double keep) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ unsigned long long s_key[kThreads / kWave];
     __shared__ uint32_t s_mag[kThreads / kWave];
@@ -63,8 +63,10 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
             if ((threadIdx.x & 63) == 0) s_mag[threadIdx.x >> 6] = mag;
             __syncthreads();
             mag = max(max(s_mag[0], s_mag[1]), max(s_mag[2], s_mag[3]));
+            const double bound = sparse_bound(mag, keep);
+            if (threadIdx.x == 0 && bound >= 0.0) atomicOr(spos + td.unit, 1u);  // a sparsely staged tile
             const unsigned long long kmax = xform_fast_p2_sparse(
-                U, td, lds, threadIdx.x, sparse_bound(mag, keep), flags,
+                U, td, lds, threadIdx.x, bound, flags,
                 [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
             block_key_max(kmax, s_key, unit_key + td.unit);
             return;
@@ -89,26 +91,47 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
 
 // Sparse-staged units whose thresh is < 0 (negative signed max, or keep > 1:
 // every coefficient is kept, src/compressor.cpp:216-226) need every
-// coefficient: workgroup u re-stages unit u densely, tile by tile.  Every
-// other workgroup exits after one key load.
+// coefficient; those with a sparsely staged tile (spos: a tile whose own
+// largest magnitude is negative stages densely, so this takes a unit whose
+// tiles disagree in sign) are re-staged densely.  k_fallback_check lists them
+// (workgroup b checks units [256b, 256b + 256), one atomicAdd per wave with
+// any); k_transform_fallback re-stages the listed units, one per workgroup
+// (grid-strided), every workgroup exiting at once when the list is empty.
+__global__ __launch_bounds__(kThreads) void k_fallback_check(const UnitDev* __restrict__ units, int n,
+                                                           const unsigned long long* __restrict__ unit_key,
+                                                           const uint32_t* __restrict__ spos, double keep,
+                                                           uint32_t* __restrict__ count, uint32_t* __restrict__ list) {
+    const int u = blockIdx.x * kThreads + (int)threadIdx.x;
+    const bool need = u < n && spos[u] && key_thresh(unit_key[u], keep) < 0.0;
+    const unsigned long long b = __ballot(need);
+    if (!b) return;  // uniform per wave
+    const int l = threadIdx.x & 63;
+    uint32_t base = 0;
+    if (l == __ffsll((long long)b) - 1) base = atomicAdd(count, (uint32_t)__popcll(b));
+    base = __shfl(base, __ffsll((long long)b) - 1);
+    if (need) list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] =
+        (uint32_t)u;
+}
+
 template <typename T>
 __global__ __launch_bounds__(kThreads) void k_transform_fallback(const T* __restrict__ cells,
                                                                const UnitDev* __restrict__ units,
                                                                const XTile* __restrict__ tiles, float* __restrict__ out,
-                                                               const unsigned long long* __restrict__ unit_key,
-                                                               double keep) {
+                                                               const uint32_t* __restrict__ count,
+                                                               const uint32_t* __restrict__ list) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const UnitDev& U = units[blockIdx.x];
-    if (!U.sparse) return;
-    if (!(key_thresh(unit_key[blockIdx.x], keep) < 0.0)) return;  // uniform
-    float* __restrict__ dst = out + U.coef_off;
-    for (uint32_t t = 0; t < U.ntx; ++t) {
-        const XTile td = tiles[U.xt_begin + t];
-        xform_fast_p1<T>(cells + U.cell_off, U, td, lds, threadIdx.x);
-        __syncthreads();
-        (void)xform_fast_p2<false>(U, td, lds, threadIdx.x,
-                                   [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
-        __syncthreads();
+    const uint32_t cnt = *count;  // written by k_fallback_check (the launch before)
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const UnitDev& U = units[list[i]];
+        float* __restrict__ dst = out + U.coef_off;
+        for (uint32_t t = 0; t < U.ntx; ++t) {
+            const XTile td = tiles[U.xt_begin + t];
+            xform_fast_p1<T>(cells + U.cell_off, U, td, lds, threadIdx.x);
+            __syncthreads();
+            (void)xform_fast_p2<false>(U, td, lds, threadIdx.x,
+                                       [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
+            __syncthreads();
+        }
     }
 }
 
@@ -219,7 +242,7 @@ static uint32_t pf_grid(size_t lds, bool keys) {
 
 hipError_t launch_transform_fast(hipStream_t st, const void* cells, int dtype, const UnitDev* units,
                                  const XTile* tiles, uint32_t ntiles, size_t lds, float* out,
-                                 int out_mode, unsigned long long* keys, uint8_t* flags, double keep) {
+                                 int out_mode, unsigned long long* keys, uint8_t* flags, uint32_t* spos, double keep) {
     if (ntiles == 0) return hipSuccess;
     if (dtype != 1 && !flags) {  // fp32 cells, dense staging: persistent, next tile's cells in flight
         const uint32_t grid = std::min(ntiles, pf_grid(lds, keys != nullptr));
@@ -234,29 +257,31 @@ hipError_t launch_transform_fast(hipStream_t st, const void* cells, int dtype, c
     if (dtype == 1) {
         if (keys)
             k_transform_fast<double, true><<<ntiles, kThreads, lds, st>>>((const double*)cells, units, tiles, out,
-                                                                  out_mode, keys, flags, keep);
+                                                                  out_mode, keys, flags, spos, keep);
         else
             k_transform_fast<double, false><<<ntiles, kThreads, lds, st>>>((const double*)cells, units, tiles, out,
-                                                                  out_mode, keys, flags, keep);
+                                                                  out_mode, keys, flags, spos, keep);
     } else {
         if (keys)
             k_transform_fast<float, true><<<ntiles, kThreads, lds, st>>>((const float*)cells, units, tiles, out,
-                                                                  out_mode, keys, flags, keep);
+                                                                  out_mode, keys, flags, spos, keep);
         else
             k_transform_fast<float, false><<<ntiles, kThreads, lds, st>>>((const float*)cells, units, tiles, out,
-                                                                  out_mode, keys, flags, keep);
+                                                                  out_mode, keys, flags, spos, keep);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_transform_fallback(hipStream_t st, const void* cells, int dtype, const UnitDev* units, int n,
                                      const XTile* tiles, size_t lds, float* out, const unsigned long long* keys,
-                                     double keep) {
+                                     const uint32_t* spos, uint32_t* count, uint32_t* list, double keep) {
     if (n == 0) return hipSuccess;
+    k_fallback_check<<<(n + kThreads - 1) / kThreads, kThreads, 0, st>>>(units, n, keys, spos, keep, count, list);
+    const int grid = std::min(n, 1024);
     if (dtype == 1)
-        k_transform_fallback<double><<<n, kThreads, lds, st>>>((const double*)cells, units, tiles, out, keys, keep);
+        k_transform_fallback<double><<<grid, kThreads, lds, st>>>((const double*)cells, units, tiles, out, count, list);
     else
-        k_transform_fallback<float><<<n, kThreads, lds, st>>>((const float*)cells, units, tiles, out, keys, keep);
+        k_transform_fallback<float><<<grid, kThreads, lds, st>>>((const float*)cells, units, tiles, out, count, list);
     return hipGetLastError();
 }
 

@@ -165,8 +165,9 @@ __device__ __forceinline__ unsigned long long xform_generic_p2(const UnitDev& U,
 // flight, and each of its 8 output rows gets 4 consecutive K -> one 16-B LDS
 // write.  LDS row stride 2*TZ + 4 floats (16-B rows; b128 writes of 8 lanes
 // hit 32 banks).  Keys come from phase 2.
-// MAG: also return the max of this thread's |c| bit patterns (NaN patterns
-// are above +inf's), for the sparse-staging bound.
+// MAG: also return the max of this thread's (|c| bits << 1 | sign) (NaN
+// patterns are above +inf's): the largest magnitude for the sparse-staging
+// bound, and in bit 0 whether some coefficient of that magnitude is negative.
 template <typename T, bool SPLIT = false, bool MAG = false>
 __device__ __forceinline__ uint32_t xform_fast_p1(const T* __restrict__ src, const UnitDev& U,
                                                   const XTile& td, float* lds, int tid) {
@@ -237,7 +238,10 @@ __device__ __forceinline__ uint32_t xform_fast_p1(const T* __restrict__ src, con
                                     c[3][ssz][ssy][ssx]);
                     if constexpr (MAG) {
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) mag = max(mag, __float_as_uint(c[q][ssz][ssy][ssx]) & 0x7fffffffu);
+                        for (int q = 0; q < 4; ++q) {
+                            const uint32_t bits = __float_as_uint(c[q][ssz][ssy][ssx]);
+                            mag = max(mag, (bits << 1) | (bits >> 31));
+                        }
                     }
                 }
     }
@@ -360,15 +364,20 @@ __device__ __forceinline__ unsigned long long xform_fast_p2(const UnitDev& U, co
 
 // Sparse staging (U.sparse: TZ >= 16 blocks per z tile and hz % TZ == 0, so
 // each TZ-coefficient flat segment belongs to one tile and to one aligned
-// group of TZ/4 lanes).  Flag byte of segment s of a unit: (coef_off >> 4) + s,
+// group of TZ/4 lanes).  A tile whose largest magnitude belongs to a negative
+// coefficient stages densely (the unit's signed max may be that coefficient:
+// thresh < 0 keeps everything); the others flag their unit (spos), so only a
+// unit with a negative max AND a sparsely staged tile needs the re-staging
+// fallback.  Flag byte of segment s of a unit: (coef_off >> 4) + s,
 // inside the unit's 16-coefficient index range (coef_off is a multiple of 32).  With m = the tile's max |c| (from phase 1), bound = m * (1 - keep)
 // (fp64, as src/compressor.cpp:216) is <= the unit's thresh whenever
 // thresh >= 0 (|tile max| <= |unit max|), so a segment with no |c| > bound
 // holds no kept coefficient.  A NaN in the tile, or a bound that is not >= 0,
 // flags every segment.  Units whose thresh turns out < 0 (negative signed
 // max: everything kept) are re-staged densely by k_transform_fallback.
-__device__ __forceinline__ double sparse_bound(uint32_t magbits, double keep) {
-    if (magbits > 0x7f800000u) return -1.0;
+__device__ __forceinline__ double sparse_bound(uint32_t magkey, double keep) {
+    const uint32_t magbits = magkey >> 1;
+    if (magbits > 0x7f800000u || (magkey & 1u)) return -1.0;  // NaN in the tile, or a negative max: dense
     const double b = (double)__uint_as_float(magbits) * (1.0 - keep);
     return b >= 0.0 ? b : -1.0;
 }
@@ -405,7 +414,8 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
         const float4 v = *reinterpret_cast<const float4*>(lds + row * rstride + col);
         const bool cand = (double)fabsf(v.x) > bound || (double)fabsf(v.y) > bound ||
                           (double)fabsf(v.z) > bound || (double)fabsf(v.w) > bound;
-        const bool flag = ((__ballot(cand) >> g0) & gmask) != 0;
+        // bound < 0 (dense tile): every segment, all-NaN ones included
+        const bool flag = ((__ballot(cand) >> g0) & gmask) != 0 || !(bound >= 0.0);
         if (flag) st(f, v);
         if ((tid & (glanes - 1)) == 0) flags[(U.coef_off >> kSegShift) + ((uint64_t)f >> lbz)] = flag ? 1 : 0;
         const uint32_t f0 = (uint32_t)f;
