@@ -182,6 +182,17 @@ int wc_rmse(wc_ctx* ctx, const void* d_orig, int dtype, const float* d_regen,
 int wc_rmse_host(wc_ctx* ctx, const void* orig, int dtype, const float* regen,
                  const wc_unit* units, int n, double* rmse);
 
+/* wc_inverse then wc_rmse of the reconstruction against d_orig, fused: the
+ * row-indexed inverse adds each tile's squared differences right after
+ * writing it (the reconstruction is not re-read from HBM).  Same d_out; RMSE
+ * equal to wc_rmse's up to the order of the double sum (a batch with a unit
+ * on the dense decode path runs the two calls).  Replaces the decompress ->
+ * calc_rmse_per_box pair of the reference's -estimate / round-trip
+ * (src/modes.cpp:209-327, src/calc-loss.cpp:12-43). */
+int wc_inverse_rmse(wc_ctx* ctx, const uint8_t* d_payload, const uint64_t* d_offsets,
+                    const wc_unit* units, int n, const void* d_orig, int dtype, float* d_out,
+                    double* d_rmse);
+
 /* Transform only, host pointers (the reference's static wavelet_decompose). */
 int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* units, int n,
                       float* flat);

@@ -343,6 +343,42 @@ def test_rmse(wc, ctx, oracle):
         assert got[i] == pytest.approx(want, rel=1e-12, abs=1e-300), DIMS[i]
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("which", ["rows", "mixed"])
+def test_inverse_rmse_fused(wc, ctx, oracle, dtype, which):
+    """wc_inverse_rmse: the reconstruction byte-equal to wc_inverse's and the
+    per-box RMSE within 1e-12 of the oracle's calc_rmse_per_box on it.  "rows":
+    every unit row-indexed (the fused pass); "mixed": odd dims put units on the
+    dense decode, so the call runs wc_inverse + wc_rmse."""
+    import torch
+    dims = ([(64, 64, 64), (32, 16, 64), (16, 16, 16), (8, 4, 8), (2, 2, 2), (48, 32, 16), (66, 2, 130),
+             (40, 40, 70), (32, 32, 32)] if which == "rows" else DIMS)
+    boxes = synth(oracle, dims, seed0=31)
+    units, n, extent, cells = pack(wc, boxes, dtype)
+    payload, offs, kept = ctx.forward_host(cells, units, n, KEEPS[1])
+    want_regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
+    dev = torch.device("cuda", 0)
+    d_p = torch.from_numpy(payload).to(dev)
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_a = torch.from_numpy(cells).to(dev)
+    d_r = torch.full((extent,), float("nan"), dtype=torch.float32, device=dev)
+    d_rm = torch.full((n,), -1.0, dtype=torch.float64, device=dev)
+    code = wc.capi.WC_F64 if dtype == np.float64 else wc.capi.WC_F32
+    torch.cuda.synchronize()
+    for _ in range(2):  # part[] reused across calls
+        ctx.inverse_rmse(d_p.data_ptr(), d_off.data_ptr(), units, n, d_a.data_ptr(), code, d_r.data_ptr(),
+                         d_rm.data_ptr())
+    ctx.synchronize()
+    regen = d_r.cpu().numpy()
+    got = d_rm.cpu().numpy()
+    for i, b in enumerate(boxes):
+        o = units[i].cell_offset
+        assert regen[o:o + b.size].tobytes() == want_regen[o:o + b.size].tobytes(), dims[i]
+        orig = oracle.narrow(b) if dtype == np.float64 else b.astype(np.float32)
+        want = oracle.rmse(orig, regen[o:o + b.size].reshape(b.shape))
+        assert got[i] == pytest.approx(want, rel=1e-12, abs=1e-300), dims[i]
+
+
 def test_malformed_payload_rejected(wc, ctx, oracle):
     b = synth(oracle, [(8, 8, 8)], seed0=6)[0]
     p = bytearray(oracle_payload(oracle, b, KEEPS[1]))

@@ -28,7 +28,7 @@ EXPORTED = (
     "wc_inverse", "wc_inverse_host", "wc_inverse_flat", "wc_rmse", "wc_version",
     "wc_profile_enable", "wc_profile_read", "wc_set_option", "wc_inverse_flat_host", "wc_rmse_host",
     "wc_decompose_host", "wc_device_count", "wc_forward_stage", "wc_hist_threshold",
-    "wc_forward_emit",
+    "wc_forward_emit", "wc_inverse_rmse",
 )
 WC_OPT_SPARSE = 12   # sparse coefficient staging in the forward (default 1)
 WC_OPT_ORDERED = 13  # look-back tile index from the launch order (1, default) or per-unit tickets (0)
@@ -83,6 +83,7 @@ def load_library() -> ctypes.CDLL:
         "wc_inverse": (i32, [vp, vp, vp, up, i32, vp]),
         "wc_inverse_host": (i32, [vp, vp, vp, up, i32, vp]),
         "wc_inverse_flat": (i32, [vp, vp, up, i32, vp]),
+        "wc_inverse_rmse": (i32, [vp, vp, vp, up, i32, vp, i32, vp, vp]),
         "wc_rmse": (i32, [vp, vp, i32, vp, up, i32, vp]),
         "wc_version": (ctypes.c_char_p, []),
         "wc_profile_enable": (i32, [vp, i32]),
@@ -228,6 +229,13 @@ class Context:
     def inverse(self, d_payload: int, d_offsets: int, units, n: int, d_out: int):
         self._check(self._L.wc_inverse(self._h, ctypes.c_void_p(d_payload), ctypes.c_void_p(d_offsets),
                                        units, n, ctypes.c_void_p(d_out)))
+
+    def inverse_rmse(self, d_payload: int, d_offsets: int, units, n: int, d_orig: int, dtype: int, d_out: int,
+                     d_rmse: int):
+        """inverse + rmse fused (include/wavelet_amd.h wc_inverse_rmse)."""
+        self._check(self._L.wc_inverse_rmse(self._h, ctypes.c_void_p(d_payload), ctypes.c_void_p(d_offsets),
+                                            units, n, ctypes.c_void_p(d_orig), dtype, ctypes.c_void_p(d_out),
+                                            ctypes.c_void_p(d_rmse)))
 
     def inverse_flat(self, d_flat: int, units, n: int, d_out: int):
         self._check(self._L.wc_inverse_flat(self._h, ctypes.c_void_p(d_flat), units, n,

@@ -36,7 +36,7 @@ hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, co
                          unsigned long long*, uint32_t, const uint8_t*, const uint64_t*, uint32_t*,
                          unsigned long long*, float*, uint2*, uint32_t*, int);
 hipError_t launch_inverse_rows(hipStream_t, const RTile*, uint32_t, size_t, const uint8_t*, const uint64_t*,
-                               const uint2*, float*, int);
+                               const uint2*, float*, int, const void*, int, const UnitDev*, int, double*, double*);
 hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const XTile*, uint32_t, size_t, uint32_t,
                           size_t, float*);
 hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDev*, int, const FTile*,
@@ -371,6 +371,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
                 const uint64_t m = (uint64_t(1) << (31 + lg)) / (uint64_t)d.nz + 1;
                 d.dmagic = m | ((uint64_t)(31 + lg) << 32);
             }
+            d.rt_begin = (uint32_t)P.rtiles.size();
             for (int by = 0; by < d.hy; by += 1 << d.ilby)
                 for (int bx = 0; bx < d.hx; bx += 1 << d.ilbx) {
                     RTile r{};
@@ -387,6 +388,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
                     r.tyv = std::min(1 << d.ilby, d.hy - by);
                     P.rtiles.push_back(r);
                 }
+            d.nrt = (uint32_t)P.rtiles.size() - d.rt_begin;
             P.lds_rows = std::max(P.lds_rows, rix_lds_bytes(d));
         }
     }
@@ -480,7 +482,7 @@ int ensure_scratch(wc_ctx* c) {
     int rc;
     if ((rc = ensure(c, c->coef, sizeof(float) * std::max<uint64_t>(P.coef_extent, 1))) ||
         (rc = ensure(c, c->flags, (P.coef_extent >> kSegShift) + kEmitTile)) ||
-        (rc = ensure(c, c->part, sizeof(double) * nft)) ||
+        (rc = ensure(c, c->part, sizeof(double) * std::max<size_t>(nft, 4 * P.rtiles.size()))) ||
         (rc = ensure(c, c->rowinfo, sizeof(uint32_t) * 2 * std::max<uint64_t>(P.rowinfo_entries, 1))) ||
         (rc = ensure_zeroed(c, c->istate, istate_bytes(P))) ||
         (rc = ensure(c, c->state, std::max<size_t>(P.state_bytes, decode_state_bytes(P)))))
@@ -817,15 +819,16 @@ int wc_decompose(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "transform launch");
 }
 
-int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
-               float* d_out) {
-    if (!c) return WC_ERR_INVALID;
-    int rc;
-    if ((rc = validate_units(c, units, n))) return rc;
-    if (n == 0) return WC_OK;
-    if (!d_payload || !d_offsets || !d_out) return fail(c, WC_ERR_INVALID, "null buffer");
-    if ((rc = set_device(c)) || (rc = get_plan(c, units, n)) || (rc = ensure_scratch(c))) return rc;
+}  // extern "C"
+
+namespace {
+
+// wc_inverse, and with orig != null also calc_rmse_per_box fused into the
+// row-indexed inverse (every unit row-indexed; the caller checks).
+int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, int n, float* d_out,
+                 const void* d_orig, int dtype, double* d_rmse) {
     Plan& P = c->plan;
+    int rc = WC_OK;
     hipError_t e;
     // per-call state of the dense decode and of the ticket form: ticket[n] |
     // status[decode tiles] (zeroed).  The row index needs none: its granules
@@ -854,7 +857,8 @@ int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, c
         StageTimer t(c, WC_STAGE_INVERSE);
         e = launch_inverse_rows(c->stream, (const RTile*)P.d_rtiles.p, (uint32_t)P.rtiles.size(), P.lds_rows,
                                 d_payload, d_offsets,
-                                (const uint2*)c->rowinfo.p, d_out, c->opt_rix_blocked ? 1 : 0);
+                                (const uint2*)c->rowinfo.p, d_out, c->opt_rix_blocked ? 1 : 0, d_orig, dtype,
+                                (const UnitDev*)P.d_units.p, n, (double*)c->part.p, d_rmse);
         if (e == hipSuccess)
             e = launch_inverse(c->stream, (const float*)c->coef.p, 0, (const UnitDev*)P.d_units.p,
                                (const XTile*)P.d_ixtiles.p, P.ign, P.lds_inverse, P.ifast, P.lds_fast, d_out);
@@ -862,7 +866,41 @@ int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, c
     if (e != hipSuccess) return hip_fail(c, e, "inverse launch");
     // Malformed payloads surface at the next wc_synchronize (WC_ERR_FORMAT).
     c->err_check_pending = true;
-    return WC_OK;
+    return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
+               float* d_out) {
+    if (!c) return WC_ERR_INVALID;
+    int rc;
+    if ((rc = validate_units(c, units, n))) return rc;
+    if (n == 0) return WC_OK;
+    if (!d_payload || !d_offsets || !d_out) return fail(c, WC_ERR_INVALID, "null buffer");
+    if ((rc = set_device(c)) || (rc = get_plan(c, units, n)) || (rc = ensure_scratch(c))) return rc;
+    return inverse_impl(c, d_payload, d_offsets, n, d_out, nullptr, 0, nullptr);
+}
+
+int wc_inverse_rmse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
+                    const void* d_orig, int dtype, float* d_out, double* d_rmse) {
+    if (!c) return WC_ERR_INVALID;
+    int rc;
+    if ((rc = validate_units(c, units, n))) return rc;
+    if (dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
+    if (n == 0) return WC_OK;
+    if (!d_payload || !d_offsets || !d_out || !d_orig || !d_rmse) return fail(c, WC_ERR_INVALID, "null buffer");
+    if ((rc = set_device(c)) || (rc = get_plan(c, units, n)) || (rc = ensure_scratch(c))) return rc;
+    const Plan& P = c->plan;
+    bool all_rix = true;
+    for (const UnitDev& d : P.units) all_rix &= d.rix != 0 || d.ncells == 0;
+    if (!all_rix) {  // some units decode densely: the two calls, same results
+        if ((rc = inverse_impl(c, d_payload, d_offsets, n, d_out, nullptr, 0, nullptr))) return rc;
+        return wc_rmse(c, d_orig, dtype, d_out, units, n, d_rmse);
+    }
+    return inverse_impl(c, d_payload, d_offsets, n, d_out, d_orig, dtype == WC_F64 ? 1 : 0, d_rmse);
 }
 
 int wc_inverse_flat(wc_ctx* c, const float* d_flat, const wc_unit* units, int n, float* d_out) {

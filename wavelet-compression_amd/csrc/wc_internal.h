@@ -42,6 +42,8 @@ struct UnitDev {
     int32_t rix;            // 1: row-indexed inverse (K5 row index + K6r), 0: dense flat scratch
     int32_t ilbx, ilby;     // log2 of K6r's tile in blocks along x and y (all of z)
     uint64_t row_off;       // first rowinfo entry of the unit (W*H + 1 entries)
+    uint32_t rt_begin;      // first K6r tile of the unit (row-indexed units)
+    uint32_t nrt;           // K6r tiles of the unit
     uint64_t dmagic;        // m | (31 + l) << 32: row = floor(position / D) = (position * m) >> (31 + l)
 };
 

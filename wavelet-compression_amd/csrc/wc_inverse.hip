@@ -602,7 +602,8 @@ __global__ __launch_bounds__(kThreads) void k_inverse_fast(const float* __restri
 #ifndef WC_RIX_F4
 #define WC_RIX_F4 1  // x-quad (16-B) stores where the output allows them
 #endif
-constexpr int kRixRounds = WC_RIX_ROUNDS;  // rounds of 64 pairs prefetched per wave
+constexpr int kRixRounds = WC_RIX_ROUNDS;
+  // rounds of 64 pairs prefetched per wave
 
 // Range info of this lane (range g = w + 4l of tile T, lanes l < TX).
 struct RixRange {
@@ -717,11 +718,19 @@ __device__ __forceinline__ void synth_block(const float (&c)[2][2][2], float (&V
 // Tiles of workgroup b: blocked (a contiguous run of ceil(ntiles / G) tiles:
 // consecutive tiles share the payload lines at their range boundaries and the
 // unit's row entries) or strided (b, b + G, ...).
+// OT (fused calc_rmse_per_box, wc_inverse_rmse): 0 none, 1 fp64 original
+// cells, 2 fp32 original cells.  After the tile's synthesis (barrier), each
+// wave re-reads part of the tile's output (L2-resident, just written) beside
+// the original cells and adds ((float)orig - regen)^2 in double; the wave's
+// sum goes to part[4 * tile + wave] and k_rmse_rows_final sums a unit's in
+// order.  A pass of its own keeps the synthesis' registers untouched.
+template <int OT>
 __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __restrict__ tiles, uint32_t ntiles,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ offsets,
                                                          const uint2* __restrict__ rowinfo, float* __restrict__ out,
-                                                         int blocked) {
+                                                         int blocked, const void* __restrict__ orig,
+                                                         double* __restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     uint32_t G = gridDim.x, t = blockIdx.x, tend = ntiles;
@@ -738,9 +747,10 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
     const uint2* pr = reinterpret_cast<const uint2*>(payload + offsets[T.unit] + 20);
     RixRange R = rix_load_range(T, rowinfo, w, l);
     RixPlan PL = rix_plan(T, R, l);
-    uint2 q[kRixRounds];
+    constexpr int NR = OT ? kRixRounds - 4 : kRixRounds;  // the RMSE pass needs registers
+    uint2 q[NR];
 #pragma unroll
-    for (int r = 0; r < kRixRounds; ++r)
+    for (int r = 0; r < NR; ++r)
         if ((uint32_t)r < PL.nrounds) q[r] = rix_load_round(pr, R, PL, l, r);
     uint32_t t1 = t + G;
     RTile T1 = T;
@@ -765,17 +775,17 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
             uint32_t carry = 0;
 #ifndef WC_XP_NOSCANS
 #pragma unroll
-            for (int r = 0; r < kRixRounds; ++r)
+            for (int r = 0; r < NR; ++r)
                 if ((uint32_t)r < PL.nrounds) rix_scatter_round(reg, RS, rlen, q[r], R, PL, l, r, carry);
             // rounds past the prefetch window (dense tiles): batches of
-            // kRixRounds loads in flight together, then their scatters (q is
+            // NR loads in flight together, then their scatters (q is
             // free until the next tile's prefetch below)
-            for (uint32_t r0 = kRixRounds; r0 < PL.nrounds; r0 += kRixRounds) {
+            for (uint32_t r0 = NR; r0 < PL.nrounds; r0 += NR) {
 #pragma unroll
-                for (int r = 0; r < kRixRounds; ++r)
+                for (int r = 0; r < NR; ++r)
                     if (r0 + r < PL.nrounds) q[r] = rix_load_round(pr, R, PL, l, r0 + r);
 #pragma unroll
-                for (int r = 0; r < kRixRounds; ++r)
+                for (int r = 0; r < NR; ++r)
                     if (r0 + r < PL.nrounds) rix_scatter_round(reg, RS, rlen, q[r], R, PL, l, r0 + r, carry);
             }
 #else
@@ -786,6 +796,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
 
         // 2. prefetch: tile t1's pairs, tile t2's row entries
         const uint32_t t2 = t1 + G;
+        const uint32_t tcur = t;
         RTile T2 = T1;
         RixRange R2{0u, 0u, 0u};
         const uint2* pr2 = pr1;
@@ -793,7 +804,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
         if (t1 < tend) {
             PL1 = rix_plan(T1, R1, l);
 #pragma unroll
-            for (int r = 0; r < kRixRounds; ++r)
+            for (int r = 0; r < NR; ++r)
                 if ((uint32_t)r < PL1.nrounds) q[r] = rix_load_round(pr1, R1, PL1, l, r);
             if (t2 < tend) {
                 T2 = tiles[t2];
@@ -912,11 +923,38 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
             }
         }
         __syncthreads();
+        if constexpr (OT != 0) {  // 4. calc_rmse_per_box over tile t's cells (src/calc-loss.cpp:12-43)
+            const int TX = 1 << T.lbx, txv = min(TX, (T.W >> 1) - T.bx0), ny2 = 2 * T.tyv;
+            const uint32_t nc = (uint32_t)(T.D * ny2) << T.lbx;
+            const int64_t sy = T.W, sz = (int64_t)T.W * T.H;
+            const int64_t lo = T.cell_off + 2 * (int64_t)T.bx0 + 2 * (int64_t)T.by0 * sy;
+            double acc = 0.0;
+            for (uint32_t ci = tid; ci < nc; ci += kThreads) {
+                const int x = (int)(ci & (uint32_t)(TX - 1));
+                if (x >= txv) continue;
+                const uint32_t row = ci >> T.lbx;
+                const int64_t i = lo + 2 * x + sy * (int64_t)(row % (uint32_t)ny2) + sz * (int64_t)(row / (uint32_t)ny2);
+                float o0, o1;
+                if constexpr (OT == 1) {
+                    o0 = (float)((const double*)orig)[i];
+                    o1 = (float)((const double*)orig)[i + 1];
+                } else {
+                    o0 = ((const float*)orig)[i];
+                    o1 = ((const float*)orig)[i + 1];
+                }
+                const float d0 = o0 - out[i], d1 = o1 - out[i + 1];  // float - float, then widened
+                acc += (double)d0 * (double)d0;
+                acc += (double)d1 * (double)d1;
+            }
+            acc = wave_sum(acc);
+            if (l == 0) part[4 * (uint64_t)tcur + w] = acc;
+        }
         if (t1 >= tend) break;
         T = T1;
         pr = pr1;
         R = R1;
         PL = PL1;
+        t = t1;
         t1 = t2;
         T1 = T2;
         pr1 = pr2;
@@ -1007,17 +1045,42 @@ static uint32_t rows_grid(size_t lds) {
     static size_t cached_lds = 0;
     static uint32_t cached = 0;
     if (cached_lds != lds || !cached) {
-        cached = resident_grid((const void*)k_inverse_rows, lds);
+        cached = resident_grid((const void*)k_inverse_rows<0>, lds);
         cached_lds = lds;
     }
     return cached;
 }
 
+// calc_rmse_per_box of the fused form: unit u's K6r tile sums in tile order.
+__global__ __launch_bounds__(64) void k_rmse_rows_final(const UnitDev* __restrict__ units,
+                                                       const double* __restrict__ part, double* __restrict__ rmse) {
+    const UnitDev& U = units[blockIdx.x];
+    double s = 0.0;
+    for (uint32_t i = threadIdx.x; i < 4 * U.nrt; i += 64) s += part[4 * (uint64_t)U.rt_begin + i];
+    s = wave_sum(s);
+    if (threadIdx.x == 0) {
+        const int vol = U.nx * U.ny * U.nz;  // int product, as src/calc-loss.cpp:37
+        rmse[blockIdx.x] = vol > 0 ? sqrt(s / (double)vol) : 0.0;
+    }
+}
+
+// orig == null: the inverse alone; else also calc_rmse_per_box against orig
+// (dtype 1 fp64, 0 fp32) into rmse[n] via part[ntiles].
 hipError_t launch_inverse_rows(hipStream_t st, const RTile* tiles, uint32_t ntiles, size_t lds, const uint8_t* payload,
-                               const uint64_t* offsets, const uint2* rowinfo, float* out, int blocked) {
+                               const uint64_t* offsets, const uint2* rowinfo, float* out, int blocked,
+                               const void* orig, int dtype, const UnitDev* units, int n, double* part, double* rmse) {
     if (!ntiles) return hipSuccess;
     const uint32_t grid = std::min(ntiles, rows_grid(lds));
-    k_inverse_rows<<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out, blocked);
+    if (!orig)
+        k_inverse_rows<0><<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out, blocked, orig,
+                                                       part);
+    else if (dtype == 1)
+        k_inverse_rows<1><<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out, blocked, orig,
+                                                       part);
+    else
+        k_inverse_rows<2><<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out, blocked, orig,
+                                                       part);
+    if (orig) k_rmse_rows_final<<<n, 64, 0, st>>>(units, part, rmse);
     return hipGetLastError();
 }
 
