@@ -14,6 +14,10 @@
 #include "wavelet_amd.h"
 #include "wc_internal.h"
 
+#ifndef WC_RIX_XCD
+#define WC_RIX_XCD 1
+#endif
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -386,12 +390,32 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
                     r.lbx = d.ilbx;
                     r.lby = d.ilby;
                     r.tyv = std::min(1 << d.ilby, d.hy - by);
+                    r.nat = (uint32_t)P.rtiles.size();
                     P.rtiles.push_back(r);
                 }
             d.nrt = (uint32_t)P.rtiles.size() - d.rt_begin;
             P.lds_rows = std::max(P.lds_rows, rix_lds_bytes(d));
         }
     }
+#if WC_RIX_XCD
+    // K6r tile order, XCD-grouped: workgroups b and b + 8 share an XCD (blocks
+    // are dealt round-robin over the 8 XCDs; the persistent grid is a multiple
+    // of 8), so list position p = 8i + x holds tile start_x + i of a contiguous
+    // unit-order run per XCD.  A round of the grid then puts each XCD on a run
+    // of whole units: neighbouring tiles of a unit, whose flat-row ranges share
+    // payload lines and row entries at their ends, read them through one L2.
+    if (P.rtiles.size() > 8) {
+        const size_t T = P.rtiles.size();
+        std::vector<RTile> perm(T);
+        size_t start = 0;
+        for (size_t x = 0; x < 8; ++x) {
+            const size_t cnt = (T - x + 7) / 8;  // positions p == x (mod 8) below T
+            for (size_t i = 0; i < cnt; ++i) perm[8 * i + x] = P.rtiles[start + i];
+            start += cnt;
+        }
+        P.rtiles.swap(perm);
+    }
+#endif
     P.ngen = (uint32_t)gen.size();
     P.nfast = (uint32_t)fast.size();
     for (UnitDev& d : P.units)

@@ -63,7 +63,7 @@ struct RTile {
     int32_t W, H, D;
     int32_t lbx, lby;   // log2 of the tile's blocks along x and y
     int32_t tyv;        // blocks along y in this tile (<= 1 << lby at the unit's edge)
-    int32_t pad;
+    uint32_t nat;       // index in unit order (the fused RMSE's partial-sum slot)
 };
 
 // LDS layout of a K6r tile: 4 wave regions of TX ranges of RS = TY*D + 4

@@ -796,7 +796,6 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
 
         // 2. prefetch: tile t1's pairs, tile t2's row entries
         const uint32_t t2 = t1 + G;
-        const uint32_t tcur = t;
         RTile T2 = T1;
         RixRange R2{0u, 0u, 0u};
         const uint2* pr2 = pr1;
@@ -947,7 +946,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
                 acc += (double)d1 * (double)d1;
             }
             acc = wave_sum(acc);
-            if (l == 0) part[4 * (uint64_t)tcur + w] = acc;
+            if (l == 0) part[4 * (uint64_t)T.nat + w] = acc;
         }
         if (t1 >= tend) break;
         T = T1;
