@@ -66,7 +66,8 @@ def load_library() -> ctypes.CDLL:
             f"{LIB_PATH} is missing: build the HIP extension first "
             "(python -c 'import __graft_entry__ as g; g.build()')")
     _share_torch_runtime()
-    L = ctypes.CDLL(str(LIB_PATH))
+    # WCAMD_LIB: another build of the same library (A/B runs of kernel variants)
+    L = ctypes.CDLL(os.environ.get("WCAMD_LIB") or str(LIB_PATH))
     vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
     up = ctypes.POINTER(WcUnit)
     sigs = {
