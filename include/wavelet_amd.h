@@ -101,13 +101,20 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  *   row-indexed inverse: LDS floats per workgroup (1024..16384) and log2 of the
  *   tile's blocks along x (0..5); y takes the rest of the budget.  Same cells.
  * WC_OPT_RIX_BLOCKED (default 0): each workgroup of the row-indexed inverse
- *   runs a contiguous run of tiles (0: tiles b, b + grid, ...).  Same cells. */
+ *   runs a contiguous run of tiles (0: tiles b, b + grid, ...).  Same cells.
+ * WC_OPT_HOST_CHUNK (default 2^25 cells): wc_forward_host splits a batch of
+ *   more than two such chunks into contiguous unit runs of about this many
+ *   cells (at most 16 runs) and pipelines them: the cells of run r+1 upload
+ *   while run r computes and run r-1's packed payloads download.  Same bytes
+ *   and offsets out; 0 = one run.
+ */
 #define WC_OPT_SPARSE 12
 #define WC_OPT_ORDERED 13
 #define WC_OPT_INVERSE_ROWS 14
 #define WC_OPT_RIX_LDS 15
 #define WC_OPT_RIX_TX 16
 #define WC_OPT_RIX_BLOCKED 17
+#define WC_OPT_HOST_CHUNK 18
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 
 /* Host-side helpers (no device work). */

@@ -597,3 +597,32 @@ def test_sparse_staging_special_values(wc, ctx, oracle):
             got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, path=path)
             for i, b in enumerate(boxes):
                 assert got[i] == oracle.compress_payload(b, keep)[0], (path, keep, i)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_forward_host_pipelined_runs(wc, ctx, oracle, dtype):
+    """wc_forward_host split into pipelined unit runs (WC_OPT_HOST_CHUNK small:
+    many runs, cells uploaded run by run, payloads downloaded run by run)
+    returns the same dense payload bytes, offsets and kept counts as one run,
+    and every unit's payload equals the oracle's; also with gaps between the
+    units' cells."""
+    from wavelet_compression_amd.capi import WC_OPT_HOST_CHUNK
+    keep = KEEPS[1]
+    boxes = synth(oracle, DIMS, seed0=17)
+    rng = np.random.default_rng(5)
+    gaps = np.cumsum([0] + [int(b.size) + int(rng.integers(0, 9)) for b in boxes[:-1]]).tolist()
+    for offsets in (None, gaps):
+        units, n, extent, cells = pack(wc, boxes, dtype, offsets)
+        ctx.set_option(WC_OPT_HOST_CHUNK, 0)
+        p1, o1, k1 = ctx.forward_host(cells, units, n, keep)
+        for chunk in (3000, 40000):
+            ctx.set_option(WC_OPT_HOST_CHUNK, chunk)
+            try:
+                p2, o2, k2 = ctx.forward_host(cells, units, n, keep)
+            finally:
+                ctx.set_option(WC_OPT_HOST_CHUNK, 1 << 25)
+            assert np.array_equal(o1, o2) and np.array_equal(k1[:n], k2[:n]), chunk
+            for i in range(n):
+                assert wc.capi.unit_payload(p2, o2, k2, i) == wc.capi.unit_payload(p1, o1, k1, i), (chunk, i)
+        for i, b in enumerate(boxes):
+            assert wc.capi.unit_payload(p1, o1, k1, i) == oracle_payload(oracle, b.astype(dtype), keep), i

@@ -36,6 +36,7 @@ WC_OPT_INVERSE_ROWS = 14  # row-indexed inverse of even-dims units (1, default) 
 WC_OPT_RIX_LDS = 15  # row-indexed inverse: LDS floats per workgroup (default 9216)
 WC_OPT_RIX_TX = 16  # row-indexed inverse: log2 of the tile's x blocks (default 4)
 WC_OPT_RIX_BLOCKED = 17  # row-indexed inverse: contiguous tile runs per workgroup (default 0)
+WC_OPT_HOST_CHUNK = 18  # wc_forward_host: cells per pipelined unit run (default 2^25, 0 = one run)
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*).
 STAGES = ("transform", "emit", "decode", "inverse", "rmse", "hist")

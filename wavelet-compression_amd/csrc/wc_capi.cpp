@@ -127,6 +127,14 @@ struct wc_ctx {
     uint32_t epoch = 0;
     // host-path staging
     DevBuf h_cells, h_payload, h_packed, h_offsets, h_poff, h_kept, h_out;
+    // wc_forward_host pipeline: copy streams, per-run events, pinned metadata
+    int64_t opt_host_chunk = int64_t(1) << 25;  // WC_OPT_HOST_CHUNK
+    hipStream_t up = nullptr, down = nullptr;
+    std::vector<hipEvent_t> hev;
+    void* pinned = nullptr;
+    size_t pinned_bytes = 0;
+    // plans of earlier batches (most recent last), swapped in when a batch recurs
+    std::vector<Plan> plan_cache;
     // per-kernel event timing (wc_profile_enable / wc_profile_read)
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -308,13 +316,51 @@ bool set_rix_tiling(UnitDev& d, int budget, int max_lx) {
     return true;
 }
 
-// Build (or reuse) the plan for this batch and upload it.
+bool plan_matches(const wc_ctx* c, const Plan& P, const wc_unit* units, int n) {
+    return P.inv_rows == c->opt_inv_rows && P.rix_lds == c->opt_rix_lds && P.rix_lx == c->opt_rix_lx &&
+           (int)P.key.size() == n && (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0);
+}
+
+void free_plan(Plan& P) {
+    DevBuf* bufs[] = {&P.d_units,  &P.d_xtiles, &P.d_ftiles, &P.d_dtiles,  &P.d_eunits,
+                      &P.d_ixtiles, &P.d_eidx,  &P.d_rtiles, &P.d_rdtiles};
+    for (DevBuf* b : bufs) {
+        if (b->p) (void)hipFree(b->p);
+        *b = DevBuf{};
+    }
+}
+
+constexpr size_t kPlanCache = 16;  // earlier plans kept (wc_forward_host's unit runs, alternating batches)
+
+// Build (or reuse) the plan for this batch and upload it.  A batch seen
+// recently swaps its cached plan back in; a new one pushes the current plan
+// into the cache (the oldest cached plan is freed past kPlanCache).
 int get_plan(wc_ctx* c, const wc_unit* units, int n) {
+    if (c->plan_valid && plan_matches(c, c->plan, units, n)) return WC_OK;
+    for (size_t i = 0; i < c->plan_cache.size(); ++i)
+        if (plan_matches(c, c->plan_cache[i], units, n)) {
+            std::swap(c->plan, c->plan_cache[i]);
+            if (!c->plan_valid) {
+                free_plan(c->plan_cache[i]);
+                c->plan_cache.erase(c->plan_cache.begin() + (std::ptrdiff_t)i);
+            }
+            c->plan_valid = true;
+            ++c->plan_gen;
+            return WC_OK;
+        }
+    if (c->plan_valid) {
+        // the new plan is built into the oldest cached plan's buffers (grow-only;
+        // the uploads are ordered after every queued kernel on the stream), or
+        // into fresh ones while the cache fills
+        Plan target{};
+        if (c->plan_cache.size() >= kPlanCache) {
+            target = std::move(c->plan_cache.front());
+            c->plan_cache.erase(c->plan_cache.begin());
+        }
+        c->plan_cache.push_back(std::move(c->plan));
+        c->plan = std::move(target);
+    }
     Plan& P = c->plan;
-    if (c->plan_valid && P.inv_rows == c->opt_inv_rows && P.rix_lds == c->opt_rix_lds &&
-        P.rix_lx == c->opt_rix_lx && (int)P.key.size() == n &&
-        (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0))
-        return WC_OK;
     c->plan_valid = false;
     ++c->plan_gen;
     P.key.assign(units, units + n);
@@ -667,6 +713,11 @@ void wc_ctx_destroy(wc_ctx* c) {
                       &c->plan.d_rdtiles, &c->rowinfo, &c->istate};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
+    for (Plan& P : c->plan_cache) free_plan(P);
+    for (hipEvent_t e : c->hev) (void)hipEventDestroy(e);
+    if (c->up) (void)hipStreamDestroy(c->up);
+    if (c->down) (void)hipStreamDestroy(c->down);
+    if (c->pinned) (void)hipHostFree(c->pinned);
     for (auto& m : c->marks) {
         c->ev_pool.push_back(m.a);
         c->ev_pool.push_back(m.b);
@@ -706,6 +757,10 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
         case WC_OPT_RIX_TX:
             if (value < 0 || value > 5) return fail(c, WC_ERR_INVALID, "WC_OPT_RIX_TX: log2 of 1..32 blocks");
             c->opt_rix_lx = (int)value;
+            return WC_OK;
+        case WC_OPT_HOST_CHUNK:
+            if (value < 0) return fail(c, WC_ERR_INVALID, "WC_OPT_HOST_CHUNK: cells >= 0");
+            c->opt_host_chunk = value;
             return WC_OK;
         default:
             return fail(c, WC_ERR_INVALID, "unknown option");
@@ -1002,29 +1057,117 @@ int wc_forward_host(wc_ctx* c, const void* cells, int dtype, const wc_unit* unit
     if ((rc = set_device(c))) return rc;
     const size_t esz = dtype == WC_F64 ? 8 : 4;
     const uint64_t ext = cells_extent(units, n);
-    if ((rc = ensure(c, c->h_cells, esz * ext)) || (rc = ensure(c, c->h_payload, bound)) ||
-        (rc = ensure(c, c->h_packed, bound)) || (rc = ensure(c, c->h_offsets, sizeof(uint64_t) * (n + 1))) ||
-        (rc = ensure(c, c->h_poff, sizeof(uint64_t) * (n + 1))) || (rc = ensure(c, c->h_kept, 4 * n)))
+
+    // Runs of contiguous units of about opt_host_chunk cells (at most 16),
+    // pipelined: run r's cells upload on `up` while run r-1 computes on the
+    // context stream, and each run's packed payloads download on `down` once
+    // its sizes are known.  The packed layout (== 4 mod 8 offsets) is the same
+    // as one run's.
+    std::vector<int> rb{0};
+    {
+        uint64_t total = 0;
+        for (int i = 0; i < n; ++i) total += (uint64_t)units[i].nx * units[i].ny * units[i].nz;
+        const uint64_t chunk = c->opt_host_chunk > 0 ? std::max<uint64_t>((uint64_t)c->opt_host_chunk, total / 16 + 1)
+                                                     : total + 1;
+        if (total > 2 * chunk) {
+            uint64_t acc = 0;
+            for (int i = 0; i < n; ++i) {
+                acc += (uint64_t)units[i].nx * units[i].ny * units[i].nz;
+                if (acc >= chunk && i + 1 < n) {
+                    rb.push_back(i + 1);
+                    acc = 0;
+                }
+            }
+        }
+        rb.push_back(n);
+    }
+    const int nr = (int)rb.size() - 1;
+    // per run: payload slot base (device), metadata base (pinned): poff[n_r + 1] | kept[n_r]
+    std::vector<uint64_t> pbase(nr + 1, 0);
+    for (int r = 0; r < nr; ++r) pbase[r + 1] = pbase[r] + wc_payload_bound(units + rb[r], rb[r + 1] - rb[r]);
+    const size_t meta_bytes = sizeof(uint64_t) * (size_t)(n + nr) + 4ull * n;
+    if ((rc = ensure(c, c->h_cells, esz * ext)) || (rc = ensure(c, c->h_payload, pbase[nr])) ||
+        (rc = ensure(c, c->h_packed, pbase[nr])) || (rc = ensure(c, c->h_offsets, sizeof(uint64_t) * (n + nr))) ||
+        (rc = ensure(c, c->h_poff, sizeof(uint64_t) * (n + nr))) || (rc = ensure(c, c->h_kept, 4 * n)))
         return rc;
-    hipError_t e = hipMemcpyAsync(c->h_cells.p, cells, esz * ext, hipMemcpyHostToDevice, c->stream);
-    if (e != hipSuccess) return hip_fail(c, e, "cells upload");
-    if ((rc = wc_forward(c, c->h_cells.p, dtype, units, n, keep, (uint8_t*)c->h_payload.p, bound,
-                         (uint64_t*)c->h_offsets.p, (uint32_t*)c->h_kept.p)))
-        return rc;
-    // Pack the slots into a dense buffer before the copy back (offsets stay == 4 mod 8).
-    e = launch_pack(c->stream, (const UnitDev*)c->plan.d_units.p, n, (const uint32_t*)c->h_kept.p,
-                    (const uint8_t*)c->h_payload.p, (uint64_t*)c->h_poff.p, (uint8_t*)c->h_packed.p);
-    if (e != hipSuccess) return hip_fail(c, e, "pack launch");
-    if ((e = hipMemcpyAsync(offsets, c->h_poff.p, sizeof(uint64_t) * (n + 1), hipMemcpyDeviceToHost, c->stream)) !=
-            hipSuccess ||
-        (e = hipMemcpyAsync(kept, c->h_kept.p, 4 * n, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
-        return hip_fail(c, e, "offsets readback");
-    if ((rc = check_kernel_errors(c))) return rc;
-    if ((e = hipMemcpyAsync(payload, c->h_packed.p, offsets[n], hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(c->stream)) != hipSuccess)
-        return hip_fail(c, e, "payload readback");
-    return WC_OK;
+    hipError_t e = hipSuccess;
+    if (c->pinned_bytes < meta_bytes) {
+        if (c->pinned) (void)hipHostFree(c->pinned);
+        c->pinned = nullptr;
+        c->pinned_bytes = 0;
+        if ((e = hipHostMalloc(&c->pinned, meta_bytes, hipHostMallocDefault)) != hipSuccess)
+            return hip_fail(c, e, "pinned metadata");
+        c->pinned_bytes = meta_bytes;
+    }
+    if (nr > 1) {
+        if (!c->up && (e = hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking)) != hipSuccess)
+            return hip_fail(c, e, "upload stream");
+        if (!c->down && (e = hipStreamCreateWithFlags(&c->down, hipStreamNonBlocking)) != hipSuccess)
+            return hip_fail(c, e, "download stream");
+    }
+    while ((int)c->hev.size() < 2 * nr) {
+        hipEvent_t ev;
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(c, e, "event");
+        c->hev.push_back(ev);
+    }
+    uint64_t* pin_poff = (uint64_t*)c->pinned;                   // [n + nr]
+    uint32_t* pin_kept = (uint32_t*)(pin_poff + (n + nr));       // [n]
+    uint8_t* d_cells = (uint8_t*)c->h_cells.p;
+    for (int r = 0; r < nr; ++r) {
+        const int a = rb[r], m = rb[r + 1] - rb[r];
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (int i = a; i < a + m; ++i) {
+            const uint64_t cnt = (uint64_t)units[i].nx * units[i].ny * units[i].nz;
+            if (!cnt) continue;
+            lo = std::min(lo, units[i].cell_offset);
+            hi = std::max(hi, units[i].cell_offset + cnt);
+        }
+        hipStream_t cs = nr > 1 ? c->up : c->stream;
+        if (hi > lo &&
+            (e = hipMemcpyAsync(d_cells + esz * lo, (const uint8_t*)cells + esz * lo, esz * (hi - lo),
+                                hipMemcpyHostToDevice, cs)) != hipSuccess)
+            return hip_fail(c, e, "cells upload");
+        if (nr > 1 && ((e = hipEventRecord(c->hev[2 * r], c->up)) != hipSuccess ||
+                       (e = hipStreamWaitEvent(c->stream, c->hev[2 * r], 0)) != hipSuccess))
+            return hip_fail(c, e, "upload event");
+        uint8_t* pay = (uint8_t*)c->h_payload.p + pbase[r];
+        uint8_t* packed = (uint8_t*)c->h_packed.p + pbase[r];
+        uint64_t* doff = (uint64_t*)c->h_offsets.p + (a + r);
+        uint64_t* dpoff = (uint64_t*)c->h_poff.p + (a + r);
+        uint32_t* dkept = (uint32_t*)c->h_kept.p + a;
+        if ((rc = wc_forward(c, c->h_cells.p, dtype, units + a, m, keep, pay, pbase[r + 1] - pbase[r], doff, dkept)))
+            return rc;
+        // Pack the slots densely (offsets stay == 4 mod 8), sizes to pinned memory.
+        e = launch_pack(c->stream, (const UnitDev*)c->plan.d_units.p, m, dkept, pay, dpoff, packed);
+        if (e != hipSuccess) return hip_fail(c, e, "pack launch");
+        if ((e = hipMemcpyAsync(pin_poff + (a + r), dpoff, sizeof(uint64_t) * (m + 1), hipMemcpyDeviceToHost,
+                                c->stream)) != hipSuccess ||
+            (e = hipMemcpyAsync(pin_kept + a, dkept, 4ull * m, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+            (e = hipEventRecord(c->hev[2 * r + 1], c->stream)) != hipSuccess)
+            return hip_fail(c, e, "sizes readback");
+    }
+    // Each run's packed bytes [4, end) land at R (== 4 mod 8); the next run starts at R + end.
+    uint64_t R = 4;
+    for (int r = 0; r < nr; ++r) {
+        const int a = rb[r], m = rb[r + 1] - rb[r];
+        if ((e = hipEventSynchronize(c->hev[2 * r + 1])) != hipSuccess) return hip_fail(c, e, "sizes sync");
+        const uint64_t* po = pin_poff + (a + r);
+        for (int i = 0; i < m; ++i) {
+            offsets[a + i] = R - 4 + po[i];
+            kept[a + i] = pin_kept[a + i];
+        }
+        const uint64_t span = po[m] - 4;
+        if (R - 4 + po[m] > cap) return fail(c, WC_ERR_INVALID, "payload_capacity");
+        hipStream_t ds = nr > 1 ? c->down : c->stream;
+        if (span && (e = hipMemcpyAsync(payload + R, (const uint8_t*)c->h_packed.p + pbase[r] + 4, span,
+                                        hipMemcpyDeviceToHost, ds)) != hipSuccess)
+            return hip_fail(c, e, "payload readback");
+        R += po[m];
+    }
+    offsets[n] = R - 4;
+    if (nr > 1 && (e = hipStreamSynchronize(c->down)) != hipSuccess) return hip_fail(c, e, "payload readback");
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(c, e, "sync");
+    return check_kernel_errors(c);
 }
 
 int wc_inverse_host(wc_ctx* c, const uint8_t* payload, const uint64_t* offsets, const wc_unit* units, int n,
