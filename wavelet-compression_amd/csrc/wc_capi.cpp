@@ -64,7 +64,7 @@ struct DevBuf {
 //   ixtiles                     the same, fast tiles in reverse unit order (inverse)
 //   ftiles                      kFlatTile flat tiles (RMSE, histogram)
 //   dtiles                      decode blocks, interleaved by tile index across units
-//   eunits, eidx                emit blocks: unit and tile index, interleaved order
+//   edesc                       emit blocks (tile + unit fields), interleaved order
 struct Plan {
     std::vector<wc_unit> key;
     std::vector<UnitDev> units;
@@ -74,7 +74,7 @@ struct Plan {
     std::vector<FTile> ftiles, dtiles, rdtiles;  // dtiles: dense decode, rdtiles: row index (K5)
     int rix_lds = kRixLds;              // WC_OPT_RIX_LDS the plan was built with
     int rix_lx = 4;                     // WC_OPT_RIX_TX the plan was built with
-    std::vector<uint32_t> eunits, eidx;
+    std::vector<EmitDesc> edesc;
     uint32_t ngen = 0, nfast = 0, netiles = 0;
     uint32_t ign = 0, ifast = 0;  // ixtiles split
     bool inv_rows = true;         // WC_OPT_INVERSE_ROWS the plan was built with
@@ -84,7 +84,7 @@ struct Plan {
     uint64_t coef_extent = 0;  // floats of staged coefficient scratch
     size_t lds_gen = 0, lds_fast = 0, lds_inverse = 0;
     size_t state_bytes = 0;    // forward per-call state: 16 | key[n] | tickets[n] | status[netiles]
-    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_eunits, d_ixtiles, d_eidx, d_rtiles, d_rdtiles;
+    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_edesc, d_ixtiles, d_rtiles, d_rdtiles;
 };
 
 int ceil_log2(int64_t v) {
@@ -268,8 +268,7 @@ void build_etiles(Plan& P, int n) {
     // per-call state: 16 (needy count) | key[n] (u64) | tickets[n] | spos[n] | needy[n] (u32) |
     // status[tiles] (u64)
     P.state_bytes = round_up(16 + 20ull * n, 8) + 8ull * total;
-    P.eunits.clear();
-    P.eidx.clear();
+    P.edesc.clear();
     uint32_t maxt = 0;
     for (int i = 0; i < n; ++i) maxt = std::max(maxt, P.units[i].net);
     const uint64_t group_tiles = std::max<uint64_t>(8192, 128ull * maxt);
@@ -287,8 +286,21 @@ void build_etiles(Plan& P, int n) {
         for (uint32_t t = 0; t < gmax; ++t)
             for (int i = g->first; i < g->second; ++i)
                 if (t < P.units[i].net) {
-                    P.eunits.push_back((uint32_t)i);
-                    P.eidx.push_back(t);
+                    const UnitDev& d = P.units[i];
+                    EmitDesc e{};
+                    e.coef_off = d.coef_off;
+                    e.pay_off = d.pay_off;
+                    e.ncells = d.ncells;
+                    e.unit = (uint32_t)i;
+                    e.index = t;
+                    e.et_begin = d.et_begin;
+                    e.net = d.net;
+                    e.nx = d.nx;
+                    e.ny = d.ny;
+                    e.nz = d.nz;
+                    e.sparse = d.sparse;
+                    e.lbz = d.lbz;
+                    P.edesc.push_back(e);
                 }
     }
 }
@@ -322,8 +334,8 @@ bool plan_matches(const wc_ctx* c, const Plan& P, const wc_unit* units, int n) {
 }
 
 void free_plan(Plan& P) {
-    DevBuf* bufs[] = {&P.d_units,  &P.d_xtiles, &P.d_ftiles, &P.d_dtiles,  &P.d_eunits,
-                      &P.d_ixtiles, &P.d_eidx,  &P.d_rtiles, &P.d_rdtiles};
+    DevBuf* bufs[] = {&P.d_units,   &P.d_xtiles, &P.d_ftiles, &P.d_dtiles,
+                      &P.d_edesc,   &P.d_ixtiles, &P.d_rtiles, &P.d_rdtiles};
     for (DevBuf* b : bufs) {
         if (b->p) (void)hipFree(b->p);
         *b = DevBuf{};
@@ -511,8 +523,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         (rc = upload(c, P.d_ixtiles, P.ixtiles.data(), sizeof(XTile) * P.ixtiles.size(), "upload ixtiles")) ||
         (rc = upload(c, P.d_ftiles, P.ftiles.data(), sizeof(FTile) * P.ftiles.size(), "upload ftiles")) ||
         (rc = upload(c, P.d_dtiles, P.dtiles.data(), sizeof(FTile) * P.dtiles.size(), "upload dtiles")) ||
-        (rc = upload(c, P.d_eunits, P.eunits.data(), sizeof(uint32_t) * P.eunits.size(), "upload eunits")) ||
-        (rc = upload(c, P.d_eidx, P.eidx.data(), sizeof(uint32_t) * P.eidx.size(), "upload eidx")) ||
+        (rc = upload(c, P.d_edesc, P.edesc.data(), sizeof(EmitDesc) * P.edesc.size(), "upload edesc")) ||
         (rc = upload(c, P.d_rtiles, P.rtiles.data(), sizeof(RTile) * P.rtiles.size(), "upload rtiles")) ||
         (rc = upload(c, P.d_rdtiles, P.rdtiles.data(), sizeof(FTile) * P.rdtiles.size(), "upload rdtiles")))
         return rc;
@@ -626,8 +637,7 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
     uint8_t* st = (uint8_t*)c->state.p;
     EmitParams p{};
     p.units = (const UnitDev*)P.d_units.p;
-    p.eunits = (const uint32_t*)P.d_eunits.p;
-    p.eidx = (const uint32_t*)P.d_eidx.p;
+    p.edesc = (const EmitDesc*)P.d_edesc.p;
     p.n = n;
     p.ordered = c->opt_ordered ? 1u : 0u;
     p.key = (const unsigned long long*)(st + 16);
@@ -709,7 +719,7 @@ void wc_ctx_destroy(wc_ctx* c) {
                       &c->flags,         &c->h_cells,        &c->h_payload,      &c->h_packed,
                       &c->h_offsets,     &c->h_poff,         &c->h_kept,         &c->h_out,
                       &c->plan.d_units,  &c->plan.d_xtiles,  &c->plan.d_ftiles,  &c->plan.d_dtiles,
-                      &c->plan.d_eunits, &c->plan.d_ixtiles, &c->plan.d_eidx, &c->plan.d_rtiles,
+                      &c->plan.d_edesc, &c->plan.d_ixtiles, &c->plan.d_rtiles,
                       &c->plan.d_rdtiles, &c->rowinfo, &c->istate};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);

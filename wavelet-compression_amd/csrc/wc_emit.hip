@@ -116,27 +116,28 @@ __device__ __forceinline__ void wave_totals(uint32_t kb, int w, int l, uint32_t&
     last = wave_max_u32(kb ? (uint32_t)(w * 2048 + (hb >> 2) * 256 + l * 4 + (hb & 3) + 1) : 0u);
 }
 
-// Unit u's header (src/compressor.cpp:55-80: int32 W, H, D, ncoeff, nrle),
-// kept count and payload offset, once its pair count is known.
-__device__ __forceinline__ void finish_unit(const EmitParams& P, const UnitDev& U, uint32_t u, uint32_t total) {
-    int32_t* hd = reinterpret_cast<int32_t*>(P.payload + U.pay_off);
-    hd[0] = U.nx;
-    hd[1] = U.ny;
-    hd[2] = U.nz;
-    hd[3] = (int32_t)U.ncells;
+// Unit E.unit's header (src/compressor.cpp:55-80: int32 W, H, D, ncoeff,
+// nrle), kept count and payload offset, once its pair count is known.
+__device__ __forceinline__ void finish_unit(const EmitParams& P, const EmitDesc& E, uint32_t total) {
+    const uint32_t u = E.unit;
+    int32_t* hd = reinterpret_cast<int32_t*>(P.payload + E.pay_off);
+    hd[0] = E.nx;
+    hd[1] = E.ny;
+    hd[2] = E.nz;
+    hd[3] = (int32_t)E.ncells;
     hd[4] = (int32_t)total;
     P.kept[u] = total;
-    P.offsets[u] = U.pay_off;
-    if ((int)u == P.n - 1) P.offsets[P.n] = U.pay_off + 20 + 8ull * total;
+    P.offsets[u] = E.pay_off;
+    if ((int)u == P.n - 1) P.offsets[P.n] = E.pay_off + 20 + 8ull * total;
 }
 
 constexpr unsigned long long kMask31 = 0x7fffffffull;
 
 // Threshold + ordered pack of tile `index` of unit `u`.  Thread t = (wave w,
 // lane l) owns elements w*2048 + it*256 + 4l + j, it 0..7.  sm: 16 LDS words.
-__device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __restrict__ coef, uint32_t u,
+__device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __restrict__ coef, const EmitDesc& U,
                                           uint32_t index, uint32_t* sm, uint2* stage, int tid) {
-    const UnitDev& U = P.units[u];
+    const uint32_t u = U.unit;
     const uint32_t et = U.et_begin + index;
     const int w = tid >> 6, l = tid & 63;
     // Sparse staging: this thread's 8 segment flags, loaded before the key.
@@ -224,7 +225,7 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
         if (l == 0) {
             sm[0] = ecnt;
             sm[1] = elast;
-            if (index + 1 == U.net) finish_unit(P, U, u, ecnt + C);  // last tile
+            if (index + 1 == U.net) finish_unit(P, U, ecnt + C);  // last tile
         }
     }
     __syncthreads();
@@ -247,8 +248,8 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
 #ifndef WC_EMIT_MINB
 #define WC_EMIT_MINB 4  // workgroups per CU the register budget is sized for
 #endif
-// One block per emit tile.  Block b packs the tile (eunits[b], eidx[b]) in
-// the ordered form, or the next ticket of unit eunits[b] in the ticket form.
+// One block per emit tile.  Block b packs the tile edesc[b] in the ordered
+// form, or the next ticket of edesc[b]'s unit in the ticket form.
 // The plan lists blocks interleaved by tile index across the units of a
 // group, groups in reverse transform order (wc_capi.cpp build_etiles).
 __global__ __launch_bounds__(kThreads, WC_EMIT_MINB) void k_emit(EmitParams P, const float* __restrict__ coef) {
@@ -256,15 +257,15 @@ __global__ __launch_bounds__(kThreads, WC_EMIT_MINB) void k_emit(EmitParams P, c
     __shared__ uint2 stage_all[kThreads / kWave][256];  // per-wave pair stage (emit_pairs)
     const int tid = threadIdx.x;
     uint2* stage = stage_all[tid >> 6];
-    const uint32_t u = P.eunits[blockIdx.x];
+    const EmitDesc E = P.edesc[blockIdx.x];
     if (P.ordered) {
-        emit_tile(P, coef, u, P.eidx[blockIdx.x], sm, stage, tid);
+        emit_tile(P, coef, E, E.index, sm, stage, tid);
         return;
     }
-    if (tid == 0) sm[16] = atomicAdd(P.tickets + u, 1u);
+    if (tid == 0) sm[16] = atomicAdd(P.tickets + E.unit, 1u);
     __syncthreads();
     const uint32_t index = __builtin_amdgcn_readfirstlane(sm[16]);
-    emit_tile(P, coef, u, index, sm, stage, tid);
+    emit_tile(P, coef, E, index, sm, stage, tid);
 }
 
 hipError_t launch_emit(hipStream_t st, const EmitParams& p, const float* coef, uint32_t netiles) {

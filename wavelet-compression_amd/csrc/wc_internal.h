@@ -91,12 +91,28 @@ constexpr uint32_t kEpochMask = 0x3fffffffu;  // epoch bits of a look-back granu
 constexpr int kEmitTile = 8192;          // coefficients per emit tile (32 per thread)
 
 // Parameter block of k_emit (wc_emit.hip), filled by wc_capi.cpp.
+// An emit block: its tile and every unit field the emit reads, so that a
+// block's first memory round trip (one uniform load) already yields the
+// addresses of its flags, key and coefficients.
+struct EmitDesc {
+    uint64_t coef_off;  // the unit's staged coefficients (UnitDev::coef_off)
+    uint64_t pay_off;   // the unit's payload slot
+    uint64_t ncells;    // W*H*D
+    uint32_t unit;
+    uint32_t index;     // tile index within the unit (the ordered form's)
+    uint32_t et_begin;  // the unit's first look-back granule
+    uint32_t net;       // emit tiles of the unit
+    int32_t nx, ny, nz;
+    uint32_t sparse;    // UnitDev::sparse
+    int32_t lbz;        // log2 of the staged segment length (UnitDev::lbz)
+    uint32_t pad;
+};
+
 struct EmitParams {
     const UnitDev* units;
-    const uint32_t* eunits;        // unit of each emit block (interleaved order)
-    const uint32_t* eidx;          // tile index of each emit block (ordered form)
+    const EmitDesc* edesc;         // emit blocks in launch order (interleaved, wc_capi.cpp build_etiles)
     int n;
-    uint32_t ordered;              // 1: tile index from eidx (dispatch order), 0: from tickets[unit]
+    uint32_t ordered;              // 1: tile index from edesc (dispatch order), 0: from tickets[unit]
     uint32_t* tickets;             // per-unit tile tickets (ticket form), zeroed per call
     const unsigned long long* key; // unit max keys (wc_xform.h coef_key)
     unsigned long long* status;    // decoupled look-back granules, per emit tile, zeroed per call
