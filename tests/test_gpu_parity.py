@@ -626,3 +626,24 @@ def test_forward_host_pipelined_runs(wc, ctx, oracle, dtype):
                 assert wc.capi.unit_payload(p2, o2, k2, i) == wc.capi.unit_payload(p1, o1, k1, i), (chunk, i)
         for i, b in enumerate(boxes):
             assert wc.capi.unit_payload(p1, o1, k1, i) == oracle_payload(oracle, b.astype(dtype), keep), i
+
+
+def test_plan_cache_eviction(wc, ctx, oracle):
+    """More distinct batches than the plan cache holds (16), each twice: plans
+    are swapped back in, evicted, and rebuilt into an evicted plan's buffers;
+    every payload still equals the oracle's, forward and inverse."""
+    keep = KEEPS[1]
+    batches = []
+    for j in range(20):
+        dims = [DIMS[(j + k) % len(DIMS)] for k in range(3)]
+        batches.append(synth(oracle, dims, seed0=100 + j))
+    for rep in range(2):
+        for j, boxes in enumerate(batches):
+            units, n, extent, cells = pack(wc, boxes)
+            payload, offs, kept = ctx.forward_host(cells, units, n, keep)
+            regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
+            for i, b in enumerate(boxes):
+                want = oracle_payload(oracle, b, keep)
+                assert wc.capi.unit_payload(payload, offs, kept, i) == want, (rep, j, i)
+                o = units[i].cell_offset
+                assert regen[o:o + b.size].tobytes() == oracle.decompress_payload(want).ravel().tobytes(), (rep, j, i)
