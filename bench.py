@@ -233,6 +233,17 @@ class Batch:
         return int(self.kept[:self.n].to(self.kept.device).sum().item()) if self.n else 0
 
 
+def new_context(args, d: Dist):
+    """The rank's library context.  Ranks sharing one GPU (--rehearse) use the
+    look-backs' ticket form: the launch-order form assumes one process owns the
+    device's dispatch (DESIGN.md §Forward progress)."""
+    import wcamd
+    ctx = wcamd.capi.Context(d.local)
+    if args.rehearse and d.world > 1:
+        ctx.set_option(wcamd.capi.WC_OPT_ORDERED, 0)
+    return ctx
+
+
 def timed(d: Dist, ctx, step, steps, warmup):
     """Warmup, then EXACTLY `steps` steps bracketed by barrier + synchronize on
     both sides; returns this rank's seconds.  No per-kernel events inside."""
@@ -378,7 +389,7 @@ def round_trip_leg(args, d: Dist, name):
     import wcamd
     spec = bw.WORKLOADS[name]
     units, _ = rank_units(name, d)
-    ctx = wcamd.capi.Context(d.local)
+    ctx = new_context(args, d)
     b = Batch(d, units, spec["dtype"], spec["keep"], inverse=True)
 
     def separate():
@@ -427,7 +438,7 @@ def sharded_forward_leg(args, d: Dist, name, hist=False):
     import wcamd
     spec = bw.WORKLOADS[name]
     units, span = rank_units(name, d)
-    ctx = wcamd.capi.Context(d.local)
+    ctx = new_context(args, d)
     b = Batch(d, units, spec["dtype"], spec["keep"])
     secs = timed(d, ctx, lambda: b.forward(ctx), args.leg_steps, 2)
     st = stage_times(ctx, lambda: b.forward(ctx), args.leg_steps)
@@ -628,7 +639,7 @@ def main():
         return
     import torch
     import wcamd
-    ctx = wcamd.capi.Context(d.local)
+    ctx = new_context(args, d)
     out, b = headline(args, d, ctx)
     if "inverse" in args.legs_set:
         out["inverse"] = inverse_leg(args, d, ctx, b)

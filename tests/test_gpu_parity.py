@@ -647,3 +647,25 @@ def test_plan_cache_eviction(wc, ctx, oracle):
                 assert wc.capi.unit_payload(payload, offs, kept, i) == want, (rep, j, i)
                 o = units[i].cell_offset
                 assert regen[o:o + b.size].tobytes() == oracle.decompress_payload(want).ravel().tobytes(), (rep, j, i)
+
+
+def test_two_contexts_on_one_device(wc, ctx, oracle):
+    """A second live context on the same device switches both to the
+    look-backs' ticket form (the launch-order form assumes one owner of the
+    device's dispatch); payloads and reconstructions stay the oracle's, with
+    both contexts' work in flight on their own streams."""
+    keep = KEEPS[1]
+    boxes = synth(oracle, DIMS, seed0=23)
+    units, n, extent, cells = pack(wc, boxes)
+    other = wc.capi.Context(0)
+    try:
+        for c in (ctx, other, ctx):
+            payload, offs, kept = c.forward_host(cells, units, n, keep)
+            regen = c.inverse_host(payload, offs[:n], units, n, extent)
+            for i, b in enumerate(boxes):
+                want = oracle_payload(oracle, b, keep)
+                assert wc.capi.unit_payload(payload, offs, kept, i) == want, i
+                o = units[i].cell_offset
+                assert regen[o:o + b.size].tobytes() == oracle.decompress_payload(want).ravel().tobytes(), i
+    finally:
+        other.close()

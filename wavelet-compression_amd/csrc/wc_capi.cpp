@@ -23,6 +23,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -103,6 +105,9 @@ struct wc_ctx {
     Plan plan;
     bool plan_valid = false;
     bool opt_ordered = true;  // WC_OPT_ORDERED (see include/wavelet_amd.h)
+    bool force_tickets = false;  // a _host call retrying after a look-back timeout
+    bool timed_out = false;      // the last error was a look-back wait that timed out
+    bool registered = false;     // counted in g_dev_ctx
     bool opt_sparse = true;   // WC_OPT_SPARSE
     bool opt_inv_rows = true; // WC_OPT_INVERSE_ROWS
     int opt_rix_lds = kRixLds; // WC_OPT_RIX_LDS
@@ -577,6 +582,22 @@ int set_device(wc_ctx* c) {
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "hipSetDevice");
 }
 
+// Live contexts per device, process-wide.  The look-backs' launch-order form
+// (WC_OPT_ORDERED 1) assumes the kernel owns the device's dispatch: with two
+// contexts' kernels in flight on one device, each can fill an XCD with blocks
+// that wait on blocks of its own kernel that the other's occupancy keeps from
+// being dispatched.  Contexts sharing a device therefore use the per-unit
+// tickets (blocks wait only on tiles that running blocks hold).
+std::mutex g_dev_mu;
+std::map<int, int> g_dev_ctx;
+
+bool use_ordered(const wc_ctx* c) {
+    if (!c->opt_ordered || c->force_tickets) return false;
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    auto it = g_dev_ctx.find(c->device);
+    return it == g_dev_ctx.end() || it->second <= 1;
+}
+
 // Surface an error bit a kernel raised (malformed payload in the decode, a
 // look-back wait that timed out) at the next synchronisation point, and clear
 // the word.  The reference exits on a malformed payload
@@ -594,7 +615,10 @@ int check_kernel_errors(wc_ctx* c) {
         std::snprintf(buf, sizeof buf, "malformed payload (flags 0x%x: 1 header, 2 negative run)", flag);
         return fail(c, WC_ERR_FORMAT, buf);
     }
-    if (flag & kErrTimeout) return fail(c, WC_ERR_HIP, "a dependency wait between workgroups timed out");
+    if (flag & kErrTimeout) {
+        c->timed_out = true;
+        return fail(c, WC_ERR_HIP, "a dependency wait between workgroups timed out");
+    }
     return WC_OK;
 }
 
@@ -639,7 +663,7 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
     p.units = (const UnitDev*)P.d_units.p;
     p.edesc = (const EmitDesc*)P.d_edesc.p;
     p.n = n;
-    p.ordered = c->opt_ordered ? 1u : 0u;
+    p.ordered = use_ordered(c) ? 1u : 0u;
     p.key = (const unsigned long long*)(st + 16);
     p.tickets = (uint32_t*)(st + 16 + 8ull * n);
     p.status = (unsigned long long*)(st + round_up(16 + 20ull * n, 8));
@@ -707,12 +731,21 @@ int wc_ctx_create(int device, wc_ctx** out) {
         wc_ctx_destroy(c);
         return WC_ERR_NOMEM;
     }
+    {
+        std::lock_guard<std::mutex> lk(g_dev_mu);
+        ++g_dev_ctx[device];
+        c->registered = true;
+    }
     *out = c;
     return WC_OK;
 }
 
 void wc_ctx_destroy(wc_ctx* c) {
     if (!c) return;
+    if (c->registered) {
+        std::lock_guard<std::mutex> lk(g_dev_mu);
+        --g_dev_ctx[c->device];
+    }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->coef,          &c->part,           &c->errflag,        &c->state,
@@ -924,7 +957,7 @@ int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets,
     // carry the call's epoch.  The dense coefficient scratch is fully written
     // by the decode (no memset).
     uint8_t* st = (uint8_t*)c->state.p;
-    if ((!P.dtiles.empty() || !c->opt_ordered) &&
+    if ((!P.dtiles.empty() || !use_ordered(c)) &&
         (e = hipMemsetAsync(st, 0, decode_state_bytes(P), c->stream)) != hipSuccess)
         return hip_fail(c, e, "memset");
     c->epoch = (c->epoch + 1) & kEpochMask;
@@ -939,7 +972,7 @@ int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets,
                           (uint32_t)P.dtiles.size(), (const FTile*)P.d_rdtiles.p, (uint32_t)P.rdtiles.size(),
                           (unsigned long long*)c->istate.p, c->epoch, d_payload, d_offsets, (uint32_t*)st,
                           (unsigned long long*)(st + round_up(4ull * n, 8)), (float*)c->coef.p, (uint2*)c->rowinfo.p,
-                          (uint32_t*)c->errflag.p, c->opt_ordered ? 1 : 0);
+                          (uint32_t*)c->errflag.p, use_ordered(c) ? 1 : 0);
     }
     if (e != hipSuccess) return hip_fail(c, e, "decode launch");
     {
@@ -1054,9 +1087,8 @@ int wc_profile_read(wc_ctx* c, double* total_ms, uint32_t* launches, int nstages
 
 // ---- host-pointer variants -------------------------------------------------
 
-int wc_forward_host(wc_ctx* c, const void* cells, int dtype, const wc_unit* units, int n, double keep,
-                    uint8_t* payload, uint64_t cap, uint64_t* offsets, uint32_t* kept) {
-    if (!c) return WC_ERR_INVALID;
+static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_unit* units, int n, double keep,
+                             uint8_t* payload, uint64_t cap, uint64_t* offsets, uint32_t* kept) {
     int rc;
     if ((rc = validate_units(c, units, n))) return rc;
     if (dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
@@ -1180,9 +1212,8 @@ int wc_forward_host(wc_ctx* c, const void* cells, int dtype, const wc_unit* unit
     return check_kernel_errors(c);
 }
 
-int wc_inverse_host(wc_ctx* c, const uint8_t* payload, const uint64_t* offsets, const wc_unit* units, int n,
-                    float* out) {
-    if (!c) return WC_ERR_INVALID;
+static int inverse_host_once(wc_ctx* c, const uint8_t* payload, const uint64_t* offsets, const wc_unit* units,
+                             int n, float* out) {
     int rc;
     if ((rc = validate_units(c, units, n))) return rc;
     if (n == 0) return WC_OK;
@@ -1220,6 +1251,37 @@ int wc_inverse_host(wc_ctx* c, const uint8_t* payload, const uint64_t* offsets, 
     }
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(c, e, "sync");
     return check_kernel_errors(c);
+}
+
+// The host-buffer entry points own their inputs until they return, so a
+// launch-order look-back that timed out (another process's kernels holding the
+// dispatch slots its predecessors need, DESIGN.md §Forward progress) is run
+// again once with the per-unit tickets, which need no dispatch order.
+extern "C++" {
+template <class F>
+static int with_ticket_retry(wc_ctx* c, F once) {
+    c->timed_out = false;
+    int rc = once();
+    if (rc == WC_ERR_HIP && c->timed_out && !c->force_tickets) {
+        c->force_tickets = true;
+        rc = once();
+        c->force_tickets = false;
+    }
+    return rc;
+}
+}
+
+int wc_forward_host(wc_ctx* c, const void* cells, int dtype, const wc_unit* units, int n, double keep,
+                    uint8_t* payload, uint64_t cap, uint64_t* offsets, uint32_t* kept) {
+    if (!c) return WC_ERR_INVALID;
+    return with_ticket_retry(
+        c, [&] { return forward_host_once(c, cells, dtype, units, n, keep, payload, cap, offsets, kept); });
+}
+
+int wc_inverse_host(wc_ctx* c, const uint8_t* payload, const uint64_t* offsets, const wc_unit* units, int n,
+                    float* out) {
+    if (!c) return WC_ERR_INVALID;
+    return with_ticket_retry(c, [&] { return inverse_host_once(c, payload, offsets, units, n, out); });
 }
 
 // Stage host arrays through the context's staging buffers for the
