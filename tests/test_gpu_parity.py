@@ -669,3 +669,31 @@ def test_two_contexts_on_one_device(wc, ctx, oracle):
                 assert regen[o:o + b.size].tobytes() == oracle.decompress_payload(want).ravel().tobytes(), i
     finally:
         other.close()
+
+
+def test_forward_host_runs_with_empty_units(wc, ctx, oracle):
+    """Pipelined host runs (WC_OPT_HOST_CHUNK small) over a batch with empty
+    units at its start, between boxes and at its end: the same bytes and
+    offsets as one run; empty units serialize as a bare header."""
+    from wavelet_compression_amd.capi import WC_OPT_HOST_CHUNK
+    keep = KEEPS[1]
+    real = synth(oracle, DIMS[:12], seed0=31)
+    empty = np.zeros((0, 4, 4), np.float64)
+    boxes = [empty] + [x for b in real for x in (b, empty)] + [empty, empty]
+    units, n, extent, cells = pack(wc, boxes)
+    ctx.set_option(WC_OPT_HOST_CHUNK, 0)
+    p1, o1, k1 = ctx.forward_host(cells, units, n, keep)
+    ctx.set_option(WC_OPT_HOST_CHUNK, 2000)
+    try:
+        p2, o2, k2 = ctx.forward_host(cells, units, n, keep)
+    finally:
+        ctx.set_option(WC_OPT_HOST_CHUNK, 1 << 25)
+    assert np.array_equal(o1, o2) and np.array_equal(k1[:n], k2[:n])
+    for i, b in enumerate(boxes):
+        got = wc.capi.unit_payload(p2, o2, k2, i)
+        assert got == wc.capi.unit_payload(p1, o1, k1, i), i
+        if b.size == 0:
+            D, H, W = b.shape
+            assert got == np.array([W, H, D, 0, 0], "<i4").tobytes(), i
+        else:
+            assert got == oracle_payload(oracle, b, keep), i
