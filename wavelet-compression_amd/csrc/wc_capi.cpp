@@ -47,7 +47,7 @@ hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const 
                           size_t, float*);
 hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDev*, int, const FTile*,
                        uint32_t, double*, double*);
-hipError_t launch_emit(hipStream_t, const EmitParams&, const float*, uint32_t);
+hipError_t launch_emit(hipStream_t, const EmitParams&, const float*, uint32_t, uint32_t);
 hipError_t launch_hist(hipStream_t, const UnitDev*, const FTile*, uint32_t, const float*, uint32_t,
                        unsigned long long*);
 }  // namespace wc
@@ -76,7 +76,8 @@ struct Plan {
     std::vector<FTile> ftiles, dtiles, rdtiles;  // dtiles: dense decode, rdtiles: row index (K5)
     int rix_lds = kRixLds;              // WC_OPT_RIX_LDS the plan was built with
     int rix_lx = 4;                     // WC_OPT_RIX_TX the plan was built with
-    std::vector<EmitDesc> edesc;
+    std::vector<EmitDesc> edesc;  // [units of kEmitTile tiles | units of kEmitTileBig tiles]
+    uint32_t nedesc_small = 0;
     uint32_t ngen = 0, nfast = 0, netiles = 0;
     uint32_t ign = 0, ifast = 0;  // ixtiles split
     bool inv_rows = true;         // WC_OPT_INVERSE_ROWS the plan was built with
@@ -262,11 +263,13 @@ uint64_t round_up(uint64_t v, uint64_t m) { return (v + m - 1) / m * m; }
 // coefficients K1 wrote last, which may still be in the Infinity Cache.
 // Measured: 1024 x 64^3 emit 0.346 -> 0.327 ms.
 void build_etiles(Plan& P, int n) {
+    auto big = [](const UnitDev& d) { return d.ncells >= kEmitBigCells; };
     uint32_t total = 0;
     for (int i = 0; i < n; ++i) {
         UnitDev& d = P.units[i];
+        const uint64_t tile = big(d) ? kEmitTileBig : kEmitTile;
         d.et_begin = total;
-        d.net = (uint32_t)std::max<uint64_t>(1, (d.ncells + kEmitTile - 1) / kEmitTile);
+        d.net = (uint32_t)std::max<uint64_t>(1, (d.ncells + tile - 1) / tile);
         total += d.net;
     }
     P.netiles = total;
@@ -274,24 +277,30 @@ void build_etiles(Plan& P, int n) {
     // status[tiles] (u64)
     P.state_bytes = round_up(16 + 20ull * n, 8) + 8ull * total;
     P.edesc.clear();
-    uint32_t maxt = 0;
-    for (int i = 0; i < n; ++i) maxt = std::max(maxt, P.units[i].net);
-    const uint64_t group_tiles = std::max<uint64_t>(8192, 128ull * maxt);
-    std::vector<std::pair<int, int>> groups;  // unit ranges [i0, i1)
-    for (int i0 = 0; i0 < n;) {
-        uint64_t tiles = 0;
-        int i1 = i0;
-        while (i1 < n && tiles < group_tiles) tiles += P.units[i1++].net;
-        groups.emplace_back(i0, i1);
-        i0 = i1;
-    }
-    for (auto g = groups.rbegin(); g != groups.rend(); ++g) {
-        uint32_t gmax = 0;
-        for (int i = g->first; i < g->second; ++i) gmax = std::max(gmax, P.units[i].net);
-        for (uint32_t t = 0; t < gmax; ++t)
-            for (int i = g->first; i < g->second; ++i)
-                if (t < P.units[i].net) {
+    P.nedesc_small = 0;
+    for (int cls = 0; cls < 2; ++cls) {  // one launch per tile size: small units, then big ones
+        std::vector<int> us;
+        for (int i = 0; i < n; ++i)
+            if (big(P.units[i]) == (cls == 1)) us.push_back(i);
+        uint32_t maxt = 0;
+        for (int i : us) maxt = std::max(maxt, P.units[i].net);
+        const uint64_t group_tiles = std::max<uint64_t>(cls ? 4096 : 8192, 128ull * maxt);
+        std::vector<std::pair<size_t, size_t>> groups;  // ranges [g0, g1) of us
+        for (size_t g0 = 0; g0 < us.size();) {
+            uint64_t tiles = 0;
+            size_t g1 = g0;
+            while (g1 < us.size() && tiles < group_tiles) tiles += P.units[us[g1++]].net;
+            groups.emplace_back(g0, g1);
+            g0 = g1;
+        }
+        for (auto g = groups.rbegin(); g != groups.rend(); ++g) {
+            uint32_t gmax = 0;
+            for (size_t k = g->first; k < g->second; ++k) gmax = std::max(gmax, P.units[us[k]].net);
+            for (uint32_t t = 0; t < gmax; ++t)
+                for (size_t k = g->first; k < g->second; ++k) {
+                    const int i = us[k];
                     const UnitDev& d = P.units[i];
+                    if (t >= d.net) continue;
                     EmitDesc e{};
                     e.coef_off = d.coef_off;
                     e.pay_off = d.pay_off;
@@ -307,6 +316,8 @@ void build_etiles(Plan& P, int n) {
                     e.lbz = d.lbz;
                     P.edesc.push_back(e);
                 }
+        }
+        if (cls == 0) P.nedesc_small = (uint32_t)P.edesc.size();
     }
 }
 
@@ -567,7 +578,7 @@ int ensure_scratch(wc_ctx* c) {
     const size_t nft = P.ftiles.size();
     int rc;
     if ((rc = ensure(c, c->coef, sizeof(float) * std::max<uint64_t>(P.coef_extent, 1))) ||
-        (rc = ensure(c, c->flags, (P.coef_extent >> kSegShift) + kEmitTile)) ||
+        (rc = ensure(c, c->flags, (P.coef_extent >> kSegShift) + kEmitTileBig)) ||
         (rc = ensure(c, c->part, sizeof(double) * std::max<size_t>(nft, 4 * P.rtiles.size()))) ||
         (rc = ensure(c, c->rowinfo, sizeof(uint32_t) * 2 * std::max<uint64_t>(P.rowinfo_entries, 1))) ||
         (rc = ensure_zeroed(c, c->istate, istate_bytes(P))) ||
@@ -678,7 +689,8 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
     }
     p.flags = (c->sparse_staged && !gthresh) ? (const uint8_t*)c->flags.p : nullptr;
     StageTimer t(c, WC_STAGE_EMIT);
-    hipError_t e = launch_emit(c->stream, p, (const float*)c->coef.p, P.netiles);
+    hipError_t e = launch_emit(c->stream, p, (const float*)c->coef.p, P.nedesc_small,
+                               (uint32_t)P.edesc.size() - P.nedesc_small);
     if (e != hipSuccess) return hip_fail(c, e, "emit launch");
     c->err_check_pending = true;  // a look-back wait that timed out surfaces at wc_synchronize
     return WC_OK;

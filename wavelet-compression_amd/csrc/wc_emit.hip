@@ -135,8 +135,10 @@ constexpr unsigned long long kMask31 = 0x7fffffffull;
 
 // Threshold + ordered pack of tile `index` of unit `u`.  Thread t = (wave w,
 // lane l) owns elements w*2048 + it*256 + 4l + j, it 0..7.  sm: 16 LDS words.
+template <int EW>
 __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __restrict__ coef, const EmitDesc& U,
                                           uint32_t index, uint32_t* sm, uint2* stage, int tid) {
+    constexpr uint32_t kTile = EW * 2048;
     const uint32_t u = U.unit;
     const uint32_t et = U.et_begin + index;
     const int w = tid >> 6, l = tid & 63;
@@ -145,7 +147,7 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
     uint32_t segf = 0xffu;  // bit it: group it may hold kept coefficients
     if (sparse) {
         // one flag byte per segment of TZ = 2^lbz coefficients (16 or 32)
-        const uint8_t* fl = P.flags + (U.coef_off >> kSegShift) + (((uint64_t)index * kEmitTile) >> U.lbz);
+        const uint8_t* fl = P.flags + (U.coef_off >> kSegShift) + (((uint64_t)index * kTile) >> U.lbz);
         const int sh = U.lbz;
         segf = 0;
 #pragma unroll
@@ -153,8 +155,8 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
     }
     // the unit key: a finished earlier launch wrote it, one uniform load
     const float tf = unit_thresh(P, P.key[u]);
-    const uint32_t start = index * (uint32_t)kEmitTile;
-    const uint32_t len = (uint32_t)min((uint64_t)kEmitTile, U.ncells - start);
+    const uint32_t start = index * kTile;
+    const uint32_t len = (uint32_t)min((uint64_t)kTile, U.ncells - start);
 
     // 1. coefficients -> keep bits (bit it*4 + j).  The flat scratch is 16-B
     // aligned per unit with kFlatTile slack past the last unit.  Sparse units
@@ -172,7 +174,7 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
     wave_totals(kb, w, l, wcnt, wlast);
     if (l == 0) {
         sm[4 + w] = wcnt;
-        sm[8 + w] = wlast;
+        sm[4 + EW + w] = wlast;
     }
     __syncthreads();
 
@@ -180,9 +182,9 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
     if (w == 0) {
         uint32_t C = 0, L = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < EW; ++i) {
             C += sm[4 + i];
-            L = sm[8 + i] > L ? sm[8 + i] : L;
+            L = sm[4 + EW + i] > L ? sm[4 + EW + i] : L;
         }
         const uint32_t L1 = L ? start + L : 0u;  // unit-relative last kept + 1
         uint32_t ecnt = 0, elast = 0;            // exclusive: pairs before, last kept + 1 before
@@ -237,7 +239,7 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
     uint32_t prev = sm[1] - 1u;
     for (int i = 0; i < w; ++i) {
         rank += sm[4 + i];
-        if (sm[8 + i]) prev = start + sm[8 + i] - 1u;
+        if (sm[4 + EW + i]) prev = start + sm[4 + EW + i] - 1u;
     }
     uint2* __restrict__ pairs = reinterpret_cast<uint2*>(P.payload + U.pay_off + 20);
     emit_pairs(q, kb, start, w, l, rank, prev, pairs, stage);
@@ -248,28 +250,37 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
 #ifndef WC_EMIT_MINB
 #define WC_EMIT_MINB 4  // workgroups per CU the register budget is sized for
 #endif
-// One block per emit tile.  Block b packs the tile edesc[b] in the ordered
-// form, or the next ticket of edesc[b]'s unit in the ticket form.
-// The plan lists blocks interleaved by tile index across the units of a
-// group, groups in reverse transform order (wc_capi.cpp build_etiles).
-__global__ __launch_bounds__(kThreads, WC_EMIT_MINB) void k_emit(EmitParams P, const float* __restrict__ coef) {
+// One block per emit tile (EW waves: EW * 2048 coefficients).  Block b packs
+// the tile edesc[b] in the ordered form, or the next ticket of edesc[b]'s unit
+// in the ticket form.  The plan lists blocks interleaved by tile index across
+// the units of a group, groups in reverse transform order (wc_capi.cpp
+// build_etiles); units of kEmitBigCells or more cells form the 8-wave launch.
+template <int EW>
+__global__ __launch_bounds__(EW * kWave, WC_EMIT_MINB * 4 / EW) void k_emit(EmitParams P,
+                                                                           const float* __restrict__ coef) {
     __shared__ __attribute__((aligned(16))) uint32_t sm[32];
-    __shared__ uint2 stage_all[kThreads / kWave][256];  // per-wave pair stage (emit_pairs)
+    __shared__ uint2 stage_all[EW][256];  // per-wave pair stage (emit_pairs)
     const int tid = threadIdx.x;
     uint2* stage = stage_all[tid >> 6];
     const EmitDesc E = P.edesc[blockIdx.x];
     if (P.ordered) {
-        emit_tile(P, coef, E, E.index, sm, stage, tid);
+        emit_tile<EW>(P, coef, E, E.index, sm, stage, tid);
         return;
     }
-    if (tid == 0) sm[16] = atomicAdd(P.tickets + E.unit, 1u);
+    if (tid == 0) sm[31] = atomicAdd(P.tickets + E.unit, 1u);
     __syncthreads();
-    const uint32_t index = __builtin_amdgcn_readfirstlane(sm[16]);
-    emit_tile(P, coef, E, index, sm, stage, tid);
+    const uint32_t index = __builtin_amdgcn_readfirstlane(sm[31]);
+    emit_tile<EW>(P, coef, E, index, sm, stage, tid);
 }
 
-hipError_t launch_emit(hipStream_t st, const EmitParams& p, const float* coef, uint32_t netiles) {
-    if (netiles) k_emit<<<netiles, kThreads, 0, st>>>(p, coef);
+hipError_t launch_emit(hipStream_t st, const EmitParams& p, const float* coef, uint32_t nsmall, uint32_t nbig) {
+    static_assert(kEmitTile == 4 * 2048 && kEmitTileBig == 8 * 2048, "emit tile sizes");
+    if (nsmall) k_emit<4><<<nsmall, 4 * kWave, 0, st>>>(p, coef);
+    if (nbig) {
+        EmitParams q = p;
+        q.edesc = p.edesc + nsmall;
+        k_emit<8><<<nbig, 8 * kWave, 0, st>>>(q, coef);
+    }
     return hipGetLastError();
 }
 

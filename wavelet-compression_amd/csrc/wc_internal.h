@@ -88,7 +88,9 @@ constexpr uint32_t kErrTimeout = 8u;     // a look-back wait between workgroups 
 
 constexpr uint32_t kEpochMask = 0x3fffffffu;  // epoch bits of a look-back granule (wc_device.h granule_e)
 
-constexpr int kEmitTile = 8192;          // coefficients per emit tile (32 per thread)
+constexpr int kEmitTile = 8192;          // coefficients per emit tile (4 waves, 32 per thread)
+constexpr int kEmitTileBig = 16384;      // emit tile of units of >= kEmitBigCells (8 waves)
+constexpr uint64_t kEmitBigCells = uint64_t(1) << 21;  // 128^3: longer tiles pay
 
 // Parameter block of k_emit (wc_emit.hip), filled by wc_capi.cpp.
 // An emit block: its tile and every unit field the emit reads, so that a
