@@ -36,7 +36,7 @@ hipError_t launch_transform(hipStream_t, const void*, int, const UnitDev*, const
 hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
                                  float*, int, unsigned long long*, uint8_t*, uint32_t*, double);
 hipError_t launch_transform_fallback(hipStream_t, const void*, int, const UnitDev*, int, const XTile*, size_t, float*,
-                                     const unsigned long long*, const uint32_t*, uint32_t*, uint32_t*, double);
+                                     const unsigned long long*, const uint32_t*, double);
 hipError_t launch_pack(hipStream_t, const UnitDev*, int, const uint32_t*, const uint8_t*, uint64_t*, uint8_t*);
 hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, const FTile*, uint32_t,
                          unsigned long long*, uint32_t, const uint8_t*, const uint64_t*, uint32_t*,
@@ -273,7 +273,7 @@ void build_etiles(Plan& P, int n) {
         total += d.net;
     }
     P.netiles = total;
-    // per-call state: 16 (needy count) | key[n] (u64) | tickets[n] | spos[n] | needy[n] (u32) |
+    // per-call state: 16 (spare) | key[n] (u64) | tickets[n] | spos[n] | spare[n] (u32) |
     // status[tiles] (u64)
     P.state_bytes = round_up(16 + 20ull * n, 8) + 8ull * total;
     P.edesc.clear();
@@ -645,7 +645,6 @@ int stage_transform(wc_ctx* c, const void* d_cells, int dtype, double keep, bool
     unsigned long long* key = (unsigned long long*)((uint8_t*)c->state.p + 16);
     const size_t n = P.units.size();
     uint32_t* spos = (uint32_t*)((uint8_t*)c->state.p + 16 + 12 * n);
-    uint32_t* needy = (uint32_t*)((uint8_t*)c->state.p + 16 + 16 * n);  // needy[-4 B .. ]: state word 0 counts
     float* coef = (float*)c->coef.p;
     uint8_t* flags = sparse && P.any_sparse ? (uint8_t*)c->flags.p : nullptr;
     {
@@ -657,7 +656,7 @@ int stage_transform(wc_ctx* c, const void* d_cells, int dtype, double keep, bool
         // units whose thresh came out < 0 need every coefficient (rare: negative signed max)
         if (e == hipSuccess && flags)
             e = launch_transform_fallback(c->stream, d_cells, dtype, du, (int)P.units.size(), dxt, P.lds_fast, coef,
-                                          key, spos, (uint32_t*)c->state.p, needy, keep);
+                                          key, spos, keep);
     }
     c->sparse_staged = flags != nullptr;
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "transform launch");

@@ -93,45 +93,41 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
 // every coefficient is kept, src/compressor.cpp:216-226) need every
 // coefficient; those with a sparsely staged tile (spos: a tile whose own
 // largest magnitude is negative stages densely, so this takes a unit whose
-// tiles disagree in sign) are re-staged densely.  k_fallback_check lists them
-// (workgroup b checks units [256b, 256b + 256), one atomicAdd per wave with
-// any); k_transform_fallback re-stages the listed units, one per workgroup
-// (grid-strided), every workgroup exiting at once when the list is empty.
-__global__ __launch_bounds__(kThreads) void k_fallback_check(const UnitDev* __restrict__ units, int n,
-                                                           const unsigned long long* __restrict__ unit_key,
-                                                           const uint32_t* __restrict__ spos, double keep,
-                                                           uint32_t* __restrict__ count, uint32_t* __restrict__ list) {
-    const int u = blockIdx.x * kThreads + (int)threadIdx.x;
-    const bool need = u < n && spos[u] && key_thresh(unit_key[u], keep) < 0.0;
-    const unsigned long long b = __ballot(need);
-    if (!b) return;  // uniform per wave
-    const int l = threadIdx.x & 63;
-    uint32_t base = 0;
-    if (l == __ffsll((long long)b) - 1) base = atomicAdd(count, (uint32_t)__popcll(b));
-    base = __shfl(base, __ffsll((long long)b) - 1);
-    if (need) list[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u))] =
-        (uint32_t)u;
-}
-
+// tiles disagree in sign) are re-staged densely.  One launch checks and
+// re-stages: workgroup b owns units b, b + G, b + 2G, ... (G = grid); its
+// threads check 256 of them at once (one key load each), list the needy ones
+// in LDS, and the workgroup re-stages those tile by tile.  With none, every
+// workgroup exits after one round of loads.
 template <typename T>
 __global__ __launch_bounds__(kThreads) void k_transform_fallback(const T* __restrict__ cells,
-                                                               const UnitDev* __restrict__ units,
+                                                               const UnitDev* __restrict__ units, int n,
                                                                const XTile* __restrict__ tiles, float* __restrict__ out,
-                                                               const uint32_t* __restrict__ count,
-                                                               const uint32_t* __restrict__ list) {
+                                                               const unsigned long long* __restrict__ unit_key,
+                                                               const uint32_t* __restrict__ spos, double keep) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const uint32_t cnt = *count;  // written by k_fallback_check (the launch before)
-    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-        const UnitDev& U = units[list[i]];
-        float* __restrict__ dst = out + U.coef_off;
-        for (uint32_t t = 0; t < U.ntx; ++t) {
-            const XTile td = tiles[U.xt_begin + t];
-            xform_fast_p1<T>(cells + U.cell_off, U, td, lds, threadIdx.x);
-            __syncthreads();
-            (void)xform_fast_p2<false>(U, td, lds, threadIdx.x,
-                                       [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
-            __syncthreads();
+    __shared__ uint32_t s_list[kThreads];
+    __shared__ uint32_t s_cnt;
+    const int tid = threadIdx.x;
+    for (int64_t base = blockIdx.x; base < n; base += (int64_t)gridDim.x * kThreads) {
+        if (tid == 0) s_cnt = 0;
+        __syncthreads();
+        const int64_t u = base + (int64_t)tid * gridDim.x;
+        if (u < n && spos[u] && key_thresh(unit_key[u], keep) < 0.0) s_list[atomicAdd(&s_cnt, 1u)] = (uint32_t)u;
+        __syncthreads();
+        const uint32_t cnt = s_cnt;
+        for (uint32_t i = 0; i < cnt; ++i) {
+            const UnitDev& U = units[s_list[i]];
+            float* __restrict__ dst = out + U.coef_off;
+            for (uint32_t t = 0; t < U.ntx; ++t) {
+                const XTile td = tiles[U.xt_begin + t];
+                xform_fast_p1<T>(cells + U.cell_off, U, td, lds, tid);
+                __syncthreads();
+                (void)xform_fast_p2<false>(U, td, lds, tid,
+                                           [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
+                __syncthreads();
+            }
         }
+        __syncthreads();  // s_cnt / s_list reused by the next round
     }
 }
 
@@ -274,14 +270,15 @@ hipError_t launch_transform_fast(hipStream_t st, const void* cells, int dtype, c
 
 hipError_t launch_transform_fallback(hipStream_t st, const void* cells, int dtype, const UnitDev* units, int n,
                                      const XTile* tiles, size_t lds, float* out, const unsigned long long* keys,
-                                     const uint32_t* spos, uint32_t* count, uint32_t* list, double keep) {
+                                     const uint32_t* spos, double keep) {
     if (n == 0) return hipSuccess;
-    k_fallback_check<<<(n + kThreads - 1) / kThreads, kThreads, 0, st>>>(units, n, keys, spos, keep, count, list);
-    const int grid = std::min(n, 1024);
+    const int grid = std::min(n, 2048);  // <= 4 workgroups per CU of the LDS-bound tile: one dispatch round
     if (dtype == 1)
-        k_transform_fallback<double><<<grid, kThreads, lds, st>>>((const double*)cells, units, tiles, out, count, list);
+        k_transform_fallback<double><<<grid, kThreads, lds, st>>>((const double*)cells, units, n, tiles, out, keys,
+                                                                  spos, keep);
     else
-        k_transform_fallback<float><<<grid, kThreads, lds, st>>>((const float*)cells, units, tiles, out, count, list);
+        k_transform_fallback<float><<<grid, kThreads, lds, st>>>((const float*)cells, units, n, tiles, out, keys,
+                                                                 spos, keep);
     return hipGetLastError();
 }
 
