@@ -599,6 +599,35 @@ def test_sparse_staging_special_values(wc, ctx, oracle):
                 assert got[i] == oracle.compress_payload(b, keep)[0], (path, keep, i)
 
 
+def test_fallback_restage_past_one_round(wc, ctx, oracle):
+    """k_transform_fallback checks units b, b + G, ... 256 at a time per
+    workgroup (G = min(n, 2048)): with n > 2048 * 256 tiny two-tile units the
+    needy ones (a positive tile staged sparsely, a negative spike in the other:
+    thresh < 0, re-staged densely) sit in both check rounds; their payloads and
+    a sample of the others equal the oracle's.  One host run (HOST_CHUNK 0)."""
+    from wavelet_compression_amd.capi import WC_OPT_HOST_CHUNK
+    n = 2048 * 256 + 777
+    W, H, D = 2, 2, 128                      # nbz 64: two 32-block z tiles, sparse
+    rng = np.random.default_rng(31)
+    cells = (1.0 + 0.05 * rng.standard_normal((n, D, H, W))).astype(np.float32)
+    needy = [3, 2047, 2048 * 255 + 5, 2048 * 256, 2048 * 256 + 1, n - 1]
+    for u in needy:
+        cells[u, 100:102] = -1.0e6           # a whole block in the second z tile: signed max < 0
+    units, nu, extent = wc.capi.make_units([(W, H, D)] * n)
+    assert nu == n and extent == cells.size  # 512-cell units pack back to back
+    keep = KEEPS[1]
+    ctx.set_option(WC_OPT_HOST_CHUNK, 0)
+    try:
+        payload, offs, kept = ctx.forward_host(cells.reshape(-1), units, n, keep)
+    finally:
+        ctx.set_option(WC_OPT_HOST_CHUNK, 1 << 25)
+    for u in needy + [0, 1, 2048, 2048 * 256 - 1, 2048 * 256 + 2, n - 2]:
+        want = oracle.compress_payload(cells[u], keep)[0]
+        assert wc.capi.unit_payload(payload, offs, kept, u) == want, u
+    for u in needy:
+        assert int(kept[u]) == W * H * D, u  # thresh < 0: every coefficient kept
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_forward_host_pipelined_runs(wc, ctx, oracle, dtype):
     """wc_forward_host split into pipelined unit runs (WC_OPT_HOST_CHUNK small:
