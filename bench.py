@@ -500,16 +500,25 @@ def host_leg(args, d: Dist, ctx, b: Batch):
     pinned.copy_(b.cells_dev)
     torch.cuda.synchronize()
     arr = pinned.numpy()
-    _, offs, _ = ctx.forward_host(arr, b.tab, b.n, b.keep)  # warm-up: host staging buffers
+    payload, offs, _ = ctx.forward_host(arr, b.tab, b.n, b.keep)  # warm-up: host staging buffers
     steps = max(1, min(args.leg_steps, 5))
     t0 = time.perf_counter()
     for _ in range(steps):
-        _, offs, _ = ctx.forward_host(arr, b.tab, b.n, b.keep)
+        payload, offs, _ = ctx.forward_host(arr, b.tab, b.n, b.keep)
     ms = (time.perf_counter() - t0) / steps * 1e3
     h2d = arr.nbytes
     d2h = int(offs[b.n])
+    # wc_inverse_host over the same payloads (host bytes in, fp32 boxes out to host memory)
+    ctx.inverse_host(payload, offs[:b.n], b.tab, b.n, arr.size)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.inverse_host(payload, offs[:b.n], b.tab, b.n, arr.size)
+    ims = (time.perf_counter() - t0) / steps * 1e3
     return {"value": b.ncells / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
             "h2d_bytes": h2d, "d2h_bytes": d2h, "host_GBps": (h2d + d2h) / (ms * 1e-3) / 1e9,
+            "inverse": {"value": b.ncells / (ims * 1e-3), "unit": "cells/s", "ms_per_step": ims,
+                        "h2d_bytes": d2h, "d2h_bytes": 4 * b.ncells,
+                        "host_GBps": (d2h + 4 * b.ncells) / (ims * 1e-3) / 1e9},
             "note": "PCIe-inclusive (pinned host cells in, packed payloads out to host memory), one rank; "
                     "`value` above is the HBM-resident rate"}
 

@@ -106,7 +106,9 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  *   more than two such chunks into contiguous unit runs of about this many
  *   cells (at most 16 runs) and pipelines them: the cells of run r+1 upload
  *   while run r computes and run r-1's packed payloads download.  Same bytes
- *   and offsets out; 0 = one run.
+ *   and offsets out; 0 = one run.  wc_inverse_host runs the same way (run
+ *   r+1's payload bytes upload while run r decodes and run r-1's boxes
+ *   download).
  */
 #define WC_OPT_SPARSE 12
 #define WC_OPT_ORDERED 13

@@ -657,6 +657,44 @@ def test_forward_host_pipelined_runs(wc, ctx, oracle, dtype):
             assert wc.capi.unit_payload(p1, o1, k1, i) == oracle_payload(oracle, b.astype(dtype), keep), i
 
 
+def test_inverse_host_pipelined_runs(wc, ctx, oracle):
+    """wc_inverse_host split into pipelined unit runs (payload spans uploaded
+    run by run, boxes downloaded run by run in back-to-back spans) reconstructs
+    the same values as one run, equal to the oracle's, also with gaps between
+    the units' cells (the gap cells of the caller's buffer stay untouched) and
+    with the units' payloads in reverse order."""
+    from wavelet_compression_amd.capi import WC_OPT_HOST_CHUNK
+    keep = KEEPS[1]
+    boxes = synth(oracle, DIMS, seed0=23)
+    rng = np.random.default_rng(6)
+    gaps = np.cumsum([0] + [int(b.size) + int(rng.integers(0, 9)) for b in boxes[:-1]]).tolist()
+    for offsets in (None, gaps):
+        units, n, extent, cells = pack(wc, boxes, np.float64, offsets)
+        payload, offs, kept = ctx.forward_host(cells, units, n, keep)
+        # the same payloads laid out in reverse unit order
+        blobs = [wc.capi.unit_payload(payload, offs, kept, i) for i in range(n)]
+        rev = bytearray(4)
+        roffs = np.zeros(n + 1, np.uint64)
+        for i in reversed(range(n)):
+            roffs[i] = len(rev)
+            rev += blobs[i] + b"\0" * ((-len(blobs[i])) % 4)
+        rev = np.frombuffer(bytes(rev), np.uint8)
+        want = [oracle.decompress_payload(blobs[i]).ravel() for i in range(n)]
+        for pay, po in ((payload, offs), (rev, roffs)):
+            for chunk in (0, 3000, 40000):
+                ctx.set_option(WC_OPT_HOST_CHUNK, chunk)
+                try:
+                    regen = ctx.inverse_host(pay, po[:n], units, n, extent)
+                finally:
+                    ctx.set_option(WC_OPT_HOST_CHUNK, 1 << 25)
+                owned = np.zeros(extent, bool)
+                for i, b in enumerate(boxes):
+                    o = units[i].cell_offset
+                    owned[o:o + b.size] = True
+                    assert regen[o:o + b.size].tobytes() == want[i].tobytes(), (chunk, i)
+                assert not regen[~owned].any(), chunk  # gap cells untouched
+
+
 def test_plan_cache_eviction(wc, ctx, oracle):
     """More distinct batches than the plan cache holds (16), each twice: plans
     are swapped back in, evicted, and rebuilt into an evicted plan's buffers;

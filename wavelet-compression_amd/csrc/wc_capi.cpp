@@ -1098,6 +1098,46 @@ int wc_profile_read(wc_ctx* c, double* total_ms, uint32_t* launches, int nstages
 
 // ---- host-pointer variants -------------------------------------------------
 
+// Unit runs of the host-buffer paths: boundaries rb[0] = 0 < ... < rb[nr] = n,
+// runs of about opt_host_chunk cells (at least total / 16), one run unless the
+// batch holds more than two chunks (or opt_host_chunk <= 0).
+static std::vector<int> host_runs(const wc_ctx* c, const wc_unit* units, int n) {
+    std::vector<int> rb{0};
+    uint64_t total = 0;
+    for (int i = 0; i < n; ++i) total += (uint64_t)units[i].nx * units[i].ny * units[i].nz;
+    const uint64_t chunk =
+        c->opt_host_chunk > 0 ? std::max<uint64_t>((uint64_t)c->opt_host_chunk, total / 16 + 1) : total + 1;
+    if (total > 2 * chunk) {
+        uint64_t acc = 0;
+        for (int i = 0; i < n; ++i) {
+            acc += (uint64_t)units[i].nx * units[i].ny * units[i].nz;
+            if (acc >= chunk && i + 1 < n) {
+                rb.push_back(i + 1);
+                acc = 0;
+            }
+        }
+    }
+    rb.push_back(n);
+    return rb;
+}
+
+// The copy streams (when there is more than one run) and 2 events per run.
+static int host_streams(wc_ctx* c, int nr) {
+    hipError_t e;
+    if (nr > 1) {
+        if (!c->up && (e = hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking)) != hipSuccess)
+            return hip_fail(c, e, "upload stream");
+        if (!c->down && (e = hipStreamCreateWithFlags(&c->down, hipStreamNonBlocking)) != hipSuccess)
+            return hip_fail(c, e, "download stream");
+    }
+    while ((int)c->hev.size() < 2 * nr) {
+        hipEvent_t ev;
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(c, e, "event");
+        c->hev.push_back(ev);
+    }
+    return WC_OK;
+}
+
 static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_unit* units, int n, double keep,
                              uint8_t* payload, uint64_t cap, uint64_t* offsets, uint32_t* kept) {
     int rc;
@@ -1116,24 +1156,7 @@ static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_u
     // context stream, and each run's packed payloads download on `down` once
     // its sizes are known.  The packed layout (== 4 mod 8 offsets) is the same
     // as one run's.
-    std::vector<int> rb{0};
-    {
-        uint64_t total = 0;
-        for (int i = 0; i < n; ++i) total += (uint64_t)units[i].nx * units[i].ny * units[i].nz;
-        const uint64_t chunk = c->opt_host_chunk > 0 ? std::max<uint64_t>((uint64_t)c->opt_host_chunk, total / 16 + 1)
-                                                     : total + 1;
-        if (total > 2 * chunk) {
-            uint64_t acc = 0;
-            for (int i = 0; i < n; ++i) {
-                acc += (uint64_t)units[i].nx * units[i].ny * units[i].nz;
-                if (acc >= chunk && i + 1 < n) {
-                    rb.push_back(i + 1);
-                    acc = 0;
-                }
-            }
-        }
-        rb.push_back(n);
-    }
+    std::vector<int> rb = host_runs(c, units, n);
     const int nr = (int)rb.size() - 1;
     // per run: payload slot base (device), metadata base (pinned): poff[n_r + 1] | kept[n_r]
     std::vector<uint64_t> pbase(nr + 1, 0);
@@ -1152,17 +1175,7 @@ static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_u
             return hip_fail(c, e, "pinned metadata");
         c->pinned_bytes = meta_bytes;
     }
-    if (nr > 1) {
-        if (!c->up && (e = hipStreamCreateWithFlags(&c->up, hipStreamNonBlocking)) != hipSuccess)
-            return hip_fail(c, e, "upload stream");
-        if (!c->down && (e = hipStreamCreateWithFlags(&c->down, hipStreamNonBlocking)) != hipSuccess)
-            return hip_fail(c, e, "download stream");
-    }
-    while ((int)c->hev.size() < 2 * nr) {
-        hipEvent_t ev;
-        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(c, e, "event");
-        c->hev.push_back(ev);
-    }
+    if ((rc = host_streams(c, nr))) return rc;
     uint64_t* pin_poff = (uint64_t*)c->pinned;                   // [n + nr]
     uint32_t* pin_kept = (uint32_t*)(pin_poff + (n + nr));       // [n]
     uint8_t* d_cells = (uint8_t*)c->h_cells.p;
@@ -1244,22 +1257,60 @@ static int inverse_host_once(wc_ctx* c, const uint8_t* payload, const uint64_t* 
     if ((rc = ensure(c, c->h_payload, extent)) || (rc = ensure(c, c->h_offsets, sizeof(uint64_t) * n)) ||
         (rc = ensure(c, c->h_out, sizeof(float) * ext)))
         return rc;
+    // Runs of contiguous units of about opt_host_chunk cells (at most 16), as
+    // in forward_host_once: run r's payload bytes upload on `up` while run r-1
+    // decodes on the context stream and run r-2's boxes download on `down`.
+    std::vector<int> rb = host_runs(c, units, n);
+    const int nr = (int)rb.size() - 1;
     hipError_t e;
-    if ((e = hipMemcpyAsync(c->h_payload.p, payload, extent, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(c->h_offsets.p, offsets, sizeof(uint64_t) * n, hipMemcpyHostToDevice, c->stream)) !=
-            hipSuccess)
-        return hip_fail(c, e, "payload upload");
-    if ((rc = wc_inverse(c, (const uint8_t*)c->h_payload.p, (const uint64_t*)c->h_offsets.p, units, n,
-                         (float*)c->h_out.p)))
-        return rc;
-    // Copy back exactly the cells the units own (the caller's buffer may have gaps).
-    for (int i = 0; i < n; ++i) {
-        const uint64_t cnt = (uint64_t)units[i].nx * units[i].ny * units[i].nz;
-        if (!cnt) continue;
-        if ((e = hipMemcpyAsync(out + units[i].cell_offset, (float*)c->h_out.p + units[i].cell_offset,
-                                sizeof(float) * cnt, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)
-            return hip_fail(c, e, "box readback");
+    if ((rc = host_streams(c, nr))) return rc;
+    if ((e = hipMemcpyAsync(c->h_offsets.p, offsets, sizeof(uint64_t) * n, hipMemcpyHostToDevice, c->stream)) !=
+        hipSuccess)
+        return hip_fail(c, e, "offsets upload");
+    for (int r = 0; r < nr; ++r) {
+        const int a = rb[r], m = rb[r + 1] - rb[r];
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (int i = a; i < a + m; ++i) {
+            int32_t cnt;
+            std::memcpy(&cnt, payload + offsets[i] + 16, 4);
+            lo = std::min(lo, offsets[i]);
+            hi = std::max(hi, offsets[i] + 20 + 8 * (uint64_t)cnt);
+        }
+        hipStream_t us = nr > 1 ? c->up : c->stream;
+        if (hi > lo && (e = hipMemcpyAsync((uint8_t*)c->h_payload.p + lo, payload + lo, hi - lo,
+                                           hipMemcpyHostToDevice, us)) != hipSuccess)
+            return hip_fail(c, e, "payload upload");
+        if (nr > 1 && ((e = hipEventRecord(c->hev[2 * r], c->up)) != hipSuccess ||
+                       (e = hipStreamWaitEvent(c->stream, c->hev[2 * r], 0)) != hipSuccess))
+            return hip_fail(c, e, "upload event");
+        if ((rc = wc_inverse(c, (const uint8_t*)c->h_payload.p, (const uint64_t*)c->h_offsets.p + a, units + a, m,
+                             (float*)c->h_out.p)))
+            return rc;
+        hipStream_t ds = c->stream;
+        if (nr > 1) {
+            if ((e = hipEventRecord(c->hev[2 * r + 1], c->stream)) != hipSuccess ||
+                (e = hipStreamWaitEvent(c->down, c->hev[2 * r + 1], 0)) != hipSuccess)
+                return hip_fail(c, e, "decode event");
+            ds = c->down;
+        }
+        // Copy back exactly the cells the units own (the caller's buffer may
+        // have gaps), one copy per span of back-to-back units.
+        for (int i = a; i < a + m;) {
+            const uint64_t o = units[i].cell_offset;
+            uint64_t end = o + (uint64_t)units[i].nx * units[i].ny * units[i].nz;
+            int j = i + 1;
+            for (; j < a + m; ++j) {
+                const uint64_t cj = (uint64_t)units[j].nx * units[j].ny * units[j].nz;
+                if (cj && units[j].cell_offset != end) break;
+                end += cj;
+            }
+            if (end > o && (e = hipMemcpyAsync(out + o, (float*)c->h_out.p + o, sizeof(float) * (end - o),
+                                               hipMemcpyDeviceToHost, ds)) != hipSuccess)
+                return hip_fail(c, e, "box readback");
+            i = j;
+        }
     }
+    if (nr > 1 && (e = hipStreamSynchronize(c->down)) != hipSuccess) return hip_fail(c, e, "box readback");
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(c, e, "sync");
     return check_kernel_errors(c);
 }
