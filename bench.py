@@ -163,6 +163,15 @@ class Dist:
         from wavelet_compression_amd.shard import reduce_metrics
         return reduce_metrics(metrics, device=self.coll_dev or self.dev)
 
+    def gather(self, obj):
+        """Every rank's `obj` (a small JSON-able value), in rank order."""
+        if self.world == 1:
+            return [obj]
+        import torch.distributed as dist
+        out = [None] * self.world
+        dist.all_gather_object(out, obj)
+        return out
+
     def close(self):
         if self.world > 1:
             import torch.distributed as dist
@@ -448,11 +457,20 @@ def sharded_forward_leg(args, d: Dist, name, hist=False):
     ms = m["seconds"] / args.leg_steps * 1e3
     alg = alg_bytes_forward(b.s_in, m["cells"], m["kept"], m["boxes"])
     per_rank_alg = alg_bytes_forward(b.s_in, b.ncells, kept, b.n)
+    # per rank: its kept total and the digest of its first unit's payload (the
+    # GPU test recomputes that unit with the oracle; bench.py itself checks nothing)
+    sample = None
+    if b.n:
+        o, k = int(b.offsets[0].item()), int(b.kept[0].item())
+        sample = {"unit": units[0].gid, "kept": k,
+                  "sha256": hashlib.sha256(b.payload[o:o + 20 + 8 * k].cpu().numpy().tobytes()).hexdigest()}
+    per_rank = d.gather({"kept": kept, "cells": b.ncells, "units": b.n, "first_unit": sample})
     out = {"workload": spec["desc"], "units_total": int(m["boxes"]), "units_this_rank": b.n,
            "rank0_span": list(span), "cells_total": int(m["cells"]), "dtype": spec["dtype"], "keep": spec["keep"],
            "kept_fraction": m["kept"] / max(m["cells"], 1), "ms_per_step": ms,
            "value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "scaling": "strong",
            "rank_cell_balance": m["max_rank_cells"] / max(m["min_rank_cells"], 1),
+           "per_rank": per_rank,
            "stage_ms_per_launch": {k: round(v[0], 4) for k, v in st.items()},
            "roofline_path": {"achieved_per_gpu": per_rank_alg / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS,
                              "unit": "GB/s", "frac": per_rank_alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,

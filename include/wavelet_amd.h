@@ -93,6 +93,20 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  *   assumption about dispatch order.  Same bytes out either way.  Every wait
  *   between workgroups is bounded: a wait that never ends is reported as
  *   WC_ERR_HIP at the next wc_synchronize, not a hang.
+ *   The launch-order form is for a device this process owns.  It is NOT safe
+ *   when several PROCESSES run look-back kernels on one GPU at once (each can
+ *   fill an XCD with waiting blocks): set WCAMD_SHARED_DEVICE=1 in their
+ *   environment (every context of the process then uses the tickets), or
+ *   WC_OPT_ORDERED 0.  Contexts of ONE process that share a device switch to
+ *   the tickets by themselves, and a context whose look-back timed out keeps
+ *   the tickets for every later call (sticky; WC_OPT_TICKETS reads it); the
+ *   _host entry points then also re-run the failed call once.  wc_get_option
+ *   (WC_OPT_ORDERED) returns the form the next launch takes.
+ * WC_OPT_TICKETS (default 0): 1 = this context uses the ticket form whatever
+ *   WC_OPT_ORDERED says (set by the library after a look-back timeout).
+ * WC_OPT_SPIN_LIMIT (default 0 = ~2^20 polls, about 2 s): bound of every wait
+ *   between workgroups, in polls.  Diagnostic: a tiny bound forces the timeout
+ *   path (tests); results of a call that timed out are not valid.
  * WC_OPT_INVERSE_ROWS (default 1): the inverse of even-dims units (W, H even,
  *   D % 8 == 0) indexes the payload's pairs by flat row and reconstructs each
  *   tile straight from the payload; 0 decodes every unit into a dense fp32
@@ -117,7 +131,10 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
 #define WC_OPT_RIX_TX 16
 #define WC_OPT_RIX_BLOCKED 17
 #define WC_OPT_HOST_CHUNK 18
+#define WC_OPT_SPIN_LIMIT 19
+#define WC_OPT_TICKETS 20
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
+int wc_get_option(const wc_ctx* ctx, int option, int64_t* value);
 
 /* Host-side helpers (no device work). */
 uint64_t wc_payload_bound(const wc_unit* units, int n);  /* worst case: every coefficient kept */

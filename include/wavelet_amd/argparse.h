@@ -18,6 +18,10 @@ struct Config {
     int min_level = 0, max_level = 0;
     float keep = 0.0f;
     std::vector<std::string> components;
+    // Not a reference parameter: `xzpreset=N` (0-9, "Ne"
+    // for the extreme variant) selects the xz preset of -c; default 6, the
+    // reference's (src/compressor.cpp:261).  -1: not given ($WCAMD_XZ_PRESET or 6).
+    int xz_preset = -1;
 };
 
 // Stand-in for amrex::Initialize's ParmParse setup: parse `name=value ...`

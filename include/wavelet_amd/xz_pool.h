@@ -23,7 +23,19 @@ struct XzJob {
     std::string path;     // output file
 };
 
-// Encode each job (preset 6, CRC64, as the reference) and write its file.  A
+// The xz preset of every encoder in the process (an
+// optional faster preset).  Default 6 = the reference's lzma_easy_encoder(6,
+// CRC64) (src/compressor.cpp:261-262), byte-identical to its files; $WCAMD_XZ_PRESET
+// or set_xz_preset() (the CLI's `xzpreset=`) select another.  Any preset is
+// read back by the reference's lzma_stream_decoder(UINT64_MAX, LZMA_CONCATENATED)
+// (src/decompressor.cpp:189), which takes the filter chain from the stream.
+// A preset value is 0-9, optionally | LZMA_PRESET_EXTREME ("6e").
+uint32_t xz_preset();
+void set_xz_preset(uint32_t preset);
+// "0".."9" with an optional trailing 'e' -> preset value; -1 if malformed.
+int parse_xz_preset(const char* text);
+
+// Encode each job (the current preset, CRC64) and write its file.  A
 // file that cannot be opened is skipped (src/compressor.cpp:256-257); encoder
 // failures exit.  Returns the bytes written.
 uint64_t xz_write_files(const std::vector<XzJob>& jobs, int threads);
@@ -31,7 +43,7 @@ uint64_t xz_write_files(const std::vector<XzJob>& jobs, int threads);
 // Read and decode each file (stream decoder, concatenated streams).  Failures exit.
 std::vector<std::string> xz_read_files(const std::vector<std::string>& paths, int threads);
 
-// One buffer -> one .xz stream (preset 6, CRC64).
-std::string xz_encode(const uint8_t* data, size_t size);
+// One buffer -> one .xz stream (preset xz_preset(), or `preset` when >= 0; CRC64).
+std::string xz_encode(const uint8_t* data, size_t size, int preset = -1);
 
 }  // namespace wavelet_amd

@@ -159,6 +159,65 @@ static void xz_pool_case() {
     for (size_t i = 0; i < payloads.size(); ++i) REQUIRE(back[i] == payloads[i]);
 }
 
+// The optional faster xz preset: preset parsing, the
+// process-wide choice ($WCAMD_XZ_PRESET / set_xz_preset), and that preset-0/1
+// streams decode through the reference's stream decoder (xz_decompress:
+// lzma_stream_decoder(UINT64_MAX, LZMA_CONCATENATED), src/decompressor.cpp:189).
+static void xz_preset_case() {
+    REQUIRE(wavelet_amd::parse_xz_preset("0") == 0 && wavelet_amd::parse_xz_preset("9") == 9);
+    REQUIRE(wavelet_amd::parse_xz_preset("6e") == (int)(6u | 0x80000000u));
+    REQUIRE(wavelet_amd::parse_xz_preset("") == -1 && wavelet_amd::parse_xz_preset("10") == -1 &&
+            wavelet_amd::parse_xz_preset("x") == -1 && wavelet_amd::parse_xz_preset("1f") == -1);
+    if (!std::getenv("WCAMD_XZ_PRESET")) REQUIRE(wavelet_amd::xz_preset() == 6);  // the reference's
+    std::string p(20 + 8 * 5000, '\0');
+    std::mt19937 rng(11);
+    for (auto& ch : p) ch = (char)(rng() % 5);
+    const uint8_t* d = reinterpret_cast<const uint8_t*>(p.data());
+    const std::string x6 = wavelet_amd::xz_encode(d, p.size(), 6);
+    REQUIRE(x6 == wavelet_amd::xz_compress(p) || std::getenv("WCAMD_XZ_PRESET"));
+    for (int pr : {0, 1, 9}) {
+        const std::string x = wavelet_amd::xz_encode(d, p.size(), pr);
+        REQUIRE(wavelet_amd::xz_decompress(x) == p);
+    }
+    const uint32_t before = wavelet_amd::xz_preset();
+    wavelet_amd::set_xz_preset(0);
+    REQUIRE(wavelet_amd::xz_compress(p) == wavelet_amd::xz_encode(d, p.size(), 0));
+    wavelet_amd::set_xz_preset(before);
+}
+
+// `test_host_io --xz-presets DIR PRESET...`: every *.bin payload in DIR is
+// written as DIR/<name>.p<PRESET>.xz by the xz pool at each preset, then all
+// are read back through the pool's stream decoder; prints "name preset bytes"
+// and exits non-zero if a decoded payload differs from its source.
+static int xz_presets_mode(const fs::path& dir, const std::vector<int>& presets) {
+    std::vector<std::string> names, payloads;
+    for (const auto& e : fs::directory_iterator(dir))
+        if (e.path().extension() == ".bin") {
+            std::ifstream f(e.path(), std::ios::binary);
+            payloads.emplace_back((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+            names.push_back(e.path().stem().string());
+        }
+    for (int pr : presets) {
+        wavelet_amd::set_xz_preset((uint32_t)pr);
+        std::vector<wavelet_amd::XzJob> jobs;
+        for (size_t i = 0; i < names.size(); ++i)
+            jobs.push_back({reinterpret_cast<const uint8_t*>(payloads[i].data()), payloads[i].size(),
+                            (dir / (names[i] + ".p" + std::to_string(pr) + ".xz")).string()});
+        wavelet_amd::xz_write_files(jobs, 4);
+        std::vector<std::string> paths;
+        for (const auto& j : jobs) paths.push_back(j.path);
+        const auto back = wavelet_amd::xz_read_files(paths, 3);
+        for (size_t i = 0; i < names.size(); ++i) {
+            if (back[i] != payloads[i]) {
+                std::fprintf(stderr, "decode mismatch %s preset %d\n", names[i].c_str(), pr);
+                return 1;
+            }
+            std::printf("%s %d %llu\n", names[i].c_str(), pr, (unsigned long long)fs::file_size(paths[i]));
+        }
+    }
+    return 0;
+}
+
 static bool same_file(const fs::path& a, const fs::path& b) {
     std::ifstream fa(a, std::ios::binary), fb(b, std::ios::binary);
     if (!fa || !fb) return false;
@@ -263,6 +322,11 @@ static void reference_fixture_cases(const fs::path& ref_tests) {
 }
 
 int main(int argc, char** argv) {
+    if (argc > 2 && std::string(argv[1]) == "--xz-presets") {
+        std::vector<int> presets;
+        for (int i = 3; i < argc; ++i) presets.push_back(wavelet_amd::parse_xz_preset(argv[i]));
+        return xz_presets_mode(argv[2], presets);
+    }
     loc_dim_case();
     box_counts_case();
     amrexinfo_case();
@@ -271,6 +335,7 @@ int main(int argc, char** argv) {
     params_case();
     format_files_case();
     xz_pool_case();
+    xz_preset_case();
     plotfile_roundtrip_case();
     bool ref = false;
     if (argc > 1 && fs::exists(fs::path(argv[1]) / "plt00074" / "Header")) {

@@ -180,3 +180,30 @@ def test_multi_device_workers_write_identical_files(run, compressed, tmp_path):
         for f in files:
             a = Path(root) / f
             assert filecmp.cmp(a, r2 / a.relative_to(r1), shallow=False), a
+
+
+def test_fast_xz_preset_round_trip(run, compressed, tmp_path):
+    """`xzpreset=0` (not a reference parameter): every .xz
+    decodes to the same payload as the default preset-6 file, the files differ
+    (another filter preset), and -d regenerates the same plotfiles."""
+    import filecmp
+    base, _ = run
+    out = base / "comp_p0"
+    cli(f"datadir={base}/data/", "minfile=plt00010", "maxfile=plt00011", "minlevel=0", "maxlevel=1",
+        "components=temp pressure", f"keep={KEEP}", f"compresseddir={out}/", "xzpreset=0", "-c",
+        env={"WCAMD_CHUNK_CELLS": "60000", "WCAMD_THREADS": "4"})
+    xz6 = sorted(compressed.glob("*.xz"))
+    assert xz6 and sorted(p.name for p in out.glob("*.xz")) == [p.name for p in xz6]
+    differ = 0
+    for f in xz6:
+        a, b = f.read_bytes(), (out / f.name).read_bytes()
+        assert lzma.decompress(a) == lzma.decompress(b), f.name
+        differ += a != b
+    assert differ > 0
+    r6, r0 = base / "regen_p6", base / "regen_p0"
+    cli(f"compresseddir={compressed}/", f"out={r6}/", "-d")
+    cli(f"compresseddir={out}/", f"out={r0}/", "-d")
+    for root, _, files in os.walk(r6):
+        for f in files:
+            a = Path(root) / f
+            assert filecmp.cmp(a, r0 / a.relative_to(r6), shallow=False), a

@@ -213,3 +213,25 @@ def test_bench_two_ranks_on_one_gpu(tmp_path):
     assert out["value"] > 0 and 0.25 < out["kept_fraction"] < 0.35
     c5 = out["c5"]
     assert c5["units_total"] == 512 and c5["units_this_rank"] == 256 and c5["cells_total"] == 512 * 128 ** 3
+    # both ranks' kept totals add up to the line's, at C5's density (keep 0.9999f on 128^3)
+    pr = c5["per_rank"]
+    assert len(pr) == 2 and [p["units"] for p in pr] == [256, 256]
+    assert sum(p["kept"] for p in pr) == round(c5["kept_fraction"] * c5["cells_total"])
+    for p in pr:
+        assert 0.35 < p["kept"] / p["cells"] < 0.55, p
+    # each rank's first 128^3 unit: its payload bytes are the oracle's
+    import hashlib
+
+    import numpy as np
+    import torch
+    import bench_workloads as bw
+    from oracle import oracle as O
+    units = bw.WORKLOADS["c5"]["units"]()
+    assert [p["first_unit"]["unit"] for p in pr] == [0, 256]
+    for p in pr:
+        u = units[p["first_unit"]["unit"]]
+        cells, _, _ = bw.synth_cells(torch, torch.device("cuda", 0), [u], "f32")
+        box = cells[:u.cells].cpu().numpy().reshape(u.D, u.H, u.W)
+        want, wk = O.compress_payload(box, float(np.float32(0.9999)))
+        assert p["first_unit"]["kept"] == wk
+        assert p["first_unit"]["sha256"] == hashlib.sha256(want).hexdigest(), p

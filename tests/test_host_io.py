@@ -53,3 +53,37 @@ def test_cli_reports_missing_parameters(tmp_path):
     """Missing parameters are logged, like ParmParse queries in src/argparse.cpp:17-68."""
     r = subprocess.run([str(CLI), f"compresseddir={tmp_path}/", "-d"], capture_output=True, text=True, timeout=60)
     assert "Missing out directory!" in r.stderr
+
+
+def test_fast_xz_preset_decodes_to_oracle_payloads(tmp_path, oracle):
+    """SURVEY §8(f) row 1's optional faster preset: oracle payloads of synthetic
+    boxes, xz-encoded by the host pool at presets 0, 1 and 6, are read back by
+    the reference-style stream decoder (host xz_decompress, src/decompressor.cpp:
+    164-234) to the same payloads; preset 6 is byte-identical to liblzma's
+    preset 6 / CRC64 (the reference's files); the fast presets are smaller than
+    the payload and at most ~1.3x preset 6's size here."""
+    import lzma
+    keep = float(np.float32(0.999))
+    want = {}
+    for i, d in enumerate([(32, 32, 32), (16, 32, 64), (48, 32, 16), (8, 4, 2)]):
+        box = oracle.narrow(oracle.synth_box_f64(oracle.unit_seed(0, 0, i, 0), (0, 0, 0), *d))
+        p, _ = oracle.compress_payload(box, keep)
+        want[f"u{i}"] = p
+        (tmp_path / f"u{i}.bin").write_bytes(p)
+    r = subprocess.run([str(BIN), "--xz-presets", str(tmp_path), "0", "1", "6"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    sizes = {}
+    for line in r.stdout.split("\n"):
+        if line.strip():
+            name, pr, nb = line.split()
+            sizes[(name, int(pr))] = int(nb)
+    assert len(sizes) == 3 * len(want)
+    for name, p in want.items():
+        for pr in (0, 1, 6):
+            blob = (tmp_path / f"{name}.p{pr}.xz").read_bytes()
+            assert lzma.decompress(blob, format=lzma.FORMAT_XZ) == p, (name, pr)
+        assert (tmp_path / f"{name}.p6.xz").read_bytes() == lzma.compress(
+            p, format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64, preset=6), name
+        if len(p) > 4096:
+            assert sizes[(name, 0)] < len(p) and sizes[(name, 0)] <= 1.3 * sizes[(name, 6)], (name, sizes)

@@ -8,7 +8,10 @@ Reported: wall seconds per mode, input GB/s of -c, units/s, and the CPU
 baseline = oracle transform/threshold/RLE/serialize + xz preset 6 (what the
 reference's compress() does per unit, single thread) on a sample of units.
 
-usage: python tools/bench_cli.py [--scale 1.0] [--ncomp 4] [--out profiles/r02/cli_e2e.json]
+-c is also run with each of --fast-presets (the optional faster xz preset,
+`xzpreset=N`): time, .xz bytes, and that -d regenerates identical plotfiles.
+
+usage: python tools/bench_cli.py [--scale 1.0] [--ncomp 4] [--out profiles/r03/cli_e2e.json]
 """
 from __future__ import annotations
 
@@ -69,7 +72,8 @@ def main():
     ap.add_argument("--ncomp", type=int, default=4)
     ap.add_argument("--keep", type=float, default=0.999)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
-    ap.add_argument("--out", default=str(ROOT / "profiles" / "r02" / "cli_e2e.json"))
+    ap.add_argument("--fast-presets", default="0,1", help="xzpreset= values timed beside the default 6")
+    ap.add_argument("--out", default=str(ROOT / "profiles" / "r03" / "cli_e2e.json"))
     args = ap.parse_args()
     import wcamd  # noqa: F401  (registers the package as wavelet_compression_amd)
     from oracle import oracle as O
@@ -113,6 +117,23 @@ def main():
         if xz_bytes == 0:
             raise SystemExit("no .xz files written:\n" + logs["-c"])
         t_d, _ = run([f"compresseddir={base}/comp/", f"out={base}/regen/", "-d"])
+        # the optional faster xz presets: same payloads, other .xz streams
+        fast = {}
+        for pr in args.fast_presets.split(","):
+            d = base / f"comp_p{pr}"
+            t_f, _ = run(common + [f"compresseddir={d}/", f"xzpreset={pr}", "-c"])
+            nb = sum(f.stat().st_size for f in d.glob("*.xz"))
+            same = all(lzma.decompress(f.read_bytes()) == lzma.decompress((d / f.name).read_bytes())
+                       for f in sorted((base / "comp").glob("*.xz"))[::97])
+            t_fd, _ = run([f"compresseddir={d}/", f"out={base}/regen_p{pr}/", "-d"])
+            regen_same = all(
+                f.read_bytes() == (base / f"regen_p{pr}" / f.relative_to(base / "regen")).read_bytes()
+                for f in (base / "regen").rglob("*") if f.is_file())
+            fast[pr] = {"compress_s": t_f, "compress_cells_per_s": ncells / t_f, "xz_bytes": nb,
+                        "size_vs_preset6": nb / xz_bytes, "decompress_s": t_fd,
+                        "payloads_equal_preset6_sample": bool(same), "regen_plotfiles_identical": bool(regen_same)}
+            shutil.rmtree(d, ignore_errors=True)
+            shutil.rmtree(base / f"regen_p{pr}", ignore_errors=True)
         t_e, est = run([*common[:3], "minlevel=0", "maxlevel=0", f"components={comp}", f"keep={args.keep}",
                         f"compresseddir={base}/x/", "-estimate"])
         nunits = sum(len(f) for f in levels) * args.ncomp
@@ -143,6 +164,7 @@ def main():
             "compress_cells_per_s": ncells / t_c,
             "decompress_cells_per_s": ncells / t_d,
             "xz_bytes": xz_bytes, "compressed_fraction": xz_bytes / (ncells * 8),
+            "xz_preset": 6, "fast_xz_presets": fast,
             "host_threads": int(os.environ.get("WCAMD_THREADS", os.environ.get("OMP_NUM_THREADS", os.cpu_count()))),
             "cpu_baseline": {"value": cpu_cells_s, "unit": "cells/s", "cores": 1, "kind": "port",
                              "sample": f"{done} random units ({cells} cells): oracle transform+threshold+RLE+serialize "

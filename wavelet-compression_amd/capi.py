@@ -28,7 +28,7 @@ EXPORTED = (
     "wc_inverse", "wc_inverse_host", "wc_inverse_flat", "wc_rmse", "wc_version",
     "wc_profile_enable", "wc_profile_read", "wc_set_option", "wc_inverse_flat_host", "wc_rmse_host",
     "wc_decompose_host", "wc_device_count", "wc_forward_stage", "wc_hist_threshold",
-    "wc_forward_emit", "wc_inverse_rmse",
+    "wc_forward_emit", "wc_inverse_rmse", "wc_get_option",
 )
 WC_OPT_SPARSE = 12   # sparse coefficient staging in the forward (default 1)
 WC_OPT_ORDERED = 13  # look-back tile index from the launch order (1, default) or per-unit tickets (0)
@@ -37,6 +37,8 @@ WC_OPT_RIX_LDS = 15  # row-indexed inverse: LDS floats per workgroup (default 92
 WC_OPT_RIX_TX = 16  # row-indexed inverse: log2 of the tile's x blocks (default 4)
 WC_OPT_RIX_BLOCKED = 17  # row-indexed inverse: contiguous tile runs per workgroup (default 0)
 WC_OPT_HOST_CHUNK = 18  # wc_forward_host: cells per pipelined unit run (default 2^25, 0 = one run)
+WC_OPT_SPIN_LIMIT = 19  # polls before a look-back wait is declared timed out (0: default, ~2 s)
+WC_OPT_TICKETS = 20  # 1: ticket form whatever WC_OPT_ORDERED says (set by a look-back timeout: sticky)
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*).
 STAGES = ("transform", "emit", "decode", "inverse", "rmse", "hist")
@@ -90,6 +92,7 @@ def load_library() -> ctypes.CDLL:
         "wc_version": (ctypes.c_char_p, []),
         "wc_profile_enable": (i32, [vp, i32]),
         "wc_set_option": (i32, [vp, i32, ctypes.c_int64]),
+        "wc_get_option": (i32, [vp, i32, ctypes.POINTER(ctypes.c_int64)]),
         "wc_inverse_flat_host": (i32, [vp, vp, up, i32, vp]),
         "wc_rmse_host": (i32, [vp, vp, i32, vp, up, i32, vp]),
         "wc_decompose_host": (i32, [vp, vp, i32, up, i32, vp]),
@@ -191,6 +194,11 @@ class Context:
 
     def set_option(self, option: int, value: int):
         self._check(self._L.wc_set_option(self._h, int(option), int(value)))
+
+    def get_option(self, option: int) -> int:
+        v = ctypes.c_int64()
+        self._check(self._L.wc_get_option(self._h, int(option), ctypes.byref(v)))
+        return int(v.value)
 
     def profile_enable(self, on: bool = True):
         self._check(self._L.wc_profile_enable(self._h, 1 if on else 0))

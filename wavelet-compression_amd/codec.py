@@ -36,6 +36,24 @@ from . import capi
 XZ_PRESET = 6
 XZ_CHECK = lzma.CHECK_CRC64
 
+
+def parse_xz_preset(text: str) -> int:
+    """"0".."9", optionally followed by "e" (extreme) -> lzma preset value."""
+    t = str(text)
+    if len(t) in (1, 2) and t[0].isdigit() and (len(t) == 1 or t[1] == "e"):
+        return int(t[0]) | (lzma.PRESET_EXTREME if len(t) == 2 else 0)
+    raise ValueError(f"xz preset: 0-9, optionally followed by e, not {text!r}")
+
+
+def xz_preset() -> int:
+    """The preset of compress(): the reference's 6, or $WCAMD_XZ_PRESET (SURVEY
+    §8(f) row 1, an optional faster preset; the reference's stream decoder,
+    src/decompressor.cpp:189, reads any).  The C++ host library reads the same
+    variable (include/wavelet_amd/xz_pool.h)."""
+    import os
+    v = os.environ.get("WCAMD_XZ_PRESET")
+    return XZ_PRESET if not v else parse_xz_preset(v)
+
 _ctx_lock = threading.Lock()
 _ctxs: dict = {}
 
@@ -135,7 +153,7 @@ def compress(box: Sequence[np.ndarray], components: Sequence[int], keep: float, 
             f = None  # a failed ofstream open silently skips the file (src/compressor.cpp:256-257)
         if f is not None:
             with f:
-                f.write(lzma.compress(p, format=lzma.FORMAT_XZ, check=XZ_CHECK, preset=XZ_PRESET))
+                f.write(lzma.compress(p, format=lzma.FORMAT_XZ, check=XZ_CHECK, preset=xz_preset()))
         out.append(cw)
     return out
 

@@ -13,6 +13,7 @@
 
 #include "log.h"
 #include "wavelet_amd/argparse.h"
+#include "wavelet_amd/xz_pool.h"
 
 using namespace wavelet_amd;
 
@@ -100,6 +101,11 @@ Config parse_config_compress() {
     if (!queryarr("components", cfg.components)) log_error("Missing component list!");
     if (!query("keep", cfg.keep)) log_error("Missing 'keep' parameter!");
     if (!query("compresseddir", cfg.compressed_dir)) log_error("Missing compresseddir!");
+    std::string preset;  // optional, not a reference parameter: no error when absent
+    if (query("xzpreset", preset)) {
+        cfg.xz_preset = parse_xz_preset(preset.c_str());
+        if (cfg.xz_preset < 0) log_error("Bad xzpreset (0-9, optionally followed by e): " + preset);
+    }
     return cfg;
 }
 

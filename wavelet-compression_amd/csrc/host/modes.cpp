@@ -288,6 +288,9 @@ void compress_run(const RunIndex& r, double keep, const std::filesystem::path& d
 }  // namespace
 
 int compress(const Config& cfg) {
+    if (cfg.xz_preset >= 0) set_xz_preset((uint32_t)cfg.xz_preset);
+    if (xz_preset() != 6) log_info("xz preset " + std::to_string(xz_preset() & 0xff) +
+                                   ((xz_preset() & 0x80000000u) ? "e" : "") + " (the reference's is 6)");
     const std::vector<std::string> files = format_files(cfg.data_dir, cfg.min_time, cfg.max_time);
     const std::vector<int> levels = format_levels(cfg.min_level, cfg.max_level);
     const int num_times = (int)files.size(), num_levels = (int)levels.size();

@@ -49,9 +49,39 @@ void parallel_for(size_t n, int threads, const std::function<void(size_t)>& fn) 
     for (auto& th : pool) th.join();
 }
 
-std::string xz_encode(const uint8_t* data, size_t size) {
+int parse_xz_preset(const char* text) {
+    if (!text || text[0] < '0' || text[0] > '9') return -1;
+    uint32_t v = (uint32_t)(text[0] - '0');
+    if (text[1] == 'e' && text[2] == '\0') return (int)(v | LZMA_PRESET_EXTREME);
+    return text[1] == '\0' ? (int)v : -1;
+}
+
+namespace {
+std::atomic<int> g_preset{-1};  // -1: not chosen yet ($WCAMD_XZ_PRESET or 6)
+}
+
+uint32_t xz_preset() {
+    int p = g_preset.load(std::memory_order_relaxed);
+    if (p < 0) {
+        p = 6;
+        if (const char* e = std::getenv("WCAMD_XZ_PRESET")) {
+            const int v = parse_xz_preset(e);
+            if (v < 0) fatal(std::string("WCAMD_XZ_PRESET: 0-9, optionally followed by e, not ") + e);
+            p = v;
+        }
+        int expect = -1;
+        g_preset.compare_exchange_strong(expect, p);
+        p = g_preset.load(std::memory_order_relaxed);
+    }
+    return (uint32_t)p;
+}
+
+void set_xz_preset(uint32_t preset) { g_preset.store((int)preset, std::memory_order_relaxed); }
+
+std::string xz_encode(const uint8_t* data, size_t size, int preset) {
     lzma_stream strm = LZMA_STREAM_INIT;
-    if (lzma_easy_encoder(&strm, 6, LZMA_CHECK_CRC64) != LZMA_OK) fatal("Failed to initialize LZMA encoder");
+    const uint32_t pr = preset >= 0 ? (uint32_t)preset : xz_preset();
+    if (lzma_easy_encoder(&strm, pr, LZMA_CHECK_CRC64) != LZMA_OK) fatal("Failed to initialize LZMA encoder");
     std::string out(static_cast<size_t>(size * 1.1) + 128, '\0');
     strm.next_in = data;
     strm.avail_in = size;

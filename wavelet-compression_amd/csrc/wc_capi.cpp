@@ -34,15 +34,18 @@ size_t transform_fast_lds_bytes(int lbx, int lby, int lbz);
 hipError_t launch_transform(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
                             float*, int, unsigned long long*);
 hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
-                                 float*, int, unsigned long long*, uint8_t*, uint32_t*, double);
+                                 float*, int, unsigned long long*, uint8_t*, uint32_t*, double, uint32_t);
+uint32_t transform_pf_grid(size_t lds);
+uint32_t inverse_rows_grid(size_t lds);
 hipError_t launch_transform_fallback(hipStream_t, const void*, int, const UnitDev*, int, const XTile*, size_t, float*,
                                      const unsigned long long*, const uint32_t*, double);
 hipError_t launch_pack(hipStream_t, const UnitDev*, int, const uint32_t*, const uint8_t*, uint64_t*, uint8_t*);
 hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, const FTile*, uint32_t,
                          unsigned long long*, uint32_t, const uint8_t*, const uint64_t*, uint32_t*,
                          unsigned long long*, float*, uint2*, uint32_t*, int);
-hipError_t launch_inverse_rows(hipStream_t, const RTile*, uint32_t, size_t, const uint8_t*, const uint64_t*,
-                               const uint2*, float*, int, const void*, int, const UnitDev*, int, double*, double*);
+hipError_t launch_inverse_rows(hipStream_t, const RTile*, uint32_t, size_t, uint32_t, const uint8_t*,
+                               const uint64_t*, const uint2*, float*, int, const void*, int, const UnitDev*, int,
+                               double*, double*);
 hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const XTile*, uint32_t, size_t, uint32_t,
                           size_t, float*);
 hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDev*, int, const FTile*,
@@ -106,7 +109,8 @@ struct wc_ctx {
     Plan plan;
     bool plan_valid = false;
     bool opt_ordered = true;  // WC_OPT_ORDERED (see include/wavelet_amd.h)
-    bool force_tickets = false;  // a _host call retrying after a look-back timeout
+    bool force_tickets = false;  // WC_OPT_TICKETS: sticky ticket form (set by a look-back timeout)
+    uint32_t opt_spin_limit = 0; // WC_OPT_SPIN_LIMIT (0: kSpinLimit), mirrored in errflag[1]
     bool timed_out = false;      // the last error was a look-back wait that timed out
     bool registered = false;     // counted in g_dev_ctx
     bool opt_sparse = true;   // WC_OPT_SPARSE
@@ -141,6 +145,8 @@ struct wc_ctx {
     size_t pinned_bytes = 0;
     // plans of earlier batches (most recent last), swapped in when a batch recurs
     std::vector<Plan> plan_cache;
+    // persistent-grid sizes (resident workgroups for an LDS size) on this device
+    std::map<std::pair<int, size_t>, uint32_t> grids;
     // per-kernel event timing (wc_profile_enable / wc_profile_read)
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -587,6 +593,17 @@ int ensure_scratch(wc_ctx* c) {
     return WC_OK;
 }
 
+// Resident workgroups of a persistent kernel (which: 0 k_transform_fast_pf,
+// 1 k_inverse_rows) for an LDS size, cached per context (one device).
+uint32_t persistent_grid(wc_ctx* c, int which, size_t lds) {
+    auto key = std::make_pair(which, lds);
+    auto it = c->grids.find(key);
+    if (it != c->grids.end()) return it->second;
+    const uint32_t g = which == 0 ? transform_pf_grid(lds) : inverse_rows_grid(lds);
+    c->grids[key] = g;
+    return g;
+}
+
 int set_device(wc_ctx* c) {
     c->staged = false;
     hipError_t e = hipSetDevice(c->device);
@@ -602,8 +619,19 @@ int set_device(wc_ctx* c) {
 std::mutex g_dev_mu;
 std::map<int, int> g_dev_ctx;
 
+// WCAMD_SHARED_DEVICE=1 (read once per process): this process shares its GPUs
+// with other processes that run look-back kernels, so every context takes the
+// ticket form (the launch-order form's dispatch assumption does not hold).
+bool shared_device_env() {
+    static const bool v = [] {
+        const char* e = std::getenv("WCAMD_SHARED_DEVICE");
+        return e && *e && std::strcmp(e, "0") != 0;
+    }();
+    return v;
+}
+
 bool use_ordered(const wc_ctx* c) {
-    if (!c->opt_ordered || c->force_tickets) return false;
+    if (!c->opt_ordered || c->force_tickets || shared_device_env()) return false;
     std::lock_guard<std::mutex> lk(g_dev_mu);
     auto it = g_dev_ctx.find(c->device);
     return it == g_dev_ctx.end() || it->second <= 1;
@@ -627,7 +655,11 @@ int check_kernel_errors(wc_ctx* c) {
         return fail(c, WC_ERR_FORMAT, buf);
     }
     if (flag & kErrTimeout) {
+        // Sticky: a launch-order look-back that timed out means another
+        // kernel holds the dispatch slots its predecessors need (a shared
+        // device); every later call of this context takes the ticket form.
         c->timed_out = true;
+        c->force_tickets = true;
         return fail(c, WC_ERR_HIP, "a dependency wait between workgroups timed out");
     }
     return WC_OK;
@@ -652,7 +684,7 @@ int stage_transform(wc_ctx* c, const void* d_cells, int dtype, double keep, bool
         e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, coef, 0, key);
         if (e == hipSuccess)
             e = launch_transform_fast(c->stream, d_cells, dtype, du, dxt + P.ngen, P.nfast, P.lds_fast, coef, 0,
-                                      key, flags, spos, keep);
+                                      key, flags, spos, keep, persistent_grid(c, 0, P.lds_fast));
         // units whose thresh came out < 0 need every coefficient (rare: negative signed max)
         if (e == hipSuccess && flags)
             e = launch_transform_fallback(c->stream, d_cells, dtype, du, (int)P.units.size(), dxt, P.lds_fast, coef,
@@ -785,7 +817,15 @@ const char* wc_last_error(const wc_ctx* c) { return c ? c->err.c_str() : "null c
 
 int wc_set_stream(wc_ctx* c, void* s) {
     if (!c) return WC_ERR_INVALID;
-    c->stream = s ? (hipStream_t)s : c->own;
+    hipStream_t next = s ? (hipStream_t)s : c->own;
+    // Kernels queued on the old stream may still read the plan's descriptors
+    // and the scratch, which later calls rebuild or reuse in stream order on
+    // the new stream: drain the old one first.
+    if (next != c->stream) {
+        hipError_t e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) return hip_fail(c, e, "wc_set_stream: synchronize the previous stream");
+    }
+    c->stream = next;
     return WC_OK;
 }
 
@@ -816,8 +856,37 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
             if (value < 0) return fail(c, WC_ERR_INVALID, "WC_OPT_HOST_CHUNK: cells >= 0");
             c->opt_host_chunk = value;
             return WC_OK;
+        case WC_OPT_SPIN_LIMIT: {
+            if (value < 0 || value > 0xffffffffll) return fail(c, WC_ERR_INVALID, "WC_OPT_SPIN_LIMIT: 0..2^32-1 polls");
+            hipError_t e;
+            if ((e = hipSetDevice(c->device)) != hipSuccess ||
+                (e = hipMemsetD32Async((hipDeviceptr_t)((uint32_t*)c->errflag.p + 1), (int)(uint32_t)value, 1,
+                                       c->stream)) != hipSuccess)
+                return hip_fail(c, e, "WC_OPT_SPIN_LIMIT");
+            c->opt_spin_limit = (uint32_t)value;
+            return WC_OK;
+        }
+        case WC_OPT_TICKETS:
+            c->force_tickets = value != 0;
+            return WC_OK;
         default:
             return fail(c, WC_ERR_INVALID, "unknown option");
+    }
+}
+
+int wc_get_option(const wc_ctx* c, int option, int64_t* value) {
+    if (!c || !value) return WC_ERR_INVALID;
+    switch (option) {
+        case WC_OPT_SPARSE: *value = c->opt_sparse; return WC_OK;
+        case WC_OPT_ORDERED: *value = use_ordered(c) ? 1 : 0; return WC_OK;  // the form the next launch takes
+        case WC_OPT_INVERSE_ROWS: *value = c->opt_inv_rows; return WC_OK;
+        case WC_OPT_RIX_LDS: *value = c->opt_rix_lds; return WC_OK;
+        case WC_OPT_RIX_TX: *value = c->opt_rix_lx; return WC_OK;
+        case WC_OPT_RIX_BLOCKED: *value = c->opt_rix_blocked; return WC_OK;
+        case WC_OPT_HOST_CHUNK: *value = c->opt_host_chunk; return WC_OK;
+        case WC_OPT_SPIN_LIMIT: *value = c->opt_spin_limit; return WC_OK;
+        case WC_OPT_TICKETS: *value = c->force_tickets ? 1 : 0; return WC_OK;
+        default: return WC_ERR_INVALID;
     }
 }
 
@@ -948,7 +1017,7 @@ int wc_decompose(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units
     hipError_t e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, d_flat, 1, nullptr);
     if (e == hipSuccess)
         e = launch_transform_fast(c->stream, d_cells, dtype, du, dxt + P.ngen, P.nfast, P.lds_fast, d_flat, 1,
-                                  nullptr, nullptr, nullptr, 0.0);
+                                  nullptr, nullptr, nullptr, 0.0, persistent_grid(c, 0, P.lds_fast));
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "transform launch");
 }
 
@@ -968,7 +1037,8 @@ int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets,
     // carry the call's epoch.  The dense coefficient scratch is fully written
     // by the decode (no memset).
     uint8_t* st = (uint8_t*)c->state.p;
-    if ((!P.dtiles.empty() || !use_ordered(c)) &&
+    const bool ord = use_ordered(c);  // once: the clear below and the launch must agree
+    if ((!P.dtiles.empty() || !ord) &&
         (e = hipMemsetAsync(st, 0, decode_state_bytes(P), c->stream)) != hipSuccess)
         return hip_fail(c, e, "memset");
     c->epoch = (c->epoch + 1) & kEpochMask;
@@ -983,13 +1053,13 @@ int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets,
                           (uint32_t)P.dtiles.size(), (const FTile*)P.d_rdtiles.p, (uint32_t)P.rdtiles.size(),
                           (unsigned long long*)c->istate.p, c->epoch, d_payload, d_offsets, (uint32_t*)st,
                           (unsigned long long*)(st + round_up(4ull * n, 8)), (float*)c->coef.p, (uint2*)c->rowinfo.p,
-                          (uint32_t*)c->errflag.p, use_ordered(c) ? 1 : 0);
+                          (uint32_t*)c->errflag.p, ord ? 1 : 0);
     }
     if (e != hipSuccess) return hip_fail(c, e, "decode launch");
     {
         StageTimer t(c, WC_STAGE_INVERSE);
         e = launch_inverse_rows(c->stream, (const RTile*)P.d_rtiles.p, (uint32_t)P.rtiles.size(), P.lds_rows,
-                                d_payload, d_offsets,
+                                P.rtiles.empty() ? 1u : persistent_grid(c, 1, P.lds_rows), d_payload, d_offsets,
                                 (const uint2*)c->rowinfo.p, d_out, c->opt_rix_blocked ? 1 : 0, d_orig, dtype,
                                 (const UnitDev*)P.d_units.p, n, (double*)c->part.p, d_rmse);
         if (e == hipSuccess)
@@ -1323,12 +1393,10 @@ extern "C++" {
 template <class F>
 static int with_ticket_retry(wc_ctx* c, F once) {
     c->timed_out = false;
+    const bool was_tickets = c->force_tickets;
     int rc = once();
-    if (rc == WC_ERR_HIP && c->timed_out && !c->force_tickets) {
-        c->force_tickets = true;
-        rc = once();
-        c->force_tickets = false;
-    }
+    // check_kernel_errors made the ticket form sticky; run once more with it
+    if (rc == WC_ERR_HIP && c->timed_out && !was_tickets) rc = once();
     return rc;
 }
 }

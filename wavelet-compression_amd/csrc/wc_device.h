@@ -161,9 +161,12 @@ __device__ __forceinline__ void add_rlx(uint32_t* p, uint32_t v) {
 
 // Bounded spin with backoff: pollers share the memory system with the
 // streaming loads (MI355X_MICROARCH.md: 255 pollers cut chip bandwidth
-// 37-71 %), so re-polls slow down from ~0.2 us to ~1.7 us.
+// 37-71 %), so re-polls slow down from ~0.2 us to ~1.7 us.  err[0] is the
+// context's error word, err[1] its poll bound (WC_OPT_SPIN_LIMIT; 0 = the
+// default kSpinLimit), read only by a wave that is already waiting.
 __device__ __forceinline__ bool spin_fail(uint32_t& spins, uint32_t* err) {
-    if (++spins > kSpinLimit) {
+    const uint32_t lim = __hip_atomic_load(err + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (++spins >= (lim ? lim : kSpinLimit)) {  // lim 1: the first unanswered poll fails
         atomicOr(err, kErrTimeout);
         return true;
     }

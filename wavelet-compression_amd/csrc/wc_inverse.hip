@@ -593,9 +593,11 @@ __global__ __launch_bounds__(kThreads) void k_inverse_fast(const float* __restri
 // when scattered) and the row entries of tile t + 2G.
 //
 // The row index of a unit is complete and monotone whatever the payload
-// (k_rowindex), negative runs count as 0 as there, and every LDS address is
-// checked against the range: a malformed payload (reported by K5) gives
-// garbage cells, never an out-of-bounds access.
+// (k_rowindex), negative runs count as 0 as there, every pair index is
+// clamped to the header's nrle (rix_load_range: a row index left incomplete
+// by a timed-out look-back cannot point past the payload) and every LDS
+// address is checked against the range: a malformed payload (reported by K5)
+// gives garbage cells, never an out-of-bounds access.
 #ifndef WC_RIX_ROUNDS
 #define WC_RIX_ROUNDS 20  // 128 VGPRs with the x-quad synthesis: 4 waves per SIMD, no spills
 #endif
@@ -610,18 +612,25 @@ struct RixRange {
     uint32_t ks, c0, e;  // rowinfo[r0] = (ks, c0), rowinfo[r0 + tyv].x = e
 };
 
-__device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* __restrict__ rowinfo, int w, int l) {
+// ph: the unit's payload header.  The pair indices are clamped to its nrle,
+// so every pair load stays inside this payload even when the row entries are
+// not this call's (a row-index look-back that timed out leaves some unwritten:
+// they hold an earlier batch's entries; the call then reports WC_ERR_HIP).
+__device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* __restrict__ rowinfo, int w, int l,
+                                                   const uint8_t* __restrict__ ph) {
     RixRange R{0u, 0u, 0u};
     const int TX = 1 << T.lbx;
     if (l < TX) {
+        const int32_t nh = reinterpret_cast<const int32_t*>(ph)[4];
+        const uint32_t nrle = nh > 0 ? (uint32_t)nh : 0u;
         const int g = w + 4 * l, bxl = g & (TX - 1), ssy = (g >> T.lbx) & 1, ssx = g >> (T.lbx + 1);
         const int bx = T.bx0 + bxl, hx = T.W >> 1, hy = T.H >> 1;
         if (bx < hx) {
             const uint64_t r0 = (uint64_t)(bx + ssx * hx) * T.H + T.by0 + ssy * hy;
             const uint2 a = rowinfo[T.row_off + r0];
-            R.ks = a.x;
+            R.ks = min(a.x, nrle);
             R.c0 = a.y;
-            R.e = rowinfo[T.row_off + r0 + T.tyv].x;
+            R.e = min(rowinfo[T.row_off + r0 + T.tyv].x, nrle);
         }
     }
     return R;
@@ -744,8 +753,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
 
     // prologue: tile t's ranges and pairs in flight, tile t + G's row entries
     RTile T = tiles[t];
-    const uint2* pr = reinterpret_cast<const uint2*>(payload + offsets[T.unit] + 20);
-    RixRange R = rix_load_range(T, rowinfo, w, l);
+    const uint8_t* ph0 = payload + offsets[T.unit];
+    const uint2* pr = reinterpret_cast<const uint2*>(ph0 + 20);
+    RixRange R = rix_load_range(T, rowinfo, w, l, ph0);
     RixPlan PL = rix_plan(T, R, l);
     constexpr int NR = OT ? kRixRounds - 4 : kRixRounds;  // the RMSE pass needs registers
     uint2 q[NR];
@@ -758,8 +768,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
     const uint2* pr1 = pr;
     if (t1 < tend) {
         T1 = tiles[t1];
-        pr1 = reinterpret_cast<const uint2*>(payload + offsets[T1.unit] + 20);
-        R1 = rix_load_range(T1, rowinfo, w, l);
+        const uint8_t* ph1 = payload + offsets[T1.unit];
+        pr1 = reinterpret_cast<const uint2*>(ph1 + 20);
+        R1 = rix_load_range(T1, rowinfo, w, l, ph1);
     }
 
     for (;;) {
@@ -807,8 +818,9 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
                 if ((uint32_t)r < PL1.nrounds) q[r] = rix_load_round(pr1, R1, PL1, l, r);
             if (t2 < tend) {
                 T2 = tiles[t2];
-                pr2 = reinterpret_cast<const uint2*>(payload + offsets[T2.unit] + 20);
-                R2 = rix_load_range(T2, rowinfo, w, l);
+                const uint8_t* ph2 = payload + offsets[T2.unit];
+                pr2 = reinterpret_cast<const uint2*>(ph2 + 20);
+                R2 = rix_load_range(T2, rowinfo, w, l, ph2);
             }
         }
 
@@ -1039,16 +1051,9 @@ hipError_t launch_inverse(hipStream_t st, const float* flat, int flat_at_cell_of
     return hipGetLastError();
 }
 
-// Workgroups of k_inverse_rows resident at once for `lds` bytes (persistent grid).
-static uint32_t rows_grid(size_t lds) {
-    static size_t cached_lds = 0;
-    static uint32_t cached = 0;
-    if (cached_lds != lds || !cached) {
-        cached = resident_grid((const void*)k_inverse_rows<0>, lds);
-        cached_lds = lds;
-    }
-    return cached;
-}
+// Workgroups of k_inverse_rows resident at once for `lds` bytes on the current
+// device (persistent grid; the caller caches it per context and LDS size).
+uint32_t inverse_rows_grid(size_t lds) { return resident_grid((const void*)k_inverse_rows<0>, lds); }
 
 // calc_rmse_per_box of the fused form: unit u's K6r tile sums in tile order.
 __global__ __launch_bounds__(64) void k_rmse_rows_final(const UnitDev* __restrict__ units,
@@ -1065,11 +1070,12 @@ __global__ __launch_bounds__(64) void k_rmse_rows_final(const UnitDev* __restric
 
 // orig == null: the inverse alone; else also calc_rmse_per_box against orig
 // (dtype 1 fp64, 0 fp32) into rmse[n] via part[ntiles].
-hipError_t launch_inverse_rows(hipStream_t st, const RTile* tiles, uint32_t ntiles, size_t lds, const uint8_t* payload,
-                               const uint64_t* offsets, const uint2* rowinfo, float* out, int blocked,
-                               const void* orig, int dtype, const UnitDev* units, int n, double* part, double* rmse) {
+hipError_t launch_inverse_rows(hipStream_t st, const RTile* tiles, uint32_t ntiles, size_t lds, uint32_t max_grid,
+                               const uint8_t* payload, const uint64_t* offsets, const uint2* rowinfo, float* out,
+                               int blocked, const void* orig, int dtype, const UnitDev* units, int n, double* part,
+                               double* rmse) {
     if (!ntiles) return hipSuccess;
-    const uint32_t grid = std::min(ntiles, rows_grid(lds));
+    const uint32_t grid = std::min(ntiles, std::max(1u, max_grid));
     if (!orig)
         k_inverse_rows<0><<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out, blocked, orig,
                                                        part);

@@ -220,28 +220,26 @@ hipError_t launch_transform(hipStream_t st, const void* cells, int dtype, const 
     return hipGetLastError();
 }
 
-// Workgroups of k_transform_fast_pf that fit on the device at once.
-static uint32_t pf_grid(size_t lds, bool keys) {
-    static int per_cu[2] = {0, 0}, ncu = 0;
-    const int k = keys ? 1 : 0;
-    if (!per_cu[k]) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        const void* fn = keys ? (const void*)k_transform_fast_pf<true> : (const void*)k_transform_fast_pf<false>;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[k], fn, kThreads, lds) != hipSuccess ||
-            per_cu[k] < 1)
-            per_cu[k] = 2;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
-    }
-    return (uint32_t)per_cu[k] * (uint32_t)ncu;
+// Workgroups of k_transform_fast_pf that fit on the current device at once
+// (keys and no-keys forms share the register budget; the caller caches it).
+uint32_t transform_pf_grid(size_t lds) {
+    int per_cu = 0, ncu = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_transform_fast_pf<true>, kThreads, lds) !=
+            hipSuccess ||
+        per_cu < 1)
+        per_cu = 2;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+    return (uint32_t)per_cu * (uint32_t)ncu;
 }
 
 hipError_t launch_transform_fast(hipStream_t st, const void* cells, int dtype, const UnitDev* units,
                                  const XTile* tiles, uint32_t ntiles, size_t lds, float* out,
-                                 int out_mode, unsigned long long* keys, uint8_t* flags, uint32_t* spos, double keep) {
+                                 int out_mode, unsigned long long* keys, uint8_t* flags, uint32_t* spos, double keep,
+                                 uint32_t pf_grid) {
     if (ntiles == 0) return hipSuccess;
     if (dtype != 1 && !flags) {  // fp32 cells, dense staging: persistent, next tile's cells in flight
-        const uint32_t grid = std::min(ntiles, pf_grid(lds, keys != nullptr));
+        const uint32_t grid = std::min(ntiles, std::max(1u, pf_grid));
         if (keys)
             k_transform_fast_pf<true><<<grid, kThreads, lds, st>>>((const float*)cells, units, tiles, ntiles, out,
                                                                  out_mode, keys);
