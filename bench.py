@@ -65,9 +65,10 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="time budget of each CPU-baseline sample (boxes run until it is spent)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r02" / "pmc_forward.json"),
-                    help="PMC traffic summary (tools/pmc_summary.py) merged into roofline.traffic when it "
-                         "was measured on the same kernel sources")
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r03"),
+                    help="PMC traffic summaries (tools/pmc_summary.py): a file or a directory of pmc_*.json, "
+                         "one per workload; merged into roofline.traffic and each leg's roofline_path.traffic "
+                         "when measured on the same workload AND the same kernel sources")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU/gloo run of the launcher, sharding and reductions (no kernels, no numbers)")
     ap.add_argument("--rehearse", action="store_true",
@@ -284,26 +285,48 @@ def stage_times(ctx, step, steps):
     return {k: (ms / cnt, cnt / steps) for k, (ms, cnt) in ctx.profile_read().items()}
 
 
-def pmc_traffic(path, workload, dtype, kernel):
-    """Counter bytes per launch for `kernel` from a committed rocprofv3 PMC summary,
-    only if it was measured on this workload AND these kernel sources."""
+FWD_STAGES = ("transform", "fallback", "emit")
+INV_STAGES = ("rowindex", "decode", "inverse", "rmse")
+
+
+def pmc_summary(path, workload, dtype):
+    """The committed rocprofv3 PMC summary of `workload` (a file, or pmc_*.json in a
+    directory), only if measured on this workload AND these kernel sources."""
     p = Path(path)
-    if not p.exists():
-        return None, {"source": None, "note": "no PMC summary"}
-    try:
-        pmc = json.loads(p.read_text())
-    except Exception:
-        return None, {"source": str(p), "note": "unreadable"}
-    meta = {"source": str(p.relative_to(ROOT)) if p.is_relative_to(ROOT) else str(p),
-            "date": pmc.get("date"), "git": pmc.get("git")}
-    cfg = pmc.get("config", {})
-    if cfg.get("workload") != workload or cfg.get("dtype") != dtype:
-        meta["note"] = "measured on another workload"
-        return None, meta
-    if pmc.get("kernel_sources_sha") != kernel_sources_sha():
-        meta["note"] = "stale: kernel sources changed since the counter run"
-        return None, meta
-    return pmc.get("per_launch_bytes", {}).get(kernel), meta
+    files = sorted(p.glob("pmc_*.json")) if p.is_dir() else ([p] if p.exists() else [])
+    meta = {"source": None, "note": "no PMC summary for this workload"}
+    for f in files:
+        try:
+            pmc = json.loads(f.read_text())
+        except Exception:
+            continue
+        cfg = pmc.get("config", {})
+        if cfg.get("workload") != workload or cfg.get("dtype") != dtype:
+            continue
+        meta = {"source": str(f.relative_to(ROOT)) if f.is_relative_to(ROOT) else str(f),
+                "date": pmc.get("date"), "git": pmc.get("git")}
+        if pmc.get("kernel_sources_sha") != kernel_sources_sha():
+            meta["note"] = "stale: kernel sources changed since the counter run"
+            return None, meta
+        return pmc, meta
+    return None, meta
+
+
+def pmc_traffic(path, workload, dtype, kernel):
+    """Counter bytes per launch of `kernel` (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE)."""
+    pmc, meta = pmc_summary(path, workload, dtype)
+    return (pmc.get("per_launch_bytes", {}).get(kernel) if pmc else None), meta
+
+
+def path_traffic(path, workload, dtype, stages, alg_bytes):
+    """Counter bytes per step of the kernels of `stages`, beside the algorithmic bytes."""
+    pmc, meta = pmc_summary(path, workload, dtype)
+    per = (pmc or {}).get("per_step_bytes")
+    if not per:
+        return {"traffic": None, "traffic_source": meta}
+    t = sum(v for k, v in per.items() if k in stages)
+    return {"traffic": t, "traffic_ratio": t / alg_bytes if alg_bytes else None,
+            "traffic_by_kernel": {k: v for k, v in per.items() if k in stages}, "traffic_source": meta}
 
 
 # ---------------------------------------------------------------------------
@@ -363,7 +386,8 @@ def headline(args, d: Dist, ctx):
         "roofline_path": {"achieved": path_bytes / (ms_step * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS,
                           "unit": "GB/s", "frac": path_bytes / (ms_step * 1e-3) / 1e9 / PEAK_HBM_GBPS,
                           "bytes_per_step": path_bytes, "kernel_ms_per_step": path_ms,
-                          "note": "algorithmic bytes / driver-clock ms_per_step (launch gaps included)"},
+                          "note": "algorithmic bytes / driver-clock ms_per_step (launch gaps included)",
+                          **path_traffic(args.pmc, args.workload, spec["dtype"], FWD_STAGES, path_bytes)},
     }
     return out, b
 
@@ -385,7 +409,9 @@ def inverse_leg(args, d: Dist, ctx, b: Batch):
     return {"value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
             "stage_ms_per_launch": {k: round(v[0], 4) for k, v in st.items()},
             "roofline_path": {"achieved": alg / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                              "frac": alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, "bytes_per_step": alg},
+                              "frac": alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, "bytes_per_step": alg,
+                              **path_traffic(args.pmc, args.workload, "f64" if b.s_in == 8 else "f32",
+                                             INV_STAGES, alg)},
             "rmse": {"mean_per_box": m["rmse_sum"] / max(m["boxes"], 1), "max": m["max_rmse"],
                      "note": "calc_rmse_per_box of the reconstruction vs the narrowed input (GPU K7); "
                              "checked against the CPU restatement in cpu_baseline.rmse_check"}}
@@ -431,7 +457,9 @@ def round_trip_leg(args, d: Dist, name):
                              "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                              "frac": (fwd + inv + rm) / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
                              "note": "fwd + inverse + RMSE algorithmic bytes (RMSE: original cells only, "
-                                     "fused) / driver-clock step"},
+                                     "fused) / driver-clock step",
+                             **path_traffic(args.pmc, name, spec["dtype"], FWD_STAGES + INV_STAGES,
+                                            fwd + inv + rm)},
            "mean_rmse_per_component": {str(c): sum(v) / len(v) for c, v in sorted(per_comp.items())}}
     ctx.close()
     del b
@@ -474,7 +502,10 @@ def sharded_forward_leg(args, d: Dist, name, hist=False):
            "stage_ms_per_launch": {k: round(v[0], 4) for k, v in st.items()},
            "roofline_path": {"achieved_per_gpu": per_rank_alg / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS,
                              "unit": "GB/s", "frac": per_rank_alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
-                             "bytes_per_step_all_ranks": alg}}
+                             "bytes_per_step_all_ranks": alg,
+                             **(path_traffic(args.pmc, name, spec["dtype"], FWD_STAGES, per_rank_alg)
+                                if d.world == 1 else {"traffic": None, "traffic_source": {
+                                    "note": "counter summaries are for the one-GPU workload"}})}}
     if hist:
         out["global_hist"] = global_hist_leg(args, d, ctx, b)
     ctx.close()

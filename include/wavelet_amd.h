@@ -93,6 +93,8 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  * WC_OPT_K1_XCD (default 1): the transform's tile list is dealt to the XCDs in
  *   contiguous runs (neighbouring tiles share flag / mask lines in one L2).
  *   Same bytes out.
+ * WC_OPT_RIX_XCD (default 0): the same for the row-indexed inverse's tiles
+ *   (neighbouring tiles share payload lines at their range ends).  Same cells.
  * WC_OPT_ORDERED (default 1): the look-back kernels (forward emit, inverse
  *   decode) take each block's tile index from the launch order, relying on
  *   workgroups being dispatched in increasing id (DESIGN.md §Forward
@@ -141,6 +143,7 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
 #define WC_OPT_SPIN_LIMIT 19
 #define WC_OPT_TICKETS 20
 #define WC_OPT_K1_XCD 21
+#define WC_OPT_RIX_XCD 22
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 int wc_get_option(const wc_ctx* ctx, int option, int64_t* value);
 

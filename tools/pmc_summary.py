@@ -34,6 +34,7 @@ def stage(name):
 
 
 def counters(path, counter):
+    """{stage: [counter value of each dispatch]}"""
     acc = defaultdict(list)
     with open(path) as f:
         for row in csv.DictReader(f):
@@ -42,7 +43,7 @@ def counters(path, counter):
             st = stage(row.get("Kernel_Name", ""))
             if st:
                 acc[st].append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+    return acc
 
 
 def main():
@@ -53,6 +54,9 @@ def main():
     ap.add_argument("--out")
     ap.add_argument("--workload", default="c2")
     ap.add_argument("--dtype", default="f64")
+    ap.add_argument("--steps", type=int, default=0,
+                    help="forward (and inverse) executions in each counter run: adds per-step bytes per stage")
+    ap.add_argument("--note", default="")
     a = ap.parse_args()
     from bench import kernel_sources_sha  # the bench only trusts counters of the same sources
     kern = {}
@@ -65,18 +69,24 @@ def main():
     git = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True, cwd=ROOT).stdout.strip()
     out = {"config": {"workload": a.workload, "dtype": a.dtype}, "date": datetime.date.today().isoformat(),
            "git": git, "kernel_sources_sha": kernel_sources_sha(), "kernels": kern}
-    per = {}
-    if a.fetch:
-        fk = counters(a.fetch, "FETCH_SIZE")
-        for k, v in fk.items():
-            per.setdefault(k, {})["read_bytes"] = 2 * v * 1024
-    if a.write:
-        wk = counters(a.write, "WRITE_SIZE")
-        for k, v in wk.items():
-            per.setdefault(k, {})["write_bytes"] = v * 1024
+    per, step = {}, {}
+    for path, counter, key, scale in ((a.fetch, "FETCH_SIZE", "read_bytes", 2 * 1024), (a.write, "WRITE_SIZE",
+                                                                                        "write_bytes", 1024)):
+        if not path:
+            continue
+        for k, v in counters(path, counter).items():
+            per.setdefault(k, {})[key] = scale * sum(v) / len(v)
+            if a.steps:
+                step.setdefault(k, {})[key] = scale * sum(v) / a.steps
+                step[k]["launches"] = len(v) / a.steps
     if per:
         out["pmc_per_launch"] = per
         out["per_launch_bytes"] = {k: v.get("read_bytes", 0) + v.get("write_bytes", 0) for k, v in per.items()}
+    if step:
+        out["pmc_per_step"] = step
+        out["per_step_bytes"] = {k: v.get("read_bytes", 0) + v.get("write_bytes", 0) for k, v in step.items()}
+    if a.note:
+        out["note"] = a.note
     s = json.dumps(out, indent=1)
     if a.out:
         open(a.out, "w").write(s + "\n")

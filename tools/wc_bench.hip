@@ -4,9 +4,9 @@
 // synthetic field of SURVEY.md §8(d) is generated on the device (hash-based
 // Box-Muller noise), then wc_forward runs `steps` times.  Prints one JSON line.
 //
-// usage: wc_bench [boxes=1024] [dim=64] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1]
+// usage: wc_bench [boxes=1024] [dim=64|c3] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1|2]
 //                 [check=0|1] [ordered=1] [sparse=2] [rows=1] [rix_lds=9216] [rix_tx=4] [rix_blocked=0]
-//                 [k1_xcd=1]
+//                 [k1_xcd=1] [rix_xcd=0]
 // check=1: also run the conservative configuration (ticket look-back, dense
 // staging, dense inverse decode) once and compare every unit's payload bytes and, with inverse=1,
 // every reconstructed cell ("paths_identical" in the JSON line).
@@ -54,14 +54,54 @@ __global__ void synth(T* out, int dim, long long nboxes, unsigned long long seed
     }
 }
 
+// One box of any shape (the C3 layout): the same field at global origin (gx0, gy0, gz0).
+template <typename T>
+__global__ void synth_box(T* out, int W, int H, int D, int gx0, int gy0, int gz0, unsigned long long seed) {
+    const long long total = (long long)W * H * D;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int x = (int)(i % W), y = (int)((i / W) % H), z = (int)(i / ((long long)W * H));
+        const double gx = gx0 + x, gy = gy0 + y, gz = gz0 + z;
+        const unsigned long long h1 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * i + 1));
+        const unsigned long long h2 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * i + 2));
+        const double u1 = ((double)(h1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);
+        const double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
+        const double g = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+        out[i] = (T)(300.0 + 50.0 * sin(0.1 * gx) * cos(0.07 * gy) + 0.01 * gz + 0.05 * g);
+    }
+}
+
+// BASELINE configs[2] (C3) layout, SURVEY §8(d): L0 64 x 64^3, L1 96 x 64^3,
+// L2 128 x 32^3, L3 256 x 16^3 + 32 x (48 x 32 x 16), `ncomp` components per box.
+static std::vector<wc_unit> c3_layout(int ncomp) {
+    std::vector<wc_unit> u;
+    uint64_t off = 0;
+    auto add = [&](int n, int W, int H, int D) {
+        for (int b = 0; b < n; ++b)
+            for (int c = 0; c < ncomp; ++c) {
+                u.push_back(wc_unit{off, W, H, D, 0});
+                off += ((uint64_t)W * H * D + 3) & ~3ull;
+            }
+    };
+    add(64, 64, 64, 64);
+    add(96, 64, 64, 64);
+    add(128, 32, 32, 32);
+    add(256, 16, 16, 16);
+    add(32, 48, 32, 16);
+    return u;
+}
+
 int main(int argc, char** argv) {
-    const int boxes = argc > 1 ? std::atoi(argv[1]) : 1024;
-    const int dim = argc > 2 ? std::atoi(argv[2]) : 64;
+    // boxes/dim: N cubes of dim^3; dim "c3": the C3 layout with `boxes` components (4 in bench.py)
+    const bool c3 = argc > 2 && std::strcmp(argv[2], "c3") == 0;
+    const int boxes_arg = argc > 1 ? std::atoi(argv[1]) : 1024;
+    const int dim = c3 ? 0 : (argc > 2 ? std::atoi(argv[2]) : 64);
     const bool f64 = argc > 3 ? std::strcmp(argv[3], "f32") != 0 : true;
     const double keep = (double)(float)(argc > 4 ? std::atof(argv[4]) : 0.999);
     const int steps = argc > 5 ? std::atoi(argv[5]) : 10;
     const int warmup = argc > 6 ? std::atoi(argv[6]) : 2;
-    const bool inverse = argc > 7 ? std::atoi(argv[7]) != 0 : false;
+    const int inv_mode = argc > 7 ? std::atoi(argv[7]) : 0;  // 1 wc_inverse, 2 wc_inverse_rmse (fused calc_rmse_per_box)
+    const bool inverse = inv_mode != 0;
     const bool check = argc > 8 ? std::atoi(argv[8]) != 0 : false;
     const int ordered = argc > 9 ? std::atoi(argv[9]) : 1;
     const int sparse = argc > 10 ? std::atoi(argv[10]) : 2;
@@ -70,17 +110,36 @@ int main(int argc, char** argv) {
     const int rix_tx = argc > 13 ? std::atoi(argv[13]) : 4;
     const int rix_blocked = argc > 14 ? std::atoi(argv[14]) : 0;
     const int k1_xcd = argc > 15 ? std::atoi(argv[15]) : 1;
+    const int rix_xcd = argc > 16 ? std::atoi(argv[16]) : 0;
 
-    std::vector<wc_unit> units(boxes);
-    const unsigned long long per = (unsigned long long)dim * dim * dim;
-    for (int i = 0; i < boxes; ++i) units[i] = wc_unit{per * i, dim, dim, dim, 0};
+    std::vector<wc_unit> units;
+    if (c3) {
+        units = c3_layout(boxes_arg);
+    } else {
+        const unsigned long long per = (unsigned long long)dim * dim * dim;
+        for (int i = 0; i < boxes_arg; ++i) units.push_back(wc_unit{per * i, dim, dim, dim, 0});
+    }
+    const int boxes = (int)units.size();
+    const unsigned long long ncells = wc_cell_count(units.data(), boxes);
+    const unsigned long long extent = units.back().cell_offset +
+                                      (unsigned long long)units.back().nx * units.back().ny * units.back().nz;
     const size_t esz = f64 ? 8 : 4;
     void* cells = nullptr;
-    CK(hipMalloc(&cells, esz * per * boxes));
-    if (f64)
+    CK(hipMalloc(&cells, esz * extent));
+    if (c3) {
+        for (int i = 0; i < boxes; ++i) {
+            const wc_unit& u = units[i];
+            const int gx = 64 * (i % 16), gy = 64 * ((i / 16) % 8), gz = 64 * (i / 128);
+            if (f64)
+                synth_box<double><<<512, 256>>>((double*)cells + u.cell_offset, u.nx, u.ny, u.nz, gx, gy, gz, 1234 + i);
+            else
+                synth_box<float><<<512, 256>>>((float*)cells + u.cell_offset, u.nx, u.ny, u.nz, gx, gy, gz, 1234 + i);
+        }
+    } else if (f64) {
         synth<double><<<4096, 256>>>((double*)cells, dim, boxes, 1234);
-    else
+    } else {
         synth<float><<<4096, 256>>>((float*)cells, dim, boxes, 1234);
+    }
     CK(hipDeviceSynchronize());
 
     const uint64_t cap = wc_payload_bound(units.data(), boxes);
@@ -91,7 +150,9 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&payload, cap));
     CK(hipMalloc(&offsets, 8 * (boxes + 1)));
     CK(hipMalloc(&kept, 4 * boxes));
-    if (inverse) CK(hipMalloc(&regen, 4 * per * boxes));
+    double* rmse = nullptr;
+    if (inverse) CK(hipMalloc(&regen, 4 * extent));
+    if (inv_mode == 2) CK(hipMalloc(&rmse, 8 * boxes));
 
     wc_ctx* ctx = nullptr;
     if (wc_ctx_create(0, &ctx) != WC_OK) {
@@ -102,7 +163,8 @@ int main(int argc, char** argv) {
     wc_set_option(ctx, WC_OPT_SPARSE, sparse);
     wc_set_option(ctx, WC_OPT_INVERSE_ROWS, rows);
     if (wc_set_option(ctx, WC_OPT_RIX_LDS, rix_lds) != WC_OK || wc_set_option(ctx, WC_OPT_RIX_TX, rix_tx) != WC_OK ||
-        wc_set_option(ctx, WC_OPT_RIX_BLOCKED, rix_blocked) != WC_OK || wc_set_option(ctx, WC_OPT_K1_XCD, k1_xcd) != WC_OK) {
+        wc_set_option(ctx, WC_OPT_RIX_BLOCKED, rix_blocked) != WC_OK || wc_set_option(ctx, WC_OPT_K1_XCD, k1_xcd) != WC_OK ||
+        wc_set_option(ctx, WC_OPT_RIX_XCD, rix_xcd) != WC_OK) {
         std::fprintf(stderr, "options: %s\n", wc_last_error(ctx));
         return 2;
     }
@@ -114,7 +176,9 @@ int main(int argc, char** argv) {
         }
     };
     auto inv = [&]() {
-        int rc = wc_inverse(ctx, payload, offsets, units.data(), boxes, regen);
+        int rc = inv_mode == 2 ? wc_inverse_rmse(ctx, payload, offsets, units.data(), boxes, cells,
+                                                 f64 ? WC_F64 : WC_F32, regen, rmse)
+                               : wc_inverse(ctx, payload, offsets, units.data(), boxes, regen);
         if (rc != WC_OK) {
             std::fprintf(stderr, "wc_inverse: %s\n", wc_last_error(ctx));
             std::exit(2);
@@ -159,7 +223,7 @@ int main(int argc, char** argv) {
             CK(hipMemset(payload, 0xA5, cap));
             fwd();
             if (inverse) {
-                CK(hipMemset(regen, 0xA5, 4 * per * boxes));
+                CK(hipMemset(regen, 0xA5, 4 * extent));
                 inv();
             }
             if (wc_synchronize(ctx) != WC_OK) {
@@ -170,8 +234,8 @@ int main(int argc, char** argv) {
             CK(hipMemcpy(k.data(), kept, 4 * boxes, hipMemcpyDeviceToHost));
             CK(hipMemcpy(pl.data(), payload, cap, hipMemcpyDeviceToHost));
             if (inverse) {
-                rg.resize(per * boxes);
-                CK(hipMemcpy(rg.data(), regen, 4 * per * boxes, hipMemcpyDeviceToHost));
+                rg.resize(extent);
+                CK(hipMemcpy(rg.data(), regen, 4 * extent, hipMemcpyDeviceToHost));
             }
         };
         run(off_a, k_a, pa, ra);
@@ -199,8 +263,8 @@ int main(int argc, char** argv) {
     std::printf("{\"boxes\": %d, \"dim\": %d, \"dtype\": \"%s\", \"keep\": %.17g, \"steps\": %d, "
                 "\"ms_per_step\": %.4f, \"cells_per_s\": %.6e, \"kept_fraction\": %.6f, \"payload_bytes\": %llu, "
                 "\"ordered\": %d, \"sparse\": %d, \"rows\": %d, \"rix\": [%d, %d, %d], \"paths_identical\": %d, \"stage_ms\": {",
-                boxes, dim, f64 ? "f64" : "f32", keep, steps, step_ms, per * boxes / (step_ms * 1e-3),
-                ksum / (double)(per * boxes), (unsigned long long)total, ordered, sparse, rows, rix_lds, rix_tx, rix_blocked, identical);
+                boxes, dim, f64 ? "f64" : "f32", keep, steps, step_ms, ncells / (step_ms * 1e-3),
+                ksum / (double)ncells, (unsigned long long)total, ordered, sparse, rows, rix_lds, rix_tx, rix_blocked, identical);
     bool first = true;
     for (int s = 0; s < WC_NUM_STAGES; ++s)
         if (cnt[s]) {
@@ -224,5 +288,6 @@ int main(int argc, char** argv) {
     (void)hipFree(offsets);
     (void)hipFree(kept);
     if (regen) (void)hipFree(regen);
+    if (rmse) (void)hipFree(rmse);
     return 0;
 }

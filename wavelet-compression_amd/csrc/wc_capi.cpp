@@ -17,9 +17,6 @@
 #ifndef WC_PACK128
 #define WC_PACK128 1  // D = 128 units: 16 x 1 x 64-block transform tiles and packed rows
 #endif
-#ifndef WC_RIX_XCD
-#define WC_RIX_XCD 0  // measured: fewer fetched bytes, slower through bench.py
-#endif
 
 #include <algorithm>
 #include <cmath>
@@ -83,6 +80,7 @@ struct Plan {
     std::vector<FTile> ftiles, dtiles, rdtiles;  // dtiles: dense decode, rdtiles: row index (K5)
     int rix_lds = kRixLds;              // WC_OPT_RIX_LDS the plan was built with
     int rix_lx = 4;                     // WC_OPT_RIX_TX the plan was built with
+    bool rix_xcd = false;               // WC_OPT_RIX_XCD the plan was built with
     // emit blocks in 4 launch segments: (kEmitTile, kEmitTileBig) tiles x (other
     // units, packed-row units), each segment's units in the interleaved order
     std::vector<EmitDesc> edesc;
@@ -125,6 +123,7 @@ struct wc_ctx {
     int opt_rix_lds = kRixLds; // WC_OPT_RIX_LDS
     int opt_rix_lx = 4;        // WC_OPT_RIX_TX
     bool opt_rix_blocked = false; // WC_OPT_RIX_BLOCKED
+    bool opt_rix_xcd = false;     // WC_OPT_RIX_XCD
     // A kernel that may raise error bits ran since the last check.  Kernels
     // atomicOr into ONE persistent error word (errflag, zeroed at creation and
     // after each read), so errors of several async calls accumulate until the
@@ -371,6 +370,7 @@ bool set_rix_tiling(UnitDev& d, int budget, int max_lx) {
 
 bool plan_matches(const wc_ctx* c, const Plan& P, const wc_unit* units, int n) {
     return P.inv_rows == c->opt_inv_rows && P.rix_lds == c->opt_rix_lds && P.rix_lx == c->opt_rix_lx &&
+           P.rix_xcd == c->opt_rix_xcd &&
            (int)P.key.size() == n && (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0);
 }
 
@@ -420,6 +420,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     P.inv_rows = c->opt_inv_rows;
     P.rix_lds = c->opt_rix_lds;
     P.rix_lx = c->opt_rix_lx;
+    P.rix_xcd = c->opt_rix_xcd;
     P.units.assign(n, UnitDev{});
     P.xtiles.clear();
     P.ftiles.clear();
@@ -497,14 +498,14 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
             P.lds_rows = std::max(P.lds_rows, rix_lds_bytes(d));
         }
     }
-#if WC_RIX_XCD
-    // K6r tile order, XCD-grouped: workgroups b and b + 8 share an XCD (blocks
-    // are dealt round-robin over the 8 XCDs; the persistent grid is a multiple
-    // of 8), so list position p = 8i + x holds tile start_x + i of a contiguous
-    // unit-order run per XCD.  A round of the grid then puts each XCD on a run
-    // of whole units: neighbouring tiles of a unit, whose flat-row ranges share
-    // payload lines and row entries at their ends, read them through one L2.
-    if (P.rtiles.size() > 8) {
+    // K6r tile order, XCD-grouped (WC_OPT_RIX_XCD): workgroups b and b + 8
+    // share an XCD (blocks are dealt round-robin over the 8 XCDs; the
+    // persistent grid is a multiple of 8), so list position p = 8i + x holds
+    // tile start_x + i of a contiguous unit-order run per XCD.  A round of the
+    // grid then puts each XCD on a run of whole units: neighbouring tiles of a
+    // unit, whose flat-row ranges share payload lines and row entries at their
+    // ends, read them through one L2.
+    if (P.rix_xcd && P.rtiles.size() > 8) {
         const size_t T = P.rtiles.size();
         std::vector<RTile> perm(T);
         size_t start = 0;
@@ -515,7 +516,6 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         }
         P.rtiles.swap(perm);
     }
-#endif
     P.ngen = (uint32_t)gen.size();
     P.nfast = (uint32_t)fast.size();
     for (UnitDev& d : P.units)
@@ -863,6 +863,9 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
         case WC_OPT_K1_XCD:
             c->opt_k1_xcd = value != 0;
             return WC_OK;
+        case WC_OPT_RIX_XCD:
+            c->opt_rix_xcd = value != 0;
+            return WC_OK;
         case WC_OPT_ORDERED:
             c->opt_ordered = value != 0;
             return WC_OK;
@@ -907,6 +910,7 @@ int wc_get_option(const wc_ctx* c, int option, int64_t* value) {
     switch (option) {
         case WC_OPT_SPARSE: *value = c->opt_sparse; return WC_OK;
         case WC_OPT_K1_XCD: *value = c->opt_k1_xcd; return WC_OK;
+        case WC_OPT_RIX_XCD: *value = c->opt_rix_xcd; return WC_OK;
         case WC_OPT_ORDERED: *value = use_ordered(c) ? 1 : 0; return WC_OK;  // the form the next launch takes
         case WC_OPT_INVERSE_ROWS: *value = c->opt_inv_rows; return WC_OK;
         case WC_OPT_RIX_LDS: *value = c->opt_rix_lds; return WC_OK;
