@@ -757,7 +757,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
     const uint2* pr = reinterpret_cast<const uint2*>(ph0 + 20);
     RixRange R = rix_load_range(T, rowinfo, w, l, ph0);
     RixPlan PL = rix_plan(T, R, l);
-    constexpr int NR = OT ? kRixRounds - 4 : kRixRounds;  // the RMSE pass needs registers
+    constexpr int NR = OT ? kRixRounds - 5 : kRixRounds;  // the RMSE pass needs registers
     uint2 q[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r)
