@@ -37,10 +37,10 @@ def pack(wc, boxes, dtype=np.float64, offsets=None):
 
 
 def set_path(ctx, path):
-    """Library options of a path ("staged" = the defaults: packed rows where
-    eligible, flagged segments elsewhere, XCD-grouped transform tiles)."""
-    ctx.set_option(WC_OPT_SPARSE, {"dense": 0, "flags": 1}.get(path, 2))
-    ctx.set_option(WC_OPT_K1_XCD, 0 if path == "dense" else 1)
+    """Library options of a path ("staged" = the defaults: flagged segments,
+    transform tiles in plain order)."""
+    ctx.set_option(WC_OPT_SPARSE, {"dense": 0, "packed": 2}.get(path, 1))
+    ctx.set_option(WC_OPT_K1_XCD, 1 if path == "packed" else 0)
     ctx.set_option(WC_OPT_ORDERED, 0 if path == "tickets" else 1)
     ctx.set_option(WC_OPT_INVERSE_ROWS, 0 if path == "dense_inverse" else 1)
 
@@ -60,13 +60,13 @@ def oracle_payload(O, b, keep):
     return O.compress_payload(b32, keep)[0]
 
 
-# Forward paths, all byte-identical: the library default (packed rows for D =
-# 64 / 128 units, flagged segments for the other sparse shapes, look-back
-# tile index from the launch order); "flags" (WC_OPT_SPARSE 1: flagged
-# segments everywhere); "dense" staging (WC_OPT_SPARSE 0, transform tiles in
-# plain order); "tickets": the look-back tile index from per-unit ticket
-# atomics (WC_OPT_ORDERED 0: no dispatch-order assumption).
-PATHS = ["staged", "flags", "dense", "tickets"]
+# Forward paths, all byte-identical: the library default (flagged segments,
+# look-back tile index from the launch order); "packed" (WC_OPT_SPARSE 2:
+# packed rows for D = 128 units, and transform tiles dealt to the XCDs in
+# contiguous runs); "dense" staging (WC_OPT_SPARSE 0); "tickets": the
+# look-back tile index from per-unit ticket atomics (WC_OPT_ORDERED 0: no
+# dispatch-order assumption).
+PATHS = ["staged", "packed", "dense", "tickets"]
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -545,7 +545,7 @@ def test_sparse_staging_sign_and_keep_edges(wc, ctx, oracle, keep):
     boxes[5] = boxes[5].copy()
     boxes[5][:, :, :] *= 1e-3
     boxes[5][3, 3, 3] = 2.0e4                  # one positive spike far above the rest
-    for path in ("staged", "flags", "dense"):
+    for path in ("staged", "packed", "dense"):
         got, _ = gpu_payloads(wc, ctx, boxes, keep, path=path)
         for i, b in enumerate(boxes):
             assert got[i] == oracle_payload(oracle, b, keep), f"{path} unit {i} dims {SPARSE_DIMS[i]} keep {keep}"
@@ -597,7 +597,7 @@ def test_sparse_staging_special_values(wc, ctx, oracle):
         box(s3, -7.0, [((20, 9, 33), 3.0e4)]),
     ]
     for keep in (KEEPS[1], 1.0):
-        for path in ("staged", "flags", "dense"):
+        for path in ("staged", "packed", "dense"):
             got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, path=path)
             for i, b in enumerate(boxes):
                 assert got[i] == oracle.compress_payload(b, keep)[0], (path, keep, i)
@@ -788,7 +788,7 @@ def test_packed_rows_bit_exact(wc, ctx, oracle, keep, dtype):
     boxes[5] = boxes[5].copy()
     boxes[5][100:102, 2:4, 40:42] = np.nan       # a NaN block in one tile (bound < 0 there)
     boxes[6] = -boxes[6]                         # all-negative field
-    for path in ("staged", "flags"):
+    for path in ("staged", "packed"):
         got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=dtype, path=path)
         for i, b in enumerate(boxes):
             assert got[i] == oracle_payload(oracle, b.astype(dtype), keep), (path, i, PACKED_DIMS[i])

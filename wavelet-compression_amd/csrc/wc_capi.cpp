@@ -14,6 +14,9 @@
 #include "wavelet_amd.h"
 #include "wc_internal.h"
 
+#ifndef WC_PACK64
+#define WC_PACK64 0  // D = 64 rows packed: measured no fewer staged lines than 32-coefficient segments
+#endif
 #ifndef WC_PACK128
 #define WC_PACK128 1  // D = 128 units: 16 x 1 x 64-block transform tiles and packed rows
 #endif
@@ -117,8 +120,8 @@ struct wc_ctx {
     uint32_t opt_spin_limit = 0; // WC_OPT_SPIN_LIMIT (0: kSpinLimit), mirrored in errflag[1]
     bool timed_out = false;      // the last error was a look-back wait that timed out
     bool registered = false;     // counted in g_dev_ctx
-    int opt_sparse = 2;       // WC_OPT_SPARSE: 0 dense, 1 flagged segments, 2 packed rows where eligible
-    bool opt_k1_xcd = true;   // WC_OPT_K1_XCD
+    int opt_sparse = 1;       // WC_OPT_SPARSE: 0 dense, 1 flagged segments, 2 packed rows where eligible
+    bool opt_k1_xcd = false;  // WC_OPT_K1_XCD
     bool opt_inv_rows = true; // WC_OPT_INVERSE_ROWS
     int opt_rix_lds = kRixLds; // WC_OPT_RIX_LDS
     int opt_rix_lx = 4;        // WC_OPT_RIX_TX
@@ -250,7 +253,7 @@ int upload(wc_ctx* c, DevBuf& d, const void* h, size_t bytes, const char* what) 
 // per tile (TZ == hz) and rows of D = 64 or 128 coefficients (2 or 4 lines:
 // shorter rows gain nothing from packing).
 bool packable(const UnitDev& d) {
-    return (d.nx % 2 == 0) && (d.ny % 2 == 0) && (d.nz == 64 || (d.nz == 128 && WC_PACK128));
+    return (d.nx % 2 == 0) && (d.ny % 2 == 0) && ((d.nz == 64 && WC_PACK64) || (d.nz == 128 && WC_PACK128));
 }
 
 void set_tiling(UnitDev& d) {
@@ -470,7 +473,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         P.lds_inverse = std::max(P.lds_inverse, transform_lds_bytes(d.lbx, d.lby, d.lbz));
         if (P.inv_rows && set_rix_tiling(d, P.rix_lds, P.rix_lx)) {
             d.row_off = P.rowinfo_entries;
-            P.rowinfo_entries += (uint64_t)d.nx * d.ny + 1;
+            P.rowinfo_entries += (uint64_t)d.nx * d.ny + 2;  // + sentinel + the call's pair count
             {  // floor(p / D) = (p * m) >> (31 + l), p < 2^31 (wc_inverse.hip div_rows)
                 const int lg = ceil_log2(d.nz);
                 const uint64_t m = (uint64_t(1) << (31 + lg)) / (uint64_t)d.nz + 1;

@@ -155,7 +155,10 @@ __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict
             v[r] = k < n ? runs[2 * k] : 0u;
         }
     }
-    if (!hok && t == 0 && tid == 0) atomicOr(err, kErrHeader);
+    if (t == 0 && tid == 0) {
+        if (!hok) atomicOr(err, kErrHeader);
+        rowinfo[U.row_off + (uint64_t)U.nx * U.ny + 1] = make_uint2(n, 0u);  // K6r's pair-count clamp
+    }
 
     // 1. v = run + 1 (k < n), 0 (k >= n) -> saturating in-wave inclusive sums
     const uint32_t kw = t * (uint32_t)kRixTile + (uint32_t)w * (kRixTile / 4);
@@ -612,17 +615,17 @@ struct RixRange {
     uint32_t ks, c0, e;  // rowinfo[r0] = (ks, c0), rowinfo[r0 + tyv].x = e
 };
 
-// ph: the unit's payload header.  The pair indices are clamped to its nrle,
-// so every pair load stays inside this payload even when the row entries are
-// not this call's (a row-index look-back that timed out leaves some unwritten:
-// they hold an earlier batch's entries; the call then reports WC_ERR_HIP).
-__device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* __restrict__ rowinfo, int w, int l,
-                                                   const uint8_t* __restrict__ ph) {
+// The pair indices are clamped to the unit's pair count, which k_rowindex's
+// tile 0 stores in this call's entry W*H + 1 (past the sentinel), so every
+// pair load stays inside this payload even when some row entries are not this
+// call's (a row-index look-back that timed out leaves them unwritten: they hold
+// an earlier batch's entries; the call then reports WC_ERR_HIP).  A load of
+// the row table, like the entries: no extra dependent round trip.
+__device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* __restrict__ rowinfo, int w, int l) {
     RixRange R{0u, 0u, 0u};
     const int TX = 1 << T.lbx;
     if (l < TX) {
-        const int32_t nh = reinterpret_cast<const int32_t*>(ph)[4];
-        const uint32_t nrle = nh > 0 ? (uint32_t)nh : 0u;
+        const uint32_t nrle = rowinfo[T.row_off + (uint64_t)T.W * T.H + 1].x;
         const int g = w + 4 * l, bxl = g & (TX - 1), ssy = (g >> T.lbx) & 1, ssx = g >> (T.lbx + 1);
         const int bx = T.bx0 + bxl, hx = T.W >> 1, hy = T.H >> 1;
         if (bx < hx) {
@@ -753,9 +756,8 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
 
     // prologue: tile t's ranges and pairs in flight, tile t + G's row entries
     RTile T = tiles[t];
-    const uint8_t* ph0 = payload + offsets[T.unit];
-    const uint2* pr = reinterpret_cast<const uint2*>(ph0 + 20);
-    RixRange R = rix_load_range(T, rowinfo, w, l, ph0);
+    const uint2* pr = reinterpret_cast<const uint2*>(payload + offsets[T.unit] + 20);
+    RixRange R = rix_load_range(T, rowinfo, w, l);
     RixPlan PL = rix_plan(T, R, l);
     constexpr int NR = OT ? kRixRounds - 5 : kRixRounds;  // the RMSE pass needs registers
     uint2 q[NR];
@@ -768,9 +770,8 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
     const uint2* pr1 = pr;
     if (t1 < tend) {
         T1 = tiles[t1];
-        const uint8_t* ph1 = payload + offsets[T1.unit];
-        pr1 = reinterpret_cast<const uint2*>(ph1 + 20);
-        R1 = rix_load_range(T1, rowinfo, w, l, ph1);
+        pr1 = reinterpret_cast<const uint2*>(payload + offsets[T1.unit] + 20);
+        R1 = rix_load_range(T1, rowinfo, w, l);
     }
 
     for (;;) {
@@ -818,9 +819,8 @@ __global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __res
                 if ((uint32_t)r < PL1.nrounds) q[r] = rix_load_round(pr1, R1, PL1, l, r);
             if (t2 < tend) {
                 T2 = tiles[t2];
-                const uint8_t* ph2 = payload + offsets[T2.unit];
-                pr2 = reinterpret_cast<const uint2*>(ph2 + 20);
-                R2 = rix_load_range(T2, rowinfo, w, l, ph2);
+                pr2 = reinterpret_cast<const uint2*>(payload + offsets[T2.unit] + 20);
+                R2 = rix_load_range(T2, rowinfo, w, l);
             }
         }
 
