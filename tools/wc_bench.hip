@@ -5,7 +5,7 @@
 // Box-Muller noise), then wc_forward runs `steps` times.  Prints one JSON line.
 //
 // usage: wc_bench [boxes=1024] [dim=64|c3] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1|2]
-//                 [check=0|1] [ordered=1] [sparse=2] [rows=1] [rix_lds=9216] [rix_tx=4] [rix_blocked=0]
+//                 [check=0|1] [ordered=1] [sparse=1] [rows=1] [rix_lds=9216] [rix_tx=4] [rix_blocked=0]
 //                 [k1_xcd=1] [rix_xcd=0]
 // check=1: also run the conservative configuration (ticket look-back, dense
 // staging, dense inverse decode) once and compare every unit's payload bytes and, with inverse=1,
@@ -104,7 +104,7 @@ int main(int argc, char** argv) {
     const bool inverse = inv_mode != 0;
     const bool check = argc > 8 ? std::atoi(argv[8]) != 0 : false;
     const int ordered = argc > 9 ? std::atoi(argv[9]) : 1;
-    const int sparse = argc > 10 ? std::atoi(argv[10]) : 2;
+    const int sparse = argc > 10 ? std::atoi(argv[10]) : 1;
     const int rows = argc > 11 ? std::atoi(argv[11]) : 1;
     const int rix_lds = argc > 12 ? std::atoi(argv[12]) : 9216;
     const int rix_tx = argc > 13 ? std::atoi(argv[13]) : 4;

@@ -183,16 +183,28 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
     if (!(tf >= 0.0f)) segf = 0xffu;
     float4 q[8];
     if (packed && tf >= 0.0f) {
-        const int lgD = U.lbz + 1;
-        const uint32_t dmask = ~((1u << lgD) - 1u);
-        const float* __restrict__ ub = coef + U.coef_off;  // uniform base, 32-bit element offsets
+        // The row's packed candidates sit at its first cnt slots: the dense
+        // path's 16-B loads, skipping every group at or past cnt; then each
+        // wave expands its 256-element block through its (yet unused) pair
+        // stage: lane l's float4 holds packed positions 4i..4i+3 of its row
+        // (i = l mod G), so packed position p of the row is at 4l - 4i + p.
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
+            const uint32_t gpos = (start + (uint32_t)(w * 2048 + it * 256 + 4 * l)) & ((2u << U.lbz) - 1u);  // 4i
+            q[it] = gpos < (pc[it] >> 11) ? p4[w * 512 + it * 64 + l] : make_float4(0, 0, 0, 0);
+        }
+        float* __restrict__ buf = reinterpret_cast<float*>(stage);
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const uint32_t gpos = (start + (uint32_t)(w * 2048 + it * 256 + 4 * l)) & ((2u << U.lbz) - 1u);
+            *reinterpret_cast<float4*>(buf + 4 * l) = q[it];
+            __builtin_amdgcn_wave_barrier();
             const uint32_t c = pc[it] & 15u;
-            const uint32_t o = ((start + (uint32_t)(w * 2048 + it * 256 + 4 * l)) & dmask) + (pc[it] >> 4);
+            const uint32_t o = 4u * (uint32_t)l - gpos + ((pc[it] >> 4) & 127u);
             const uint32_t n0 = c & 1u, n1 = n0 + ((c >> 1) & 1u), n2 = n1 + ((c >> 2) & 1u);
-            q[it] = make_float4((c & 1u) ? ub[o] : 0.f, (c & 2u) ? ub[o + n0] : 0.f, (c & 4u) ? ub[o + n1] : 0.f,
-                                (c & 8u) ? ub[o + n2] : 0.f);
+            q[it] = make_float4((c & 1u) ? buf[o] : 0.f, (c & 2u) ? buf[o + n0] : 0.f, (c & 4u) ? buf[o + n1] : 0.f,
+                                (c & 8u) ? buf[o + n2] : 0.f);
+            __builtin_amdgcn_wave_barrier();
         }
     } else {
 #pragma unroll

@@ -625,7 +625,10 @@ __device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* 
     RixRange R{0u, 0u, 0u};
     const int TX = 1 << T.lbx;
     if (l < TX) {
-        const uint32_t nrle = rowinfo[T.row_off + (uint64_t)T.W * T.H + 1].x;
+#ifndef WC_RIX_CLAMP
+#define WC_RIX_CLAMP 1
+#endif
+        const uint32_t nrle = WC_RIX_CLAMP ? rowinfo[T.row_off + (uint64_t)T.W * T.H + 1].x : 0xffffffffu;
         const int g = w + 4 * l, bxl = g & (TX - 1), ssy = (g >> T.lbx) & 1, ssx = g >> (T.lbx + 1);
         const int bx = T.bx0 + bxl, hx = T.W >> 1, hy = T.H >> 1;
         if (bx < hx) {

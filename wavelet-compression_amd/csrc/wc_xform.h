@@ -436,12 +436,14 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
 // row's candidates (|c| > bound, every coefficient when bound < 0) are stored
 // front-packed at the start of the row's dense slot (coef_off + (I*H+J)*D),
 // in K order, and the row's candidate mask at masks + (slot >> 3): D/8 bytes,
-// four words of G bits, word j bit i = coefficient K = 4i + j.  A row with c
-// candidates writes ceil(4c / 128) lines instead of 4D / 128; with every
-// coefficient a candidate the packed row IS the dense row.  Returns this
-// thread's max key over all its coefficients.
-__device__ __forceinline__ unsigned long long xform_fast_p2_packed(const UnitDev& U, const XTile& td,
-                                                                   const float* lds, int tid, double bound,
+// four words of G bits, word j bit i = coefficient K = 4i + j.  The row is
+// compacted in place in its LDS row (one wave owns a row), then stored with
+// the dense path's 16-B stores, ceil(c / 4) of them: a row with c candidates
+// writes ceil(4c / 128) lines instead of 4D / 128; with every coefficient a
+// candidate the packed row IS the dense row.  Returns this thread's max key
+// over all its coefficients.
+__device__ __forceinline__ unsigned long long xform_fast_p2_packed(const UnitDev& U, const XTile& td, float* lds,
+                                                                   int tid, double bound,
                                                                    uint8_t* __restrict__ masks,
                                                                    float* __restrict__ dst) {
     const int H = U.ny, D = U.nz;
@@ -455,6 +457,7 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_packed(const UnitDev
     const int l = tid & 63;
     const int gi = l & ((1 << q4) - 1), g0 = l - gi;
     const unsigned long long below = (1ull << l) - (1ull << g0);  // lanes of my row below me
+    const unsigned long long grp = ((q4 == 5 ? 0xffffffffull : 0xffffull) << g0);
     const bool all = !(bound >= 0.0);
     unsigned long long kmax = 0;
     for (int e = tid; e < total4; e += kThreads) {
@@ -465,17 +468,24 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_packed(const UnitDev
         if (bx >= hx || by >= hy) continue;  // uniform per row
         const int I = bx + ssx * hx, J = by + ssy * hy;
         const int64_t frow = ((int64_t)I * H + J) * D;
-        const float4 v = *reinterpret_cast<const float4*>(lds + row * rstride + 4 * gi);
+        float* lrow = lds + row * rstride;
+        const float4 v = *reinterpret_cast<const float4*>(lrow + 4 * gi);
         const bool c0 = all || (double)fabsf(v.x) > bound, c1 = all || (double)fabsf(v.y) > bound,
                    c2 = all || (double)fabsf(v.z) > bound, c3 = all || (double)fabsf(v.w) > bound;
         const unsigned long long b0 = __ballot(c0), b1 = __ballot(c1), b2 = __ballot(c2), b3 = __ballot(c3);
         uint32_t p = (uint32_t)(__popcll(b0 & below) + __popcll(b1 & below) + __popcll(b2 & below) +
                                 __popcll(b3 & below));
-        float* __restrict__ rp = dst + frow;
-        if (c0) rp[p++] = v.x;
-        if (c1) rp[p++] = v.y;
-        if (c2) rp[p++] = v.z;
-        if (c3) rp[p] = v.w;
+        const uint32_t cnt = (uint32_t)(__popcll(b0 & grp) + __popcll(b1 & grp) + __popcll(b2 & grp) +
+                                        __popcll(b3 & grp));
+        // in-place compaction: this wave read the whole row above (LDS operations
+        // of a wave complete in order), so the row's slots are free to rewrite
+        if (c0) lrow[p++] = v.x;
+        if (c1) lrow[p++] = v.y;
+        if (c2) lrow[p++] = v.z;
+        if (c3) lrow[p] = v.w;
+        __builtin_amdgcn_wave_barrier();
+        if (4u * (uint32_t)gi < cnt)
+            *reinterpret_cast<float4*>(dst + frow + 4 * gi) = *reinterpret_cast<const float4*>(lrow + 4 * gi);
         if (gi == 0) {
             uint8_t* mp = masks + ((U.coef_off + (uint64_t)frow) >> 3);
             if (q4 == 5)
@@ -504,8 +514,9 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_packed(const UnitDev
 // row: rows are 16- or 32-lane aligned) load the 4 mask words of their row,
 // word j = lane & 3; packed_rank then broadcasts them within the quad (DPP)
 // and returns, for this lane's 4 coefficients 4i..4i+3 (i = (f mod D) / 4),
-// their candidate bits (low 4 bits) and the number of candidates before them
-// in the row (<< 4).  f: unit-relative flat index; lgD = log2 D (6 or 7).
+// their candidate bits (low 4 bits), the number of candidates before them in
+// the row (<< 4, 7 bits) and the row's candidate count (<< 11).  f:
+// unit-relative flat index; lgD = log2 D (6 or 7).
 __device__ __forceinline__ uint32_t packed_mask_word(const uint8_t* __restrict__ masks, uint64_t coef_off, uint32_t f,
                                                      int lgD, int l) {
     const uint8_t* mp = masks + ((coef_off + ((uint64_t)(f >> lgD) << lgD)) >> 3);
@@ -522,7 +533,8 @@ __device__ __forceinline__ uint32_t packed_rank(uint32_t word, uint32_t f, int l
     const uint32_t lo = (1u << i) - 1u;
     const uint32_t pre = __popc(m0 & lo) + __popc(m1 & lo) + __popc(m2 & lo) + __popc(m3 & lo);
     const uint32_t c = ((m0 >> i) & 1u) | ((m1 >> i) & 1u) << 1 | ((m2 >> i) & 1u) << 2 | ((m3 >> i) & 1u) << 3;
-    return pre << 4 | c;
+    const uint32_t cnt = __popc(m0) + __popc(m1) + __popc(m2) + __popc(m3);
+    return cnt << 11 | pre << 4 | c;
 }
 
 }  // namespace wc
