@@ -82,17 +82,10 @@ int wc_set_stream(wc_ctx* ctx, void* hip_stream);
 int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side errors of earlier async calls */
 
 /* Tuning switches (wc_set_option).
- * WC_OPT_SPARSE (default 2): how the forward's transform stages coefficients
- *   for the emit.  A "candidate" is a coefficient with |c| > (tile max) *
- *   (1 - keep), a superset of the kept ones.  1: only the 16/32/64-coefficient
- *   flat segments holding a candidate are stored, and flagged; 2: as 1, but
- *   units with D = 64 or 128 (even W, H) store each flat row's candidates
- *   front-packed at the start of the row with a candidate bit mask (fewer
- *   staged lines when rows are partly kept); 0 = dense staging of every
- *   coefficient.  Same bytes out.
- * WC_OPT_K1_XCD (default 1): the transform's tile list is dealt to the XCDs in
- *   contiguous runs (neighbouring tiles share flag / mask lines in one L2).
- *   Same bytes out.
+ * WC_OPT_SPARSE (default 1): the forward's transform stores only the
+ *   16/32-coefficient flat segments that hold some |c| > (tile max) * (1 - keep)
+ *   and flags them; the emit loads only flagged segments.  Same bytes out;
+ *   0 = dense staging of every coefficient.
  * WC_OPT_RIX_XCD (default 0): the same for the row-indexed inverse's tiles
  *   (neighbouring tiles share payload lines at their range ends).  Same cells.
  * WC_OPT_ORDERED (default 1): the look-back kernels (forward emit, inverse
@@ -142,7 +135,6 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
 #define WC_OPT_HOST_CHUNK 18
 #define WC_OPT_SPIN_LIMIT 19
 #define WC_OPT_TICKETS 20
-#define WC_OPT_K1_XCD 21
 #define WC_OPT_RIX_XCD 22
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 int wc_get_option(const wc_ctx* ctx, int option, int64_t* value);

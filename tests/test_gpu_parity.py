@@ -8,7 +8,7 @@ in a fixed tree order).
 """
 import numpy as np
 import pytest
-from wavelet_compression_amd.capi import WC_OPT_INVERSE_ROWS, WC_OPT_K1_XCD, WC_OPT_ORDERED, WC_OPT_SPARSE
+from wavelet_compression_amd.capi import WC_OPT_INVERSE_ROWS, WC_OPT_ORDERED, WC_OPT_SPARSE
 
 pytestmark = pytest.mark.gpu
 
@@ -37,10 +37,8 @@ def pack(wc, boxes, dtype=np.float64, offsets=None):
 
 
 def set_path(ctx, path):
-    """Library options of a path ("staged" = the defaults: flagged segments,
-    transform tiles in plain order)."""
-    ctx.set_option(WC_OPT_SPARSE, {"dense": 0, "packed": 2}.get(path, 1))
-    ctx.set_option(WC_OPT_K1_XCD, 1 if path == "packed" else 0)
+    """Library options of a path ("staged" = the defaults)."""
+    ctx.set_option(WC_OPT_SPARSE, 0 if path == "dense" else 1)
     ctx.set_option(WC_OPT_ORDERED, 0 if path == "tickets" else 1)
     ctx.set_option(WC_OPT_INVERSE_ROWS, 0 if path == "dense_inverse" else 1)
 
@@ -60,13 +58,11 @@ def oracle_payload(O, b, keep):
     return O.compress_payload(b32, keep)[0]
 
 
-# Forward paths, all byte-identical: the library default (flagged segments,
-# look-back tile index from the launch order); "packed" (WC_OPT_SPARSE 2:
-# packed rows for D = 128 units, and transform tiles dealt to the XCDs in
-# contiguous runs); "dense" staging (WC_OPT_SPARSE 0); "tickets": the
-# look-back tile index from per-unit ticket atomics (WC_OPT_ORDERED 0: no
-# dispatch-order assumption).
-PATHS = ["staged", "packed", "dense", "tickets"]
+# Forward paths, all byte-identical: the library default (sparse staging of
+# 32-coefficient segments, look-back tile index from the launch order);
+# "dense" staging (WC_OPT_SPARSE 0); "tickets": the look-back tile index from
+# per-unit ticket atomics (WC_OPT_ORDERED 0: no dispatch-order assumption).
+PATHS = ["staged", "dense", "tickets"]
 
 
 @pytest.mark.parametrize("path", PATHS)
@@ -545,7 +541,7 @@ def test_sparse_staging_sign_and_keep_edges(wc, ctx, oracle, keep):
     boxes[5] = boxes[5].copy()
     boxes[5][:, :, :] *= 1e-3
     boxes[5][3, 3, 3] = 2.0e4                  # one positive spike far above the rest
-    for path in ("staged", "packed", "dense"):
+    for path in ("staged", "dense"):
         got, _ = gpu_payloads(wc, ctx, boxes, keep, path=path)
         for i, b in enumerate(boxes):
             assert got[i] == oracle_payload(oracle, b, keep), f"{path} unit {i} dims {SPARSE_DIMS[i]} keep {keep}"
@@ -597,7 +593,7 @@ def test_sparse_staging_special_values(wc, ctx, oracle):
         box(s3, -7.0, [((20, 9, 33), 3.0e4)]),
     ]
     for keep in (KEEPS[1], 1.0):
-        for path in ("staged", "packed", "dense"):
+        for path in ("staged", "dense"):
             got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=np.float32, path=path)
             for i, b in enumerate(boxes):
                 assert got[i] == oracle.compress_payload(b, keep)[0], (path, keep, i)
@@ -768,27 +764,3 @@ def test_forward_host_runs_with_empty_units(wc, ctx, oracle):
             assert got == np.array([W, H, D, 0, 0], "<i4").tobytes(), i
         else:
             assert got == oracle_payload(oracle, b, keep), i
-
-
-PACKED_DIMS = [(64, 64, 64), (128, 128, 128), (48, 32, 64), (2, 2, 64), (2, 4, 128), (96, 6, 128), (16, 200, 64),
-               (34, 18, 128), (64, 64, 32), (8, 8, 256)]
-
-
-@pytest.mark.parametrize("keep", [float(np.float32(k)) for k in (0.5, 0.99, 0.9999, 1.0, 1.5)])
-@pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_packed_rows_bit_exact(wc, ctx, oracle, keep, dtype):
-    """Packed-row staging (D = 64 / 128 units: each flat row's candidates
-    front-packed with a candidate mask): partial x tiles (W = 48, 34, 96),
-    tiny W/H, many rows per tile, a D = 128 unit of 16 x 1 x 64-block tiles,
-    neighbours on the other staging forms (D = 32, 256); a negative spike
-    (thresh < 0: dense re-stage), a NaN-tile, and dense-ish / sparse keeps."""
-    boxes = synth(oracle, PACKED_DIMS, seed0=51)
-    boxes[2] = boxes[2].copy()
-    boxes[2][10, 5, 7] = -1.0e6                  # signed max < 0: every coefficient kept
-    boxes[5] = boxes[5].copy()
-    boxes[5][100:102, 2:4, 40:42] = np.nan       # a NaN block in one tile (bound < 0 there)
-    boxes[6] = -boxes[6]                         # all-negative field
-    for path in ("staged", "packed"):
-        got, _ = gpu_payloads(wc, ctx, boxes, keep, dtype=dtype, path=path)
-        for i, b in enumerate(boxes):
-            assert got[i] == oracle_payload(oracle, b.astype(dtype), keep), (path, i, PACKED_DIMS[i])

@@ -7,8 +7,8 @@ progress; VERDICT r2 "next" 6).
   its own stream at the same time — give the oracle's payloads without another
   ~2 s wait.
 * The row-indexed inverse never reads past a payload when a timed-out row
-  index left row entries of an earlier, larger batch behind (K6r clamps its
-  pair ranges to the header's nrle).
+  index would leave row entries of an earlier, denser batch behind (the
+  timed-out row-index tile empties every row entry of its unit).
 * WCAMD_SHARED_DEVICE=1 puts every context of a process on the tickets.
 """
 import os

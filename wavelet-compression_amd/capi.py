@@ -30,7 +30,7 @@ EXPORTED = (
     "wc_decompose_host", "wc_device_count", "wc_forward_stage", "wc_hist_threshold",
     "wc_forward_emit", "wc_inverse_rmse", "wc_get_option",
 )
-WC_OPT_SPARSE = 12   # forward staging: 0 dense, 1 flagged segments, 2 packed rows where eligible (default)
+WC_OPT_SPARSE = 12   # sparse coefficient staging in the forward (default 1)
 WC_OPT_ORDERED = 13  # look-back tile index from the launch order (1, default) or per-unit tickets (0)
 WC_OPT_INVERSE_ROWS = 14  # row-indexed inverse of even-dims units (1, default) or dense decode (0)
 WC_OPT_RIX_LDS = 15  # row-indexed inverse: LDS floats per workgroup (default 9216)
@@ -39,7 +39,6 @@ WC_OPT_RIX_BLOCKED = 17  # row-indexed inverse: contiguous tile runs per workgro
 WC_OPT_HOST_CHUNK = 18  # wc_forward_host: cells per pipelined unit run (default 2^25, 0 = one run)
 WC_OPT_SPIN_LIMIT = 19  # polls before a look-back wait is declared timed out (0: default, ~2 s)
 WC_OPT_TICKETS = 20  # 1: ticket form whatever WC_OPT_ORDERED says (set by a look-back timeout: sticky)
-WC_OPT_K1_XCD = 21  # transform tiles dealt to XCDs in contiguous runs (default 1)
 WC_OPT_RIX_XCD = 22  # row-indexed inverse tiles dealt to XCDs in contiguous runs (default 0)
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*).

@@ -14,13 +14,6 @@
 #include "wavelet_amd.h"
 #include "wc_internal.h"
 
-#ifndef WC_PACK64
-#define WC_PACK64 0  // D = 64 rows packed: measured no fewer staged lines than 32-coefficient segments
-#endif
-#ifndef WC_PACK128
-#define WC_PACK128 1  // D = 128 units: 16 x 1 x 64-block transform tiles and packed rows
-#endif
-
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -37,8 +30,7 @@ size_t transform_fast_lds_bytes(int lbx, int lby, int lbz);
 hipError_t launch_transform(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
                             float*, int, unsigned long long*);
 hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
-                                 float*, int, unsigned long long*, uint8_t*, uint32_t*, double, uint32_t, uint8_t*,
-                                 int);
+                                 float*, int, unsigned long long*, uint8_t*, uint32_t*, double, uint32_t);
 uint32_t transform_pf_grid(size_t lds);
 uint32_t inverse_rows_grid(size_t lds);
 hipError_t launch_transform_fallback(hipStream_t, const void*, int, const UnitDev*, int, const XTile*, size_t, float*,
@@ -54,7 +46,7 @@ hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const 
                           size_t, float*);
 hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDev*, int, const FTile*,
                        uint32_t, double*, double*);
-hipError_t launch_emit(hipStream_t, const EmitParams&, const float*, const uint32_t*);
+hipError_t launch_emit(hipStream_t, const EmitParams&, const float*, uint32_t, uint32_t);
 hipError_t launch_hist(hipStream_t, const UnitDev*, const FTile*, uint32_t, const float*, uint32_t,
                        unsigned long long*);
 }  // namespace wc
@@ -84,10 +76,8 @@ struct Plan {
     int rix_lds = kRixLds;              // WC_OPT_RIX_LDS the plan was built with
     int rix_lx = 4;                     // WC_OPT_RIX_TX the plan was built with
     bool rix_xcd = false;               // WC_OPT_RIX_XCD the plan was built with
-    // emit blocks in 4 launch segments: (kEmitTile, kEmitTileBig) tiles x (other
-    // units, packed-row units), each segment's units in the interleaved order
-    std::vector<EmitDesc> edesc;
-    uint32_t nedesc[4] = {0, 0, 0, 0};
+    std::vector<EmitDesc> edesc;  // [units of kEmitTile tiles | units of kEmitTileBig tiles]
+    uint32_t nedesc_small = 0;
     uint32_t ngen = 0, nfast = 0, netiles = 0;
     uint32_t ign = 0, ifast = 0;  // ixtiles split
     bool inv_rows = true;         // WC_OPT_INVERSE_ROWS the plan was built with
@@ -120,8 +110,7 @@ struct wc_ctx {
     uint32_t opt_spin_limit = 0; // WC_OPT_SPIN_LIMIT (0: kSpinLimit), mirrored in errflag[1]
     bool timed_out = false;      // the last error was a look-back wait that timed out
     bool registered = false;     // counted in g_dev_ctx
-    int opt_sparse = 1;       // WC_OPT_SPARSE: 0 dense, 1 flagged segments, 2 packed rows where eligible
-    bool opt_k1_xcd = false;  // WC_OPT_K1_XCD
+    bool opt_sparse = true;   // WC_OPT_SPARSE
     bool opt_inv_rows = true; // WC_OPT_INVERSE_ROWS
     int opt_rix_lds = kRixLds; // WC_OPT_RIX_LDS
     int opt_rix_lx = 4;        // WC_OPT_RIX_TX
@@ -136,10 +125,9 @@ struct wc_ctx {
     // (cleared by set_device, i.e. by every other compute entry point)
     bool staged = false;
     bool sparse_staged = false;  // the last stage_transform used sparse staging
-    bool packed_staged = false;  // ... and packed rows (masks) for the units with sparse == 2
     uint64_t plan_gen = 0;  // bumped whenever get_plan rebuilds the plan
     // scratch (grow-only)
-    DevBuf coef, part, errflag, state, flags, masks, rowinfo;
+    DevBuf coef, part, errflag, state, flags, rowinfo;
     // row index (wc_inverse): epoch-tagged look-back granules, zeroed when
     // allocated and never again (a granule of an earlier call reads as
     // unpublished); epoch: the call counter they are tagged with
@@ -249,20 +237,11 @@ int upload(wc_ctx* c, DevBuf& d, const void* h, size_t bytes, const char* what) 
     return e == hipSuccess ? WC_OK : hip_fail(c, e, what);
 }
 
-// Packed-row staging (wc_xform.h xform_fast_p2_packed) needs whole flat rows
-// per tile (TZ == hz) and rows of D = 64 or 128 coefficients (2 or 4 lines:
-// shorter rows gain nothing from packing).
-bool packable(const UnitDev& d) {
-    return (d.nx % 2 == 0) && (d.ny % 2 == 0) && ((d.nz == 64 && WC_PACK64) || (d.nz == 128 && WC_PACK128));
-}
-
 void set_tiling(UnitDev& d) {
     // Up to 32 blocks along x (coalesced input rows) and z (contiguous flat
-    // rows), the rest along y, at most kMaxTileBlocks blocks per tile.  D = 128
-    // units (packable): all 64 z-blocks, 16 along x (128-B fp32 input rows).
-    const int zmax = packable(d) ? 6 : 5;
-    d.lbz = std::min(zmax, ceil_log2(std::max(1, d.nbz)));
-    d.lbx = std::min(std::min(5, 10 - d.lbz), ceil_log2(std::max(1, d.nbx)));
+    // rows), the rest along y, at most kMaxTileBlocks blocks per tile.
+    d.lbx = std::min(5, ceil_log2(std::max(1, d.nbx)));
+    d.lbz = std::min(5, ceil_log2(std::max(1, d.nbz)));
     d.lby = std::min(ceil_log2(std::max(1, d.nby)), 10 - d.lbx - d.lbz);
 }
 
@@ -302,13 +281,11 @@ void build_etiles(Plan& P, int n) {
     // status[tiles] (u64)
     P.state_bytes = round_up(16 + 20ull * n, 8) + 8ull * total;
     P.edesc.clear();
-    for (int seg = 0; seg < 4; ++seg) {  // one launch per tile size and staging form
-        const int cls = seg >> 1;
-        const bool pk = (seg & 1) != 0;
-        const size_t before = P.edesc.size();
+    P.nedesc_small = 0;
+    for (int cls = 0; cls < 2; ++cls) {  // one launch per tile size: small units, then big ones
         std::vector<int> us;
         for (int i = 0; i < n; ++i)
-            if (big(P.units[i]) == (cls == 1) && (P.units[i].sparse == 2) == pk) us.push_back(i);
+            if (big(P.units[i]) == (cls == 1)) us.push_back(i);
         uint32_t maxt = 0;
         for (int i : us) maxt = std::max(maxt, P.units[i].net);
         const uint64_t group_tiles = std::max<uint64_t>(cls ? 4096 : 8192, 128ull * maxt);
@@ -344,7 +321,7 @@ void build_etiles(Plan& P, int n) {
                     P.edesc.push_back(e);
                 }
         }
-        P.nedesc[seg] = (uint32_t)(P.edesc.size() - before);
+        if (cls == 0) P.nedesc_small = (uint32_t)P.edesc.size();
     }
 }
 
@@ -452,7 +429,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         d.ntz = (d.nbz + (1 << d.lbz) - 1) >> d.lbz;
         d.pay_off = pay_cursor;  // slot of 20 + 8*ncells bytes + 4 pad: next slot stays == 4 (mod 8)
         pay_cursor += 24 + 8 * d.ncells;
-        d.coef_off = (coef_cursor + 127) & ~uint64_t(127);  // 512 B: segments and 16-B row masks align
+        d.coef_off = (coef_cursor + 31) & ~uint64_t(31);  // 128 B: sparse-staging segments align
         coef_cursor = d.coef_off + d.ncells;
         if (d.ncells == 0) continue;
         d.fast = (u.nx % 2 == 0) && (u.ny % 2 == 0) && (u.nz % 8 == 0);
@@ -463,7 +440,6 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         // Sparse staging (wc_xform.h xform_fast_p2_sparse): z tiles of >= 16
         // blocks whose flat segments of TZ coefficients each belong to one tile.
         d.sparse = (d.fast && d.lbz >= kSegShift && d.hz % (1 << d.lbz) == 0) ? 1u : 0u;
-        if (d.sparse && packable(d) && (1 << d.lbz) == d.hz) d.sparse = 2u;
         P.any_sparse |= d.sparse != 0;
         d.xt_begin = (uint32_t)before;  // rebased below for fast units
         if (d.fast)
@@ -473,7 +449,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         P.lds_inverse = std::max(P.lds_inverse, transform_lds_bytes(d.lbx, d.lby, d.lbz));
         if (P.inv_rows && set_rix_tiling(d, P.rix_lds, P.rix_lx)) {
             d.row_off = P.rowinfo_entries;
-            P.rowinfo_entries += (uint64_t)d.nx * d.ny + 2;  // + sentinel + the call's pair count
+            P.rowinfo_entries += (uint64_t)d.nx * d.ny + 1;
             {  // floor(p / D) = (p * m) >> (31 + l), p < 2^31 (wc_inverse.hip div_rows)
                 const int lg = ceil_log2(d.nz);
                 const uint64_t m = (uint64_t(1) << (31 + lg)) / (uint64_t)d.nz + 1;
@@ -608,7 +584,6 @@ int ensure_scratch(wc_ctx* c) {
     int rc;
     if ((rc = ensure(c, c->coef, sizeof(float) * std::max<uint64_t>(P.coef_extent, 1))) ||
         (rc = ensure(c, c->flags, (P.coef_extent >> kSegShift) + kEmitTileBig)) ||
-        (rc = ensure(c, c->masks, (P.coef_extent >> 3) + kEmitTileBig)) ||
         (rc = ensure(c, c->part, sizeof(double) * std::max<size_t>(nft, 4 * P.rtiles.size()))) ||
         (rc = ensure(c, c->rowinfo, sizeof(uint32_t) * 2 * std::max<uint64_t>(P.rowinfo_entries, 1))) ||
         (rc = ensure_zeroed(c, c->istate, istate_bytes(P))) ||
@@ -703,21 +678,18 @@ int stage_transform(wc_ctx* c, const void* d_cells, int dtype, double keep, bool
     uint32_t* spos = (uint32_t*)((uint8_t*)c->state.p + 16 + 12 * n);
     float* coef = (float*)c->coef.p;
     uint8_t* flags = sparse && P.any_sparse ? (uint8_t*)c->flags.p : nullptr;
-    uint8_t* masks = flags && c->opt_sparse == 2 ? (uint8_t*)c->masks.p : nullptr;
     {
         StageTimer t(c, WC_STAGE_TRANSFORM);
         e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, coef, 0, key);
         if (e == hipSuccess)
             e = launch_transform_fast(c->stream, d_cells, dtype, du, dxt + P.ngen, P.nfast, P.lds_fast, coef, 0,
-                                      key, flags, spos, keep, persistent_grid(c, 0, P.lds_fast), masks,
-                                      c->opt_k1_xcd ? 1 : 0);
+                                      key, flags, spos, keep, persistent_grid(c, 0, P.lds_fast));
         // units whose thresh came out < 0 need every coefficient (rare: negative signed max)
         if (e == hipSuccess && flags)
             e = launch_transform_fallback(c->stream, d_cells, dtype, du, (int)P.units.size(), dxt, P.lds_fast, coef,
                                           key, spos, keep);
     }
     c->sparse_staged = flags != nullptr;
-    c->packed_staged = masks != nullptr;
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "transform launch");
 }
 
@@ -746,9 +718,9 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
         p.gthresh = *gthresh;
     }
     p.flags = (c->sparse_staged && !gthresh) ? (const uint8_t*)c->flags.p : nullptr;
-    p.masks = (c->packed_staged && !gthresh) ? (const uint8_t*)c->masks.p : nullptr;
     StageTimer t(c, WC_STAGE_EMIT);
-    hipError_t e = launch_emit(c->stream, p, (const float*)c->coef.p, P.nedesc);
+    hipError_t e = launch_emit(c->stream, p, (const float*)c->coef.p, P.nedesc_small,
+                               (uint32_t)P.edesc.size() - P.nedesc_small);
     if (e != hipSuccess) return hip_fail(c, e, "emit launch");
     c->err_check_pending = true;  // a look-back wait that timed out surfaces at wc_synchronize
     return WC_OK;
@@ -756,7 +728,7 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
 
 int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
                    uint64_t* d_offsets, uint32_t* d_kept) {
-    int rc = stage_transform(c, d_cells, dtype, keep, c->opt_sparse != 0);
+    int rc = stage_transform(c, d_cells, dtype, keep, c->opt_sparse);
     return rc ? rc : stage_emit(c, n, keep, nullptr, d_payload, d_offsets, d_kept);
 }
 
@@ -819,7 +791,7 @@ void wc_ctx_destroy(wc_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->coef,          &c->part,           &c->errflag,        &c->state,
-                      &c->flags,         &c->masks,          &c->h_cells,        &c->h_payload,      &c->h_packed,
+                      &c->flags,         &c->h_cells,        &c->h_payload,      &c->h_packed,
                       &c->h_offsets,     &c->h_poff,         &c->h_kept,         &c->h_out,
                       &c->plan.d_units,  &c->plan.d_xtiles,  &c->plan.d_ftiles,  &c->plan.d_dtiles,
                       &c->plan.d_edesc, &c->plan.d_ixtiles, &c->plan.d_rtiles,
@@ -860,11 +832,7 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
     if (!c) return WC_ERR_INVALID;
     switch (option) {
         case WC_OPT_SPARSE:
-            if (value < 0 || value > 2) return fail(c, WC_ERR_INVALID, "WC_OPT_SPARSE: 0, 1 or 2");
-            c->opt_sparse = (int)value;
-            return WC_OK;
-        case WC_OPT_K1_XCD:
-            c->opt_k1_xcd = value != 0;
+            c->opt_sparse = value != 0;
             return WC_OK;
         case WC_OPT_RIX_XCD:
             c->opt_rix_xcd = value != 0;
@@ -912,7 +880,6 @@ int wc_get_option(const wc_ctx* c, int option, int64_t* value) {
     if (!c || !value) return WC_ERR_INVALID;
     switch (option) {
         case WC_OPT_SPARSE: *value = c->opt_sparse; return WC_OK;
-        case WC_OPT_K1_XCD: *value = c->opt_k1_xcd; return WC_OK;
         case WC_OPT_RIX_XCD: *value = c->opt_rix_xcd; return WC_OK;
         case WC_OPT_ORDERED: *value = use_ordered(c) ? 1 : 0; return WC_OK;  // the form the next launch takes
         case WC_OPT_INVERSE_ROWS: *value = c->opt_inv_rows; return WC_OK;
@@ -1053,8 +1020,7 @@ int wc_decompose(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units
     hipError_t e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, d_flat, 1, nullptr);
     if (e == hipSuccess)
         e = launch_transform_fast(c->stream, d_cells, dtype, du, dxt + P.ngen, P.nfast, P.lds_fast, d_flat, 1,
-                                  nullptr, nullptr, nullptr, 0.0, persistent_grid(c, 0, P.lds_fast), nullptr,
-                                  c->opt_k1_xcd ? 1 : 0);
+                                  nullptr, nullptr, nullptr, 0.0, persistent_grid(c, 0, P.lds_fast));
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "transform launch");
 }
 

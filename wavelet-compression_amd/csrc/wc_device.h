@@ -213,8 +213,9 @@ __device__ __forceinline__ unsigned long long granule_e(unsigned long long flag,
 }
 
 // lookback_sum62 over epoch-tagged granules; the result saturates at 2^32 - 1.
+// timed_out: the wait hit its bound (the sum is then partial).
 __device__ __forceinline__ uint32_t lookback_sum32e(const unsigned long long* st, int64_t t, int l, uint32_t* err,
-                                                    uint32_t epoch) {
+                                                    uint32_t epoch, bool& timed_out) {
     unsigned long long excl = 0;
     int64_t pos = t - 1;
     const uint32_t ep = epoch & kEpochMask;
@@ -230,7 +231,10 @@ __device__ __forceinline__ uint32_t lookback_sum32e(const unsigned long long* st
         if (take > 0) excl += wave_sum(l < take ? (v & 0xffffffffull) : 0ull);
         if (kI < kZ) break;
         pos -= take;
-        if (take == 0 && spin_fail(spins, err)) break;
+        if (take == 0 && spin_fail(spins, err)) {
+            timed_out = true;
+            break;
+        }
     }
     return excl > 0xffffffffull ? 0xffffffffu : (uint32_t)excl;
 }

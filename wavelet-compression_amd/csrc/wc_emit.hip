@@ -135,31 +135,15 @@ constexpr unsigned long long kMask31 = 0x7fffffffull;
 
 // Threshold + ordered pack of tile `index` of unit `u`.  Thread t = (wave w,
 // lane l) owns elements w*2048 + it*256 + 4l + j, it 0..7.  sm: 16 LDS words.
-template <int EW, bool PK>
+template <int EW>
 __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __restrict__ coef, const EmitDesc& U,
                                           uint32_t index, uint32_t* sm, uint2* stage, int tid) {
     constexpr uint32_t kTile = EW * 2048;
     const uint32_t u = U.unit;
     const uint32_t et = U.et_begin + index;
     const int w = tid >> 6, l = tid & 63;
-    const uint32_t start = index * kTile;
-    const uint32_t len = (uint32_t)min((uint64_t)kTile, U.ncells - start);
-    // Packed rows (wc_xform.h xform_fast_p2_packed): each element group's
-    // candidate bits and packed rank, from its row's mask, before the key.
-    const bool packed = PK && P.masks && U.sparse == 2;
-    uint32_t pc[8];
-    if (packed) {
-        const int lgD = U.lbz + 1;
-#pragma unroll
-        for (int it = 0; it < 8; ++it) {
-            const uint32_t e = (uint32_t)(w * 2048 + it * 256 + 4 * l);  // len: a multiple of 64 here
-            pc[it] = e < len ? packed_mask_word(P.masks, U.coef_off, start + e, lgD, l) : 0u;
-        }
-#pragma unroll
-        for (int it = 0; it < 8; ++it) pc[it] = packed_rank(pc[it], start + (uint32_t)(w * 2048 + it * 256 + 4 * l), lgD);
-    }
     // Sparse staging: this thread's 8 segment flags, loaded before the key.
-    const bool sparse = P.flags && U.sparse && !packed;
+    const bool sparse = P.flags && U.sparse;
     uint32_t segf = 0xffu;  // bit it: group it may hold kept coefficients
     if (sparse) {
         // one flag byte per segment of TZ = 2^lbz coefficients (16 or 32)
@@ -171,47 +155,20 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
     }
     // the unit key: a finished earlier launch wrote it, one uniform load
     const float tf = unit_thresh(P, P.key[u]);
+    const uint32_t start = index * kTile;
+    const uint32_t len = (uint32_t)min((uint64_t)kTile, U.ncells - start);
 
     // 1. coefficients -> keep bits (bit it*4 + j).  The flat scratch is 16-B
     // aligned per unit with kFlatTile slack past the last unit.  Sparse units
     // with thresh >= 0 skip unflagged segments (never stored); thresh < 0
     // units were re-staged densely (k_transform_fallback).
-    // Packed units with thresh >= 0 read each group's candidates from the
-    // front of its row (a candidate-free group loads nothing); thresh < 0
-    // units were re-staged densely (k_transform_fallback) and read densely.
     const float4* __restrict__ p4 = reinterpret_cast<const float4*>(coef + U.coef_off + start);
     if (!(tf >= 0.0f)) segf = 0xffu;
     float4 q[8];
-    if (packed && tf >= 0.0f) {
-        // The row's packed candidates sit at its first cnt slots: the dense
-        // path's 16-B loads, skipping every group at or past cnt; then each
-        // wave expands its 256-element block through its (yet unused) pair
-        // stage: lane l's float4 holds packed positions 4i..4i+3 of its row
-        // (i = l mod G), so packed position p of the row is at 4l - 4i + p.
 #pragma unroll
-        for (int it = 0; it < 8; ++it) {
-            const uint32_t gpos = (start + (uint32_t)(w * 2048 + it * 256 + 4 * l)) & ((2u << U.lbz) - 1u);  // 4i
-            q[it] = gpos < (pc[it] >> 11) ? p4[w * 512 + it * 64 + l] : make_float4(0, 0, 0, 0);
-        }
-        float* __restrict__ buf = reinterpret_cast<float*>(stage);
-#pragma unroll
-        for (int it = 0; it < 8; ++it) {
-            const uint32_t gpos = (start + (uint32_t)(w * 2048 + it * 256 + 4 * l)) & ((2u << U.lbz) - 1u);
-            *reinterpret_cast<float4*>(buf + 4 * l) = q[it];
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t c = pc[it] & 15u;
-            const uint32_t o = 4u * (uint32_t)l - gpos + ((pc[it] >> 4) & 127u);
-            const uint32_t n0 = c & 1u, n1 = n0 + ((c >> 1) & 1u), n2 = n1 + ((c >> 2) & 1u);
-            q[it] = make_float4((c & 1u) ? buf[o] : 0.f, (c & 2u) ? buf[o + n0] : 0.f, (c & 4u) ? buf[o + n1] : 0.f,
-                                (c & 8u) ? buf[o + n2] : 0.f);
-            __builtin_amdgcn_wave_barrier();
-        }
-    } else {
-#pragma unroll
-        for (int it = 0; it < 8; ++it)
-            q[it] = ((segf >> it) & 1u) && (uint32_t)(w * 2048 + it * 256 + 4 * l) < len ? p4[w * 512 + it * 64 + l]
-                                                                                          : make_float4(0, 0, 0, 0);
-    }
+    for (int it = 0; it < 8; ++it)
+        q[it] = ((segf >> it) & 1u) && (uint32_t)(w * 2048 + it * 256 + 4 * l) < len ? p4[w * 512 + it * 64 + l]
+                                                                                      : make_float4(0, 0, 0, 0);
     const uint32_t kb = keep_bits(q, tf, len, w, l);
     uint32_t wcnt, wlast;
     wave_totals(kb, w, l, wcnt, wlast);
@@ -293,48 +250,36 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
 #ifndef WC_EMIT_MINB
 #define WC_EMIT_MINB 8  // 4-wave launch: workgroups per CU the register budget is sized for (64 VGPRs)
 #endif
-#ifndef WC_EMIT_MINB_PK
-#define WC_EMIT_MINB_PK 7  // 4-wave packed-row launch: 72 VGPRs (the mask ranks need 8 more)
-#endif
 // One block per emit tile (EW waves: EW * 2048 coefficients).  Block b packs
 // the tile edesc[b] in the ordered form, or the next ticket of edesc[b]'s unit
 // in the ticket form.  The plan lists blocks interleaved by tile index across
 // the units of a group, groups in reverse transform order (wc_capi.cpp
 // build_etiles); units of kEmitBigCells or more cells form the 8-wave launch.
-// PK: the launch of the packed-row units (U.sparse == 2; read through their
-// masks when P.masks is set, else as flagged segments).
-template <int EW, bool PK>
-__global__ __launch_bounds__(EW * kWave, EW == 4 ? (PK ? WC_EMIT_MINB_PK : WC_EMIT_MINB) : 2) void k_emit(
-    EmitParams P, const float* __restrict__ coef) {
+template <int EW>
+__global__ __launch_bounds__(EW * kWave, EW == 4 ? WC_EMIT_MINB : 2) void k_emit(EmitParams P,
+                                                                           const float* __restrict__ coef) {
     __shared__ __attribute__((aligned(16))) uint32_t sm[32];
     __shared__ uint2 stage_all[EW][256];  // per-wave pair stage (emit_pairs)
     const int tid = threadIdx.x;
     uint2* stage = stage_all[tid >> 6];
     const EmitDesc E = P.edesc[blockIdx.x];
     if (P.ordered) {
-        emit_tile<EW, PK>(P, coef, E, E.index, sm, stage, tid);
+        emit_tile<EW>(P, coef, E, E.index, sm, stage, tid);
         return;
     }
     if (tid == 0) sm[31] = atomicAdd(P.tickets + E.unit, 1u);
     __syncthreads();
     const uint32_t index = __builtin_amdgcn_readfirstlane(sm[31]);
-    emit_tile<EW, PK>(P, coef, E, index, sm, stage, tid);
+    emit_tile<EW>(P, coef, E, index, sm, stage, tid);
 }
 
-// nseg[4]: emit blocks of the plan's launch segments (wc_capi.cpp build_etiles):
-// 4-wave other units, 4-wave packed-row units, 8-wave other, 8-wave packed.
-hipError_t launch_emit(hipStream_t st, const EmitParams& p, const float* coef, const uint32_t* nseg) {
+hipError_t launch_emit(hipStream_t st, const EmitParams& p, const float* coef, uint32_t nsmall, uint32_t nbig) {
     static_assert(kEmitTile == 4 * 2048 && kEmitTileBig == 8 * 2048, "emit tile sizes");
-    EmitParams q = p;
-    for (int seg = 0; seg < 4; ++seg) {
-        const uint32_t nb = nseg[seg];
-        if (nb) {
-            if (seg == 0) k_emit<4, false><<<nb, 4 * kWave, 0, st>>>(q, coef);
-            if (seg == 1) k_emit<4, true><<<nb, 4 * kWave, 0, st>>>(q, coef);
-            if (seg == 2) k_emit<8, false><<<nb, 8 * kWave, 0, st>>>(q, coef);
-            if (seg == 3) k_emit<8, true><<<nb, 8 * kWave, 0, st>>>(q, coef);
-        }
-        q.edesc += nb;
+    if (nsmall) k_emit<4><<<nsmall, 4 * kWave, 0, st>>>(p, coef);
+    if (nbig) {
+        EmitParams q = p;
+        q.edesc = p.edesc + nsmall;
+        k_emit<8><<<nbig, 8 * kWave, 0, st>>>(q, coef);
     }
     return hipGetLastError();
 }

@@ -35,7 +35,7 @@ struct UnitDev {
     uint32_t xt_begin;      // first transform tile of the unit in the plan's tile list
     uint32_t et_begin;      // first emit tile (kEmitTile coefficients) of the unit
     uint32_t net;           // emit tiles = max(1, ceil(ncells / kEmitTile))
-    uint32_t sparse;        // staged forward: 1 flagged TZ-coefficient segments, 2 packed rows (wc_xform.h)
+    uint32_t sparse;        // 1: staged forward stores only flagged 32-coefficient segments (wc_xform.h)
     // inverse (wc_inverse.hip)
     uint32_t dt_begin;      // first decode tile (kFlatTile pairs) of the unit: look-back status index
     uint32_t ndt;           // decode tiles launched for the unit
@@ -126,7 +126,6 @@ struct EmitParams {
     uint32_t use_gthresh;          // 1: every unit uses gthresh (global histogram mode), 0: reference rule
     float gthresh;                 // fp32 threshold: keep |c| > gthresh
     const uint8_t* flags;          // sparse-staging segment flags (null: every unit dense)
-    const uint8_t* masks;          // packed-row candidate masks (null: units with sparse == 2 use flags)
 };
 
 constexpr int kSegShift = 4;    // sparse staging: flag index space of 16 coefficients per byte (min segment)

@@ -155,10 +155,7 @@ __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict
             v[r] = k < n ? runs[2 * k] : 0u;
         }
     }
-    if (t == 0 && tid == 0) {
-        if (!hok) atomicOr(err, kErrHeader);
-        rowinfo[U.row_off + (uint64_t)U.nx * U.ny + 1] = make_uint2(n, 0u);  // K6r's pair-count clamp
-    }
+    if (!hok && t == 0 && tid == 0) atomicOr(err, kErrHeader);
 
     // 1. v = run + 1 (k < n), 0 (k >= n) -> saturating in-wave inclusive sums
     const uint32_t kw = t * (uint32_t)kRixTile + (uint32_t)w * (kRixTile / 4);
@@ -188,18 +185,33 @@ __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict
     if (w == 0) {
         unsigned long long* st = status + U.dt_begin;
         uint32_t excl = 0;
+        bool timed_out = false;
         if (t == 0) {
             if (l == 0) st_rlx(st, granule_e(kFlagIncl, epoch, tot));
         } else {
             if (l == 0) st_rlx(st + t, granule_e(kFlagAgg, epoch, tot));
 #ifndef WC_XP_NOLB
-            excl = lookback_sum32e(st, (int64_t)t, l, err, epoch);
+            excl = lookback_sum32e(st, (int64_t)t, l, err, epoch, timed_out);
 #endif
             if (l == 0) st_rlx(st + t, granule_e(kFlagIncl, epoch, sat_add(excl, tot)));
         }
-        if (l == 0) s_x[1] = (uint32_t)excl;
+        if (l == 0) {
+            s_x[0] = timed_out ? 1u : 0u;
+            s_x[1] = (uint32_t)excl;
+        }
     }
     __syncthreads();
+    if (s_x[0]) {
+        // The wait timed out (reported as WC_ERR_HIP): this tile's positions are
+        // unknown, so the rows it should have written would keep an earlier
+        // call's entries, which K6r could follow past this payload.  Overwrite
+        // every row of the unit with an empty range (k = 0): any mix of these
+        // and correctly written entries keeps every pair index within [0, n].
+        uint2* __restrict__ ri = rowinfo + U.row_off;
+        const uint32_t rows = (uint32_t)U.nx * (uint32_t)U.ny + 1u;
+        for (uint32_t r = tid; r < rows; r += kThreads) ri[r] = make_uint2(0u, 0u);
+        return;
+    }
     const uint32_t nc = (uint32_t)U.ncells;
     const uint32_t A = sat_add(s_x[1], wexcl);
 
@@ -596,11 +608,11 @@ __global__ __launch_bounds__(kThreads) void k_inverse_fast(const float* __restri
 // when scattered) and the row entries of tile t + 2G.
 //
 // The row index of a unit is complete and monotone whatever the payload
-// (k_rowindex), negative runs count as 0 as there, every pair index is
-// clamped to the header's nrle (rix_load_range: a row index left incomplete
-// by a timed-out look-back cannot point past the payload) and every LDS
-// address is checked against the range: a malformed payload (reported by K5)
-// gives garbage cells, never an out-of-bounds access.
+// (k_rowindex), negative runs count as 0 as there, a row-index tile whose
+// look-back timed out empties every row entry of its unit (so no entry of an
+// earlier call survives to point past this payload) and every LDS address is
+// checked against the range: a malformed payload (reported by K5) gives
+// garbage cells, never an out-of-bounds access.
 #ifndef WC_RIX_ROUNDS
 #define WC_RIX_ROUNDS 20  // 128 VGPRs with the x-quad synthesis: 4 waves per SIMD, no spills
 #endif
@@ -615,28 +627,18 @@ struct RixRange {
     uint32_t ks, c0, e;  // rowinfo[r0] = (ks, c0), rowinfo[r0 + tyv].x = e
 };
 
-// The pair indices are clamped to the unit's pair count, which k_rowindex's
-// tile 0 stores in this call's entry W*H + 1 (past the sentinel), so every
-// pair load stays inside this payload even when some row entries are not this
-// call's (a row-index look-back that timed out leaves them unwritten: they hold
-// an earlier batch's entries; the call then reports WC_ERR_HIP).  A load of
-// the row table, like the entries: no extra dependent round trip.
 __device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* __restrict__ rowinfo, int w, int l) {
     RixRange R{0u, 0u, 0u};
     const int TX = 1 << T.lbx;
     if (l < TX) {
-#ifndef WC_RIX_CLAMP
-#define WC_RIX_CLAMP 1
-#endif
-        const uint32_t nrle = WC_RIX_CLAMP ? rowinfo[T.row_off + (uint64_t)T.W * T.H + 1].x : 0xffffffffu;
         const int g = w + 4 * l, bxl = g & (TX - 1), ssy = (g >> T.lbx) & 1, ssx = g >> (T.lbx + 1);
         const int bx = T.bx0 + bxl, hx = T.W >> 1, hy = T.H >> 1;
         if (bx < hx) {
             const uint64_t r0 = (uint64_t)(bx + ssx * hx) * T.H + T.by0 + ssy * hy;
             const uint2 a = rowinfo[T.row_off + r0];
-            R.ks = min(a.x, nrle);
+            R.ks = a.x;
             R.c0 = a.y;
-            R.e = min(rowinfo[T.row_off + r0 + T.tyv].x, nrle);
+            R.e = rowinfo[T.row_off + r0 + T.tyv].x;
         }
     }
     return R;

@@ -41,30 +41,18 @@ __global__ __launch_bounds__(kThreads) void k_transform(
     }
 }
 
-// Tile of block b.  xcd: the blocks that share an XCD (b, b + 8, ...: dealt
-// round-robin, observed, MI355X_MICROARCH.md) take a contiguous run of the
-// tile list, so neighbouring tiles — whose segment flags / row masks share
-// lines — write through one L2 (the bijective form for grids not a multiple
-// of 8, cdna_hip_programming.md T1).  Speed only: any placement is correct.
-__device__ __forceinline__ uint32_t k1_tile_index(uint32_t b, uint32_t n, int xcd) {
-    if (!xcd) return b;
-    const uint32_t q = n >> 3, r = n & 7u, x = b & 7u;
-    return x * q + min(x, r) + (b >> 3);
-}
-
 // Even W, H, D with D % 8 == 0: 4 z-blocks per thread, 16-B LDS and global stores.
 // flags != null (staged forward): units with U.sparse store only the flagged
-// TZ-coefficient segments (xform_fast_p2_sparse), or with U.sparse == 2 and
-// masks != null their rows' candidates front-packed (xform_fast_p2_packed).
+// 32-coefficient segments (xform_fast_p2_sparse).
 template <typename T, bool KEYS>
 __global__ __launch_bounds__(kThreads) void k_transform_fast(
     const T* __restrict__ cells, const UnitDev* __restrict__ units, const XTile* __restrict__ tiles,
     float* __restrict__ out, int out_mode, unsigned long long* __restrict__ unit_key,
-    uint8_t* __restrict__ flags, uint32_t* __restrict__ spos, double keep, uint8_t* __restrict__ masks, int xcd) {
+    uint8_t* __restrict__ flags, uint32_t* __restrict__ spos, double keep) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ unsigned long long s_key[kThreads / kWave];
     __shared__ uint32_t s_mag[kThreads / kWave];
-    const XTile td = tiles[k1_tile_index(blockIdx.x, gridDim.x, xcd)];
+    const XTile td = tiles[blockIdx.x];
     const UnitDev& U = units[td.unit];
     const uint64_t obase = out_base(U, out_mode);
     float* __restrict__ dst = out + obase;
@@ -77,11 +65,9 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
             mag = max(max(s_mag[0], s_mag[1]), max(s_mag[2], s_mag[3]));
             const double bound = sparse_bound(mag, keep);
             if (threadIdx.x == 0 && bound >= 0.0) atomicOr(spos + td.unit, 1u);  // a sparsely staged tile
-            const unsigned long long kmax =
-                (masks && U.sparse == 2)
-                    ? xform_fast_p2_packed(U, td, lds, threadIdx.x, bound, masks, dst)
-                    : xform_fast_p2_sparse(U, td, lds, threadIdx.x, bound, flags,
-                                           [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
+            const unsigned long long kmax = xform_fast_p2_sparse(
+                U, td, lds, threadIdx.x, bound, flags,
+                [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
             block_key_max(kmax, s_key, unit_key + td.unit);
             return;
         }
@@ -250,7 +236,7 @@ uint32_t transform_pf_grid(size_t lds) {
 hipError_t launch_transform_fast(hipStream_t st, const void* cells, int dtype, const UnitDev* units,
                                  const XTile* tiles, uint32_t ntiles, size_t lds, float* out,
                                  int out_mode, unsigned long long* keys, uint8_t* flags, uint32_t* spos, double keep,
-                                 uint32_t pf_grid, uint8_t* masks, int xcd) {
+                                 uint32_t pf_grid) {
     if (ntiles == 0) return hipSuccess;
     if (dtype != 1 && !flags) {  // fp32 cells, dense staging: persistent, next tile's cells in flight
         const uint32_t grid = std::min(ntiles, std::max(1u, pf_grid));
@@ -265,17 +251,17 @@ hipError_t launch_transform_fast(hipStream_t st, const void* cells, int dtype, c
     if (dtype == 1) {
         if (keys)
             k_transform_fast<double, true><<<ntiles, kThreads, lds, st>>>((const double*)cells, units, tiles, out,
-                                                                  out_mode, keys, flags, spos, keep, masks, xcd);
+                                                                  out_mode, keys, flags, spos, keep);
         else
             k_transform_fast<double, false><<<ntiles, kThreads, lds, st>>>((const double*)cells, units, tiles, out,
-                                                                  out_mode, keys, flags, spos, keep, masks, xcd);
+                                                                  out_mode, keys, flags, spos, keep);
     } else {
         if (keys)
             k_transform_fast<float, true><<<ntiles, kThreads, lds, st>>>((const float*)cells, units, tiles, out,
-                                                                  out_mode, keys, flags, spos, keep, masks, xcd);
+                                                                  out_mode, keys, flags, spos, keep);
         else
             k_transform_fast<float, false><<<ntiles, kThreads, lds, st>>>((const float*)cells, units, tiles, out,
-                                                                  out_mode, keys, flags, spos, keep, masks, xcd);
+                                                                  out_mode, keys, flags, spos, keep);
     }
     return hipGetLastError();
 }

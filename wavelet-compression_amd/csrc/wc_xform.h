@@ -362,7 +362,7 @@ __device__ __forceinline__ unsigned long long xform_fast_p2(const UnitDev& U, co
 }
 
 
-// Sparse staging (U.sparse >= 1: TZ >= 16 blocks per z tile and hz % TZ == 0, so
+// Sparse staging (U.sparse: TZ >= 16 blocks per z tile and hz % TZ == 0, so
 // each TZ-coefficient flat segment belongs to one tile and to one aligned
 // group of TZ/4 lanes).  A tile whose largest magnitude belongs to a negative
 // coefficient stages densely (the unit's signed max may be that coefficient:
@@ -429,112 +429,6 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
         kmax = k > kmax ? k : kmax;
     }
     return kmax;
-}
-
-// Packed rows (U.sparse == 2: TZ == hz, so a tile produces whole flat rows of
-// D = 2 * TZ coefficients, D = 64 or 128; G = D / 4 lanes per row).  Each
-// row's candidates (|c| > bound, every coefficient when bound < 0) are stored
-// front-packed at the start of the row's dense slot (coef_off + (I*H+J)*D),
-// in K order, and the row's candidate mask at masks + (slot >> 3): D/8 bytes,
-// four words of G bits, word j bit i = coefficient K = 4i + j.  The row is
-// compacted in place in its LDS row (one wave owns a row), then stored with
-// the dense path's 16-B stores, ceil(c / 4) of them: a row with c candidates
-// writes ceil(4c / 128) lines instead of 4D / 128; with every coefficient a
-// candidate the packed row IS the dense row.  Returns this thread's max key
-// over all its coefficients.
-__device__ __forceinline__ unsigned long long xform_fast_p2_packed(const UnitDev& U, const XTile& td, float* lds,
-                                                                   int tid, double bound,
-                                                                   uint8_t* __restrict__ masks,
-                                                                   float* __restrict__ dst) {
-    const int H = U.ny, D = U.nz;
-    const int hx = U.hx, hy = U.hy;
-    const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
-    const int TZ = 1 << lbz;
-    const int rstride = 2 * TZ + 4;
-    const int nrows = 4 << (lbx + lby);
-    const int q4 = lbz - 1;  // log2(G)
-    const int total4 = nrows << q4;
-    const int l = tid & 63;
-    const int gi = l & ((1 << q4) - 1), g0 = l - gi;
-    const unsigned long long below = (1ull << l) - (1ull << g0);  // lanes of my row below me
-    const unsigned long long grp = ((q4 == 5 ? 0xffffffffull : 0xffffull) << g0);
-    const bool all = !(bound >= 0.0);
-    unsigned long long kmax = 0;
-    for (int e = tid; e < total4; e += kThreads) {
-        const int row = e >> q4;
-        int bxl, ssx, byl, ssy;
-        row_of(row, lbx, lby, bxl, ssx, byl, ssy);
-        const int bx = td.bx0 + bxl, by = td.by0 + byl;
-        if (bx >= hx || by >= hy) continue;  // uniform per row
-        const int I = bx + ssx * hx, J = by + ssy * hy;
-        const int64_t frow = ((int64_t)I * H + J) * D;
-        float* lrow = lds + row * rstride;
-        const float4 v = *reinterpret_cast<const float4*>(lrow + 4 * gi);
-        const bool c0 = all || (double)fabsf(v.x) > bound, c1 = all || (double)fabsf(v.y) > bound,
-                   c2 = all || (double)fabsf(v.z) > bound, c3 = all || (double)fabsf(v.w) > bound;
-        const unsigned long long b0 = __ballot(c0), b1 = __ballot(c1), b2 = __ballot(c2), b3 = __ballot(c3);
-        uint32_t p = (uint32_t)(__popcll(b0 & below) + __popcll(b1 & below) + __popcll(b2 & below) +
-                                __popcll(b3 & below));
-        const uint32_t cnt = (uint32_t)(__popcll(b0 & grp) + __popcll(b1 & grp) + __popcll(b2 & grp) +
-                                        __popcll(b3 & grp));
-        // in-place compaction: this wave read the whole row above (LDS operations
-        // of a wave complete in order), so the row's slots are free to rewrite
-        if (c0) lrow[p++] = v.x;
-        if (c1) lrow[p++] = v.y;
-        if (c2) lrow[p++] = v.z;
-        if (c3) lrow[p] = v.w;
-        __builtin_amdgcn_wave_barrier();
-        if (4u * (uint32_t)gi < cnt)
-            *reinterpret_cast<float4*>(dst + frow + 4 * gi) = *reinterpret_cast<const float4*>(lrow + 4 * gi);
-        if (gi == 0) {
-            uint8_t* mp = masks + ((U.coef_off + (uint64_t)frow) >> 3);
-            if (q4 == 5)
-                *reinterpret_cast<uint4*>(mp) = make_uint4((uint32_t)(b0 >> g0), (uint32_t)(b1 >> g0),
-                                                           (uint32_t)(b2 >> g0), (uint32_t)(b3 >> g0));
-            else
-                *reinterpret_cast<uint2*>(mp) =
-                    make_uint2((uint32_t)((b0 >> g0) & 0xffffu) | (uint32_t)((b1 >> g0) & 0xffffu) << 16,
-                               (uint32_t)((b2 >> g0) & 0xffffu) | (uint32_t)((b3 >> g0) & 0xffffu) << 16);
-        }
-        const uint32_t f0 = (uint32_t)(frow + 4 * gi);
-        unsigned long long k = coef_key(v.x, f0);
-        kmax = k > kmax ? k : kmax;
-        k = coef_key(v.y, f0 + 1);
-        kmax = k > kmax ? k : kmax;
-        k = coef_key(v.z, f0 + 2);
-        kmax = k > kmax ? k : kmax;
-        k = coef_key(v.w, f0 + 3);
-        kmax = k > kmax ? k : kmax;
-    }
-    return kmax;
-}
-
-// Emit side of a packed row, in two steps so that a thread's 8 mask loads
-// are in flight together in one VGPR each.  Lanes 4k..4k+3 (one quad, same
-// row: rows are 16- or 32-lane aligned) load the 4 mask words of their row,
-// word j = lane & 3; packed_rank then broadcasts them within the quad (DPP)
-// and returns, for this lane's 4 coefficients 4i..4i+3 (i = (f mod D) / 4),
-// their candidate bits (low 4 bits), the number of candidates before them in
-// the row (<< 4, 7 bits) and the row's candidate count (<< 11).  f:
-// unit-relative flat index; lgD = log2 D (6 or 7).
-__device__ __forceinline__ uint32_t packed_mask_word(const uint8_t* __restrict__ masks, uint64_t coef_off, uint32_t f,
-                                                     int lgD, int l) {
-    const uint8_t* mp = masks + ((coef_off + ((uint64_t)(f >> lgD) << lgD)) >> 3);
-    return lgD == 7 ? reinterpret_cast<const uint32_t*>(mp)[l & 3]
-                    : (uint32_t)reinterpret_cast<const uint16_t*>(mp)[l & 3];
-}
-
-__device__ __forceinline__ uint32_t packed_rank(uint32_t word, uint32_t f, int lgD) {
-    const uint32_t m0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)word, 0x00, 0xf, 0xf, false);  // quad_perm 0,0,0,0
-    const uint32_t m1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)word, 0x55, 0xf, 0xf, false);  // 1,1,1,1
-    const uint32_t m2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)word, 0xaa, 0xf, 0xf, false);  // 2,2,2,2
-    const uint32_t m3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)word, 0xff, 0xf, 0xf, false);  // 3,3,3,3
-    const uint32_t i = (f & ((1u << lgD) - 1u)) >> 2;
-    const uint32_t lo = (1u << i) - 1u;
-    const uint32_t pre = __popc(m0 & lo) + __popc(m1 & lo) + __popc(m2 & lo) + __popc(m3 & lo);
-    const uint32_t c = ((m0 >> i) & 1u) | ((m1 >> i) & 1u) << 1 | ((m2 >> i) & 1u) << 2 | ((m3 >> i) & 1u) << 3;
-    const uint32_t cnt = __popc(m0) + __popc(m1) + __popc(m2) + __popc(m3);
-    return cnt << 11 | pre << 4 | c;
 }
 
 }  // namespace wc
