@@ -147,8 +147,8 @@ def test_host_entry_point_retries_after_timeout(wc, ctx, oracle):
 def test_inverse_timeout_never_reads_past_payload(wc, ctx, oracle):
     """Row entries of an earlier, denser batch are left in the context's row
     index; an inverse of sparser payloads whose row-index look-backs time out
-    must not fault (K6r clamps pair ranges to nrle), reports WC_ERR_HIP, and the
-    next inverse (tickets) reconstructs exactly."""
+    must not fault (the timed-out tile empties its unit's row entries), reports
+    WC_ERR_HIP, and the next inverse (tickets) reconstructs exactly."""
     dense = _boxes(oracle, 64, 64, seed0=45)
     bd = DevBatch(wc, dense)
     bd.forward(wc, ctx)
