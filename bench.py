@@ -69,6 +69,8 @@ def parse(argv=None):
                     help="PMC traffic summaries (tools/pmc_summary.py): a file or a directory of pmc_*.json, "
                          "one per workload; merged into roofline.traffic and each leg's roofline_path.traffic "
                          "when measured on the same workload AND the same kernel sources")
+    ap.add_argument("--rix-xcd", action="store_true",
+                    help="diagnostic: row-indexed inverse tiles in XCD-grouped order (WC_OPT_RIX_XCD 1)")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU/gloo run of the launcher, sharding and reductions (no kernels, no numbers)")
     ap.add_argument("--rehearse", action="store_true",
@@ -251,6 +253,8 @@ def new_context(args, d: Dist):
     ctx = wcamd.capi.Context(d.local)
     if args.rehearse and d.world > 1:
         ctx.set_option(wcamd.capi.WC_OPT_ORDERED, 0)
+    if args.rix_xcd:
+        ctx.set_option(wcamd.capi.WC_OPT_RIX_XCD, 1)
     return ctx
 
 
