@@ -71,6 +71,8 @@ def parse(argv=None):
                          "when measured on the same workload AND the same kernel sources")
     ap.add_argument("--rix-xcd", action="store_true",
                     help="diagnostic: row-indexed inverse tiles in XCD-grouped order (WC_OPT_RIX_XCD 1)")
+    ap.add_argument("--inv-groups", type=int, default=0,
+                    help="diagnostic: WC_OPT_INV_GROUPS of the inverse legs (0: the library default)")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU/gloo run of the launcher, sharding and reductions (no kernels, no numbers)")
     ap.add_argument("--rehearse", action="store_true",
@@ -255,6 +257,8 @@ def new_context(args, d: Dist):
         ctx.set_option(wcamd.capi.WC_OPT_ORDERED, 0)
     if args.rix_xcd:
         ctx.set_option(wcamd.capi.WC_OPT_RIX_XCD, 1)
+    if args.inv_groups:
+        ctx.set_option(wcamd.capi.WC_OPT_INV_GROUPS, args.inv_groups)
     return ctx
 
 

@@ -86,8 +86,13 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  *   16/32-coefficient flat segments that hold some |c| > (tile max) * (1 - keep)
  *   and flags them; the emit loads only flagged segments.  Same bytes out;
  *   0 = dense staging of every coefficient.
- * WC_OPT_RIX_XCD (default 0): the same for the row-indexed inverse's tiles
- *   (neighbouring tiles share payload lines at their range ends).  Same cells.
+ * WC_OPT_RIX_XCD (default 0): the row-indexed inverse's tiles dealt to the XCDs
+ *   in contiguous runs (neighbouring tiles share payload lines at their range
+ *   ends).  Same cells.
+ * WC_OPT_INV_GROUPS (default 2): the row-indexed inverse runs in this many
+ *   unit groups, pipelined: the row index of group g + 1 (latency-bound) runs
+ *   beside the reconstruction of group g on a second stream of the context;
+ *   the call stays ordered on the context's stream.  1 = one group.  Same cells.
  * WC_OPT_ORDERED (default 1): the look-back kernels (forward emit, inverse
  *   decode) take each block's tile index from the launch order, relying on
  *   workgroups being dispatched in increasing id (DESIGN.md §Forward
@@ -136,6 +141,7 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
 #define WC_OPT_SPIN_LIMIT 19
 #define WC_OPT_TICKETS 20
 #define WC_OPT_RIX_XCD 22
+#define WC_OPT_INV_GROUPS 23
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 int wc_get_option(const wc_ctx* ctx, int option, int64_t* value);
 

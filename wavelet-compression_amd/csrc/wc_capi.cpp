@@ -41,7 +41,7 @@ hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, co
                          unsigned long long*, float*, uint2*, uint32_t*, int);
 hipError_t launch_inverse_rows(hipStream_t, const RTile*, uint32_t, size_t, uint32_t, const uint8_t*,
                                const uint64_t*, const uint2*, float*, int, const void*, int, const UnitDev*, int,
-                               double*, double*);
+                               double*, double*, bool);
 hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const XTile*, uint32_t, size_t, uint32_t,
                           size_t, float*);
 hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDev*, int, const FTile*,
@@ -76,6 +76,11 @@ struct Plan {
     int rix_lds = kRixLds;              // WC_OPT_RIX_LDS the plan was built with
     int rix_lx = 4;                     // WC_OPT_RIX_TX the plan was built with
     bool rix_xcd = false;               // WC_OPT_RIX_XCD the plan was built with
+    int inv_groups = 1;                 // WC_OPT_INV_GROUPS the plan was built with
+    // row-indexed inverse in unit groups (pipelined: K5 of group g + 1 runs
+    // beside K6r of group g): group g's row-index tiles are rdtiles
+    // [ig_rd[g], ig_rd[g+1]) and its K6r tiles rtiles [ig_rt[g], ig_rt[g+1])
+    std::vector<uint32_t> ig_rd, ig_rt;
     std::vector<EmitDesc> edesc;  // [units of kEmitTile tiles | units of kEmitTileBig tiles]
     uint32_t nedesc_small = 0;
     uint32_t ngen = 0, nfast = 0, netiles = 0;
@@ -116,6 +121,9 @@ struct wc_ctx {
     int opt_rix_lx = 4;        // WC_OPT_RIX_TX
     bool opt_rix_blocked = false; // WC_OPT_RIX_BLOCKED
     bool opt_rix_xcd = false;     // WC_OPT_RIX_XCD
+    int opt_inv_groups = 2;       // WC_OPT_INV_GROUPS
+    hipStream_t aux = nullptr;    // second stream of the pipelined inverse
+    std::vector<hipEvent_t> iev;  // its events
     // A kernel that may raise error bits ran since the last check.  Kernels
     // atomicOr into ONE persistent error word (errflag, zeroed at creation and
     // after each read), so errors of several async calls accumulate until the
@@ -350,7 +358,7 @@ bool set_rix_tiling(UnitDev& d, int budget, int max_lx) {
 
 bool plan_matches(const wc_ctx* c, const Plan& P, const wc_unit* units, int n) {
     return P.inv_rows == c->opt_inv_rows && P.rix_lds == c->opt_rix_lds && P.rix_lx == c->opt_rix_lx &&
-           P.rix_xcd == c->opt_rix_xcd &&
+           P.rix_xcd == c->opt_rix_xcd && P.inv_groups == c->opt_inv_groups &&
            (int)P.key.size() == n && (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0);
 }
 
@@ -401,6 +409,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     P.rix_lds = c->opt_rix_lds;
     P.rix_lx = c->opt_rix_lx;
     P.rix_xcd = c->opt_rix_xcd;
+    P.inv_groups = c->opt_inv_groups;
     P.units.assign(n, UnitDev{});
     P.xtiles.clear();
     P.ftiles.clear();
@@ -526,15 +535,49 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     P.rdtiles.clear();
     {
         uint32_t maxt = 0, total = 0;
+        uint64_t rix_cells = 0;
         for (UnitDev& d : P.units) {
             d.ndt = d.rix ? (uint32_t)(d.ncells / kRixTile) + 1 : d.nftiles;
             d.dt_begin = total;
             total += d.ndt;
             maxt = std::max(maxt, d.ndt);
+            if (d.rix) rix_cells += d.ncells;
         }
         for (uint32_t t = 0; t < maxt; ++t)
             for (int i = 0; i < n; ++i)
-                if (t < P.units[i].ndt) (P.units[i].rix ? P.rdtiles : P.dtiles).push_back(FTile{(uint32_t)i, t});
+                if (t < P.units[i].ndt && !P.units[i].rix) P.dtiles.push_back(FTile{(uint32_t)i, t});
+        // Row-indexed units in up to inv_groups contiguous unit ranges of about
+        // equal cells (one group with the XCD-grouped K6r order, which permutes
+        // the tiles across units); within a group the row-index tiles are
+        // interleaved by tile index across its units (a tile's look-back waits
+        // only on lower block ids), and the group's K6r tiles are a contiguous
+        // run of the unit-major rtiles.
+        const int ng = P.rix_xcd ? 1 : std::max(1, P.inv_groups);
+        P.ig_rd.assign(1, 0u);
+        P.ig_rt.assign(1, 0u);
+        int a = 0;
+        for (int g = 0; g < ng && a < n; ++g) {
+            const uint64_t target = rix_cells * (uint64_t)(g + 1) / (uint64_t)ng;
+            int b = a;
+            uint64_t acc = 0;
+            for (int i = 0; i < a; ++i) acc += P.units[i].rix ? P.units[i].ncells : 0;
+            for (; b < n && (g == ng - 1 || acc < target); ++b)
+                if (P.units[b].rix) acc += P.units[b].ncells;
+            uint32_t gmax = 0, rt_end = P.ig_rt.back();
+            for (int i = a; i < b; ++i)
+                if (P.units[i].rix) {
+                    gmax = std::max(gmax, P.units[i].ndt);
+                    rt_end = P.units[i].rt_begin + P.units[i].nrt;
+                }
+            for (uint32_t t = 0; t < gmax; ++t)
+                for (int i = a; i < b; ++i)
+                    if (P.units[i].rix && t < P.units[i].ndt) P.rdtiles.push_back(FTile{(uint32_t)i, t});
+            if (P.rdtiles.size() > P.ig_rd.back()) {
+                P.ig_rd.push_back((uint32_t)P.rdtiles.size());
+                P.ig_rt.push_back(P.rix_xcd ? (uint32_t)P.rtiles.size() : rt_end);
+            }
+            a = b;
+        }
     }
     P.coef_extent = coef_cursor ? coef_cursor + kFlatTile : 0;  // slack: flat tiles read whole float4 groups
     build_etiles(P, n);
@@ -601,6 +644,19 @@ uint32_t persistent_grid(wc_ctx* c, int which, size_t lds) {
     const uint32_t g = which == 0 ? transform_pf_grid(lds) : inverse_rows_grid(lds);
     c->grids[key] = g;
     return g;
+}
+
+// The pipelined inverse's second stream and `nev` events (created once).
+int inverse_stream(wc_ctx* c, int nev) {
+    hipError_t e;
+    if (!c->aux && (e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking)) != hipSuccess)
+        return hip_fail(c, e, "inverse stream");
+    while ((int)c->iev.size() < nev) {
+        hipEvent_t ev;
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(c, e, "event");
+        c->iev.push_back(ev);
+    }
+    return WC_OK;
 }
 
 int set_device(wc_ctx* c) {
@@ -800,6 +856,8 @@ void wc_ctx_destroy(wc_ctx* c) {
         if (b->p) (void)hipFree(b->p);
     for (Plan& P : c->plan_cache) free_plan(P);
     for (hipEvent_t e : c->hev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->iev) (void)hipEventDestroy(e);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
     if (c->up) (void)hipStreamDestroy(c->up);
     if (c->down) (void)hipStreamDestroy(c->down);
     if (c->pinned) (void)hipHostFree(c->pinned);
@@ -836,6 +894,10 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
             return WC_OK;
         case WC_OPT_RIX_XCD:
             c->opt_rix_xcd = value != 0;
+            return WC_OK;
+        case WC_OPT_INV_GROUPS:
+            if (value < 1 || value > 16) return fail(c, WC_ERR_INVALID, "WC_OPT_INV_GROUPS: 1..16");
+            c->opt_inv_groups = (int)value;
             return WC_OK;
         case WC_OPT_ORDERED:
             c->opt_ordered = value != 0;
@@ -881,6 +943,7 @@ int wc_get_option(const wc_ctx* c, int option, int64_t* value) {
     switch (option) {
         case WC_OPT_SPARSE: *value = c->opt_sparse; return WC_OK;
         case WC_OPT_RIX_XCD: *value = c->opt_rix_xcd; return WC_OK;
+        case WC_OPT_INV_GROUPS: *value = c->opt_inv_groups; return WC_OK;
         case WC_OPT_ORDERED: *value = use_ordered(c) ? 1 : 0; return WC_OK;  // the form the next launch takes
         case WC_OPT_INVERSE_ROWS: *value = c->opt_inv_rows; return WC_OK;
         case WC_OPT_RIX_LDS: *value = c->opt_rix_lds; return WC_OK;
@@ -1034,7 +1097,7 @@ int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets,
                  const void* d_orig, int dtype, double* d_rmse) {
     Plan& P = c->plan;
     int rc = WC_OK;
-    hipError_t e;
+    hipError_t e = hipSuccess;
     // per-call state of the dense decode and of the ticket form: ticket[n] |
     // status[decode tiles] (zeroed).  The row index needs none: its granules
     // carry the call's epoch.  The dense coefficient scratch is fully written
@@ -1050,21 +1113,60 @@ int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets,
             return hip_fail(c, e, "memset");
         c->epoch = 1;
     }
+    const int ng = (int)P.ig_rd.size() - 1;  // row-indexed groups (0: none)
+    const bool piped = ng > 1 && !c->prof;   // profiling times each kernel alone
+    if (piped && (rc = inverse_stream(c, 2 * ng + 2))) return rc;
+    auto rows = [&](int g, hipStream_t s) {  // K6r over group g's tiles
+        const uint32_t t0 = P.ig_rt[g], nt = P.ig_rt[g + 1] - P.ig_rt[g];
+        return launch_inverse_rows(s, (const RTile*)P.d_rtiles.p + t0, nt, P.lds_rows,
+                                   nt ? persistent_grid(c, 1, P.lds_rows) : 1u, d_payload, d_offsets,
+                                   (const uint2*)c->rowinfo.p, d_out, c->opt_rix_blocked ? 1 : 0, d_orig, dtype,
+                                   (const UnitDev*)P.d_units.p, n, (double*)c->part.p, d_rmse, g == ng - 1);
+    };
+    auto index = [&](int g, hipStream_t s) {  // K5 over group g's tiles (g = ng: the dense decode)
+        const bool dense = g == ng;
+        return launch_decode(s, (const UnitDev*)P.d_units.p, (const FTile*)P.d_dtiles.p,
+                             dense ? (uint32_t)P.dtiles.size() : 0u, (const FTile*)P.d_rdtiles.p + (dense ? 0 : P.ig_rd[g]),
+                             dense ? 0u : P.ig_rd[g + 1] - P.ig_rd[g], (unsigned long long*)c->istate.p, c->epoch,
+                             d_payload, d_offsets, (uint32_t*)st, (unsigned long long*)(st + round_up(4ull * n, 8)),
+                             (float*)c->coef.p, (uint2*)c->rowinfo.p, (uint32_t*)c->errflag.p, ord ? 1 : 0);
+    };
+    if (piped) {
+        // K5 of group g + 1 on the context stream beside K6r of group g on the
+        // aux stream: the latency-bound row index overlaps the streaming
+        // reconstruction; the aux stream joins back before the call returns.
+        hipEvent_t* ev = c->iev.data();
+        if ((e = hipEventRecord(ev[0], c->stream)) != hipSuccess || (e = hipStreamWaitEvent(c->aux, ev[0], 0)) != hipSuccess)
+            return hip_fail(c, e, "inverse pipeline");
+        for (int g = 0; g < ng && e == hipSuccess; ++g) {
+            e = index(g, c->stream);
+            if (e == hipSuccess) e = hipEventRecord(ev[1 + g], c->stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(c->aux, ev[1 + g], 0);
+            if (e == hipSuccess) e = rows(g, c->aux);
+        }
+        if (e == hipSuccess && !P.dtiles.empty()) e = index(ng, c->stream);
+        if (e == hipSuccess) e = hipEventRecord(ev[1 + ng], c->aux);
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, ev[1 + ng], 0);
+        if (e == hipSuccess)
+            e = launch_inverse(c->stream, (const float*)c->coef.p, 0, (const UnitDev*)P.d_units.p,
+                               (const XTile*)P.d_ixtiles.p, P.ign, P.lds_inverse, P.ifast, P.lds_fast, d_out);
+        if (e != hipSuccess) return hip_fail(c, e, "inverse launch");
+        c->err_check_pending = true;
+        return rc;
+    }
     {
         StageTimer t(c, WC_STAGE_DECODE);
-        e = launch_decode(c->stream, (const UnitDev*)P.d_units.p, (const FTile*)P.d_dtiles.p,
-                          (uint32_t)P.dtiles.size(), (const FTile*)P.d_rdtiles.p, (uint32_t)P.rdtiles.size(),
-                          (unsigned long long*)c->istate.p, c->epoch, d_payload, d_offsets, (uint32_t*)st,
-                          (unsigned long long*)(st + round_up(4ull * n, 8)), (float*)c->coef.p, (uint2*)c->rowinfo.p,
-                          (uint32_t*)c->errflag.p, ord ? 1 : 0);
+        for (int g = 0; g <= ng && e == hipSuccess; ++g)
+            if (g < ng || !P.dtiles.empty()) e = index(g, c->stream);
     }
     if (e != hipSuccess) return hip_fail(c, e, "decode launch");
     {
         StageTimer t(c, WC_STAGE_INVERSE);
-        e = launch_inverse_rows(c->stream, (const RTile*)P.d_rtiles.p, (uint32_t)P.rtiles.size(), P.lds_rows,
-                                P.rtiles.empty() ? 1u : persistent_grid(c, 1, P.lds_rows), d_payload, d_offsets,
-                                (const uint2*)c->rowinfo.p, d_out, c->opt_rix_blocked ? 1 : 0, d_orig, dtype,
-                                (const UnitDev*)P.d_units.p, n, (double*)c->part.p, d_rmse);
+        for (int g = 0; g < ng && e == hipSuccess; ++g) e = rows(g, c->stream);
+        if (e == hipSuccess && ng == 0 && d_orig)  // every unit empty: the per-unit RMSE (0) only
+            e = launch_inverse_rows(c->stream, nullptr, 0, 0, 1u, d_payload, d_offsets, (const uint2*)c->rowinfo.p,
+                                    d_out, 0, d_orig, dtype, (const UnitDev*)P.d_units.p, n, (double*)c->part.p,
+                                    d_rmse, true);
         if (e == hipSuccess)
             e = launch_inverse(c->stream, (const float*)c->coef.p, 0, (const UnitDev*)P.d_units.p,
                                (const XTile*)P.d_ixtiles.p, P.ign, P.lds_inverse, P.ifast, P.lds_fast, d_out);

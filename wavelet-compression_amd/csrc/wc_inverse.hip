@@ -1075,11 +1075,15 @@ __global__ __launch_bounds__(64) void k_rmse_rows_final(const UnitDev* __restric
 
 // orig == null: the inverse alone; else also calc_rmse_per_box against orig
 // (dtype 1 fp64, 0 fp32) into rmse[n] via part[ntiles].
+// rmse_final: also launch k_rmse_rows_final (after the last group's tiles).
 hipError_t launch_inverse_rows(hipStream_t st, const RTile* tiles, uint32_t ntiles, size_t lds, uint32_t max_grid,
                                const uint8_t* payload, const uint64_t* offsets, const uint2* rowinfo, float* out,
                                int blocked, const void* orig, int dtype, const UnitDev* units, int n, double* part,
-                               double* rmse) {
-    if (!ntiles) return hipSuccess;
+                               double* rmse, bool rmse_final) {
+    if (!ntiles) {
+        if (orig && rmse_final) k_rmse_rows_final<<<n, 64, 0, st>>>(units, part, rmse);
+        return hipGetLastError();
+    }
     const uint32_t grid = std::min(ntiles, std::max(1u, max_grid));
     if (!orig)
         k_inverse_rows<0><<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out, blocked, orig,
@@ -1090,7 +1094,7 @@ hipError_t launch_inverse_rows(hipStream_t st, const RTile* tiles, uint32_t ntil
     else
         k_inverse_rows<2><<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out, blocked, orig,
                                                        part);
-    if (orig) k_rmse_rows_final<<<n, 64, 0, st>>>(units, part, rmse);
+    if (orig && rmse_final) k_rmse_rows_final<<<n, 64, 0, st>>>(units, part, rmse);
     return hipGetLastError();
 }
 
