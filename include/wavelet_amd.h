@@ -89,10 +89,12 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  * WC_OPT_RIX_XCD (default 0): the row-indexed inverse's tiles dealt to the XCDs
  *   in contiguous runs (neighbouring tiles share payload lines at their range
  *   ends).  Same cells.
- * WC_OPT_INV_GROUPS (default 2): the row-indexed inverse runs in this many
+ * WC_OPT_INV_GROUPS (default 1): the row-indexed inverse runs in this many
  *   unit groups, pipelined: the row index of group g + 1 (latency-bound) runs
  *   beside the reconstruction of group g on a second stream of the context;
- *   the call stays ordered on the context's stream.  1 = one group.  Same cells.
+ *   the call stays ordered on the context's stream.  Same cells.  Measured
+ *   slower on MI355X (C2: 0.53 ms at 1 group, 0.62 at 2, 0.59 at 4), kept as
+ *   an option for workloads whose row index dominates.
  * WC_OPT_ORDERED (default 1): the look-back kernels (forward emit, inverse
  *   decode) take each block's tile index from the launch order, relying on
  *   workgroups being dispatched in increasing id (DESIGN.md §Forward

@@ -6,7 +6,7 @@
 //
 // usage: wc_bench [boxes=1024] [dim=64|c3] [f64|f32] [keep=0.999] [steps=10] [warmup=2] [inverse=0|1|2]
 //                 [check=0|1] [ordered=1] [sparse=1] [rows=1] [rix_lds=9216] [rix_tx=4] [rix_blocked=0]
-//                 [rix_xcd=0] [inv_groups=2]
+//                 [rix_xcd=0] [inv_groups=1]
 // check=1: also run the conservative configuration (ticket look-back, dense
 // staging, dense inverse decode) once and compare every unit's payload bytes and, with inverse=1,
 // every reconstructed cell ("paths_identical" in the JSON line).
@@ -110,7 +110,7 @@ int main(int argc, char** argv) {
     const int rix_tx = argc > 13 ? std::atoi(argv[13]) : 4;
     const int rix_blocked = argc > 14 ? std::atoi(argv[14]) : 0;
     const int rix_xcd = argc > 15 ? std::atoi(argv[15]) : 0;
-    const int inv_groups = argc > 16 ? std::atoi(argv[16]) : 2;
+    const int inv_groups = argc > 16 ? std::atoi(argv[16]) : 1;
 
     std::vector<wc_unit> units;
     if (c3) {

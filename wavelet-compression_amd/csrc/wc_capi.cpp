@@ -121,7 +121,7 @@ struct wc_ctx {
     int opt_rix_lx = 4;        // WC_OPT_RIX_TX
     bool opt_rix_blocked = false; // WC_OPT_RIX_BLOCKED
     bool opt_rix_xcd = false;     // WC_OPT_RIX_XCD
-    int opt_inv_groups = 2;       // WC_OPT_INV_GROUPS
+    int opt_inv_groups = 1;       // WC_OPT_INV_GROUPS
     hipStream_t aux = nullptr;    // second stream of the pipelined inverse
     std::vector<hipEvent_t> iev;  // its events
     // A kernel that may raise error bits ran since the last check.  Kernels
