@@ -148,7 +148,7 @@ int main(int argc, char** argv) {
     uint32_t* kept = nullptr;
     float* regen = nullptr;
     CK(hipMalloc(&payload, cap));
-    CK(hipMalloc(&offsets, 8 * (boxes + 1)));
+    CK(hipMalloc(&offsets, 8 * (2 * boxes + 1)));
     CK(hipMalloc(&kept, 4 * boxes));
     double* rmse = nullptr;
     if (inverse) CK(hipMalloc(&regen, 4 * extent));
@@ -167,8 +167,22 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "options: %s\n", wc_last_error(ctx));
         return 2;
     }
+    // WCB_CHUNK=k (uniform cubes only, diagnostic): the forward as boxes/k calls of k
+    // units each (same unit list, cells/payload pointers advanced per call), so the
+    // context's coefficient staging is one k-unit buffer reused by every call.
+    const char* chunk_env = std::getenv("WCB_CHUNK");
+    const int chunk = (!c3 && chunk_env) ? std::atoi(chunk_env) : 0;
     auto fwd = [&]() {
-        int rc = wc_forward(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, keep, payload, cap, offsets, kept);
+        int rc = WC_OK;
+        if (chunk > 0 && chunk < boxes && boxes % chunk == 0) {
+            const uint64_t per = (uint64_t)dim * dim * dim;
+            const uint64_t ccap = wc_payload_bound(units.data(), chunk);
+            for (int g = 0; g < boxes / chunk && rc == WC_OK; ++g)
+                rc = wc_forward(ctx, (uint8_t*)cells + esz * per * chunk * g, f64 ? WC_F64 : WC_F32, units.data(),
+                                chunk, keep, payload + ccap * g, ccap, offsets + (chunk + 1) * g, kept + chunk * g);
+        } else {
+            rc = wc_forward(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, keep, payload, cap, offsets, kept);
+        }
         if (rc != WC_OK) {
             std::fprintf(stderr, "wc_forward: %s\n", wc_last_error(ctx));
             std::exit(2);
