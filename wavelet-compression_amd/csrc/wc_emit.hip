@@ -250,13 +250,16 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
 #ifndef WC_EMIT_MINB
 #define WC_EMIT_MINB 8  // 4-wave launch: workgroups per CU the register budget is sized for (64 VGPRs)
 #endif
+#ifndef WC_EMIT_MINB8
+#define WC_EMIT_MINB8 2  // 8-wave launch (units of >= 2^21 cells)
+#endif
 // One block per emit tile (EW waves: EW * 2048 coefficients).  Block b packs
 // the tile edesc[b] in the ordered form, or the next ticket of edesc[b]'s unit
 // in the ticket form.  The plan lists blocks interleaved by tile index across
 // the units of a group, groups in reverse transform order (wc_capi.cpp
 // build_etiles); units of kEmitBigCells or more cells form the 8-wave launch.
 template <int EW>
-__global__ __launch_bounds__(EW * kWave, EW == 4 ? WC_EMIT_MINB : 2) void k_emit(EmitParams P,
+__global__ __launch_bounds__(EW * kWave, EW == 4 ? WC_EMIT_MINB : WC_EMIT_MINB8) void k_emit(EmitParams P,
                                                                            const float* __restrict__ coef) {
     __shared__ __attribute__((aligned(16))) uint32_t sm[32];
     __shared__ uint2 stage_all[EW][256];  // per-wave pair stage (emit_pairs)

@@ -118,7 +118,13 @@ __device__ __forceinline__ void write_rows(uint2* __restrict__ ri, uint32_t r_lo
 // the payload's pair tiles exit after the header.  The look-back granules are
 // epoch-tagged: no zeroing between calls.
 
-__global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict__ units,
+#ifndef WC_RIX_LDSV
+#define WC_RIX_LDSV 1  // park the inclusive sums in LDS across the look-back (16 KB per workgroup)
+#endif
+#ifndef WC_RIX_MINB
+#define WC_RIX_MINB 8  // waves per SIMD the register budget is sized for (4-wave blocks: 8 per CU, <= 64 VGPRs)
+#endif
+__global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDev* __restrict__ units,
                                                      const FTile* __restrict__ tiles, uint32_t* __restrict__ ticket,
                                                      const uint8_t* __restrict__ payload,
                                                      const uint64_t* __restrict__ offsets,
@@ -127,6 +133,11 @@ __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict
                                                      int ordered, uint32_t epoch) {
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_x[2];
+#if WC_RIX_LDSV
+    // the waves' inclusive sums, parked across the look-back (round r of thread
+    // tid at [r][tid]: the row phase holds no 16-register array)
+    __shared__ uint32_t s_v[kRixRounds5][kThreads];
+#endif
     const int tid = threadIdx.x, l = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const FTile ft = cst(tiles)[blockIdx.x];
@@ -168,7 +179,11 @@ __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict
         neg |= k < n && run < 0;
         const uint32_t x = k < n ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
         const uint32_t s = wave_incl_sum32_sat(x);
+#if WC_RIX_LDSV
+        s_v[r][tid] = sat_add(wsum, s);
+#else
         v[r] = sat_add(wsum, s);
+#endif
         wsum = sat_add(wsum, __builtin_amdgcn_readlane(s, 63));
     }
     if (neg) atomicOr(err, kErrNegativeRun);
@@ -228,7 +243,12 @@ __global__ __launch_bounds__(kThreads) void k_rowindex(const UnitDev* __restrict
 #pragma unroll
     for (int r = 0; r < kRixRounds5; ++r) {
         const uint32_t k = kw + r * 64 + l;
-        const uint32_t phk = k < n ? min(sat_add(A, v[r]) - 1u, nc) : nc;
+#if WC_RIX_LDSV
+        const uint32_t vr = s_v[r][tid];
+#else
+        const uint32_t vr = v[r];
+#endif
+        const uint32_t phk = k < n ? min(sat_add(A, vr) - 1u, nc) : nc;
         const int32_t rhi = k <= n ? (int32_t)div_rows(phk, U.dmagic) : -1;
         // rhi of pair k - 1: lane l - 1, the carry in lane 0
         const int32_t from = __builtin_amdgcn_ds_bpermute((l - 1) << 2, rhi);
