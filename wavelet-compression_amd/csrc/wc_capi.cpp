@@ -268,12 +268,20 @@ uint64_t round_up(uint64_t v, uint64_t m) { return (v + m - 1) / m * m; }
 // across the units of a group, so that a tile's look-back predecessors (the
 // lower tile indices of its unit) have lower block ids and the per-unit
 // traffic spreads over the group instead of arriving in one burst.  Groups
-// hold >= 8192 tiles (256 MB of fp32 coefficients, the Infinity Cache's size)
-// and >= 128 x the longest unit's tile chain (a look-back chain advances one
-// tile per status round trip, so long chains need the whole launch to hide
-// in), and run in REVERSE transform order: the first emit blocks read the
-// coefficients K1 wrote last, which may still be in the Infinity Cache.
-// Measured: 1024 x 64^3 emit 0.346 -> 0.327 ms.
+// hold >= WC_EMIT_GROUP tiles and >= 128 x the longest unit's tile chain (a
+// look-back chain advances one tile per status round trip, so long chains
+// need the whole launch to hide in), and run in REVERSE transform order: the
+// first emit blocks read the coefficients K1 wrote last, which may still be
+// in the Infinity Cache (round 1, 8192-tile groups: 1024 x 64^3 emit 0.346 ->
+// 0.327 ms).  Round 3: 65536-tile groups (a tile's predecessor 1024+ blocks
+// earlier in a batch of many units) measured equal for 1024 x 64^3 and C5,
+// 3-5 % faster for 32^3 and 16^3 batches (profiles/r03/experiments/gpu_emit_group.txt).
+#ifndef WC_EMIT_GROUP
+#define WC_EMIT_GROUP 65536     // emit tiles per dispatch group, 4-wave launch (round 3; was 8192)
+#endif
+#ifndef WC_EMIT_GROUP_BIG
+#define WC_EMIT_GROUP_BIG 65536 // the 8-wave launch (units of >= kEmitBigCells; was 4096)
+#endif
 void build_etiles(Plan& P, int n) {
     auto big = [](const UnitDev& d) { return d.ncells >= kEmitBigCells; };
     uint32_t total = 0;
@@ -296,7 +304,7 @@ void build_etiles(Plan& P, int n) {
             if (big(P.units[i]) == (cls == 1)) us.push_back(i);
         uint32_t maxt = 0;
         for (int i : us) maxt = std::max(maxt, P.units[i].net);
-        const uint64_t group_tiles = std::max<uint64_t>(cls ? 4096 : 8192, 128ull * maxt);
+        const uint64_t group_tiles = std::max<uint64_t>(cls ? WC_EMIT_GROUP_BIG : WC_EMIT_GROUP, 128ull * maxt);
         std::vector<std::pair<size_t, size_t>> groups;  // ranges [g0, g1) of us
         for (size_t g0 = 0; g0 < us.size();) {
             uint64_t tiles = 0;
