@@ -248,6 +248,8 @@ int upload(wc_ctx* c, DevBuf& d, const void* h, size_t bytes, const char* what) 
 void set_tiling(UnitDev& d) {
     // Up to 32 blocks along x (coalesced input rows) and z (contiguous flat
     // rows), the rest along y, at most kMaxTileBlocks blocks per tile.
+    // (64 x 1 x 16 tiles for 128^3 units — whole 512-B fp32 rows — measured
+    // slower, round 3: profiles/r03/experiments/gpu_x6.txt.)
     d.lbx = std::min(5, ceil_log2(std::max(1, d.nbx)));
     d.lbz = std::min(5, ceil_log2(std::max(1, d.nbz)));
     d.lby = std::min(ceil_log2(std::max(1, d.nby)), 10 - d.lbx - d.lbz);
@@ -273,14 +275,15 @@ uint64_t round_up(uint64_t v, uint64_t m) { return (v + m - 1) / m * m; }
 // need the whole launch to hide in), and run in REVERSE transform order: the
 // first emit blocks read the coefficients K1 wrote last, which may still be
 // in the Infinity Cache (round 1, 8192-tile groups: 1024 x 64^3 emit 0.346 ->
-// 0.327 ms).  Round 3: 65536-tile groups (a tile's predecessor 1024+ blocks
-// earlier in a batch of many units) measured equal for 1024 x 64^3 and C5,
-// 3-5 % faster for 32^3 and 16^3 batches (profiles/r03/experiments/gpu_emit_group.txt).
+// 0.327 ms).  Round 3: 65536-tile groups were 3-5 % faster for 8192 x 32^3
+// and 32768 x 16^3, equal for 1024 x 64^3, but 7-9 % slower for the full C5
+// and C4 batches, where the reverse-order Infinity-Cache reuse matters
+// (profiles/r03/experiments/gpu_emit_group.txt): kept at 8192 / 4096.
 #ifndef WC_EMIT_GROUP
-#define WC_EMIT_GROUP 65536     // emit tiles per dispatch group, 4-wave launch (round 3; was 8192)
+#define WC_EMIT_GROUP 8192      // emit tiles per dispatch group, 4-wave launch
 #endif
 #ifndef WC_EMIT_GROUP_BIG
-#define WC_EMIT_GROUP_BIG 65536 // the 8-wave launch (units of >= kEmitBigCells; was 4096)
+#define WC_EMIT_GROUP_BIG 4096  // the 8-wave launch (units of >= kEmitBigCells)
 #endif
 void build_etiles(Plan& P, int n) {
     auto big = [](const UnitDev& d) { return d.ncells >= kEmitBigCells; };
