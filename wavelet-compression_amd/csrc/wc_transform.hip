@@ -21,6 +21,10 @@ __device__ __forceinline__ uint64_t out_base(const UnitDev& U, int mode) {
 }
 
 // ---------------------------------------------------------------------------
+#ifndef WC_K1_S32
+#define WC_K1_S32 1  // the 32 x 1 x 32 tile shape specialised (wc_xform.h s32_ok)
+#endif
+
 // K1 kernels of the staged path: one tile per workgroup, coefficients written
 // to the flat scratch (plain stores: the next kernel reads them), the unit's
 // max key reduced with one 64-bit atomicMax per wave.
@@ -58,16 +62,20 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
     float* __restrict__ dst = out + obase;
     if constexpr (KEYS) {
         if (flags && U.sparse) {  // uniform; coef_off is 128-B aligned here
-            uint32_t mag = xform_fast_p1<T, false, true>(cells + U.cell_off, U, td, lds, threadIdx.x);
+            const bool s32 = WC_K1_S32 && s32_ok(U);  // uniform
+            uint32_t mag = s32 ? xform_fast_p1<T, false, true, true>(cells + U.cell_off, U, td, lds, threadIdx.x)
+                               : xform_fast_p1<T, false, true>(cells + U.cell_off, U, td, lds, threadIdx.x);
             mag = wave_max_u32(mag);
             if ((threadIdx.x & 63) == 0) s_mag[threadIdx.x >> 6] = mag;
             __syncthreads();
             mag = max(max(s_mag[0], s_mag[1]), max(s_mag[2], s_mag[3]));
             const double bound = sparse_bound(mag, keep);
             if (threadIdx.x == 0 && bound >= 0.0) atomicOr(spos + td.unit, 1u);  // a sparsely staged tile
-            const unsigned long long kmax = xform_fast_p2_sparse(
-                U, td, lds, threadIdx.x, bound, flags,
-                [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
+            // mag >> 1: the tile's largest |c| bits (NaN patterns above +inf's)
+            const unsigned long long kmax =
+                s32 ? xform_fast_p2_sparse_s32(U, td, lds, threadIdx.x, bound, mag >> 1, flags, dst)
+                    : xform_fast_p2_sparse(U, td, lds, threadIdx.x, bound, flags,
+                                           [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
             block_key_max(kmax, s_key, unit_key + td.unit);
             return;
         }

@@ -168,24 +168,28 @@ __device__ __forceinline__ unsigned long long xform_generic_p2(const UnitDev& U,
 // MAG: also return the max of this thread's (|c| bits << 1 | sign) (NaN
 // patterns are above +inf's): the largest magnitude for the sparse-staging
 // bound, and in bit 0 whether some coefficient of that magnitude is negative.
-template <typename T, bool SPLIT = false, bool MAG = false>
+// S32 (template): the tile shape is the compile-time 32 x 1 x 32 blocks, the
+// unit's hx and hz are multiples of 32 and its cells 16-B / 8-B aligned
+// (s32_ok): no bounds checks, no unaligned-load branches, index arithmetic
+// folded (the shape of every C2 and C5 unit).
+template <typename T, bool SPLIT = false, bool MAG = false, bool S32 = false>
 __device__ __forceinline__ uint32_t xform_fast_p1(const T* __restrict__ src, const UnitDev& U,
                                                   const XTile& td, float* lds, int tid) {
     uint32_t mag = 0;
     const int W = U.nx, H = U.ny;
     const int hx = U.hx, hy = U.hy, hz = U.hz;
-    const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
+    const int lbx = S32 ? 5 : U.lbx, lby = S32 ? 0 : U.lby, lbz = S32 ? 5 : U.lbz;
     const int TX = 1 << lbx, TY = 1 << lby, TZ = 1 << lbz;
     const int rstride = 2 * TZ + 4;
     const int ncol = (TX * TY * TZ) >> 2;
     const int64_t sy = W, sz = (int64_t)W * H;
-    const bool vec = (U.cell_off & 1) == 0;
+    const bool vec = S32 || (U.cell_off & 1) == 0;
     for (int ci = tid; ci < ncol; ci += kThreads) {
         const int bxl = ci & (TX - 1);
         const int byl = (ci >> lbx) & (TY - 1);
         const int bzq = ci >> (lbx + lby);  // quad of z-blocks within the tile
         const int bx = td.bx0 + bxl, by = td.by0 + byl, bzb = td.bz0 + 4 * bzq;
-        if (bx >= hx || by >= hy || bzb >= hz) continue;
+        if (!S32 && (bx >= hx || by >= hy || bzb >= hz)) continue;
         const T* p0 = src + 2 * (int64_t)bx + sy * (2 * by) + sz * (2 * (int64_t)bzb);
         float c[4][2][2][2];  // [q][sz][sy][sx]
         // Two halves of 4 z-planes (8 x-pair loads in flight each): bounds the
@@ -375,6 +379,10 @@ __device__ __forceinline__ unsigned long long xform_fast_p2(const UnitDev& U, co
 // holds no kept coefficient.  A NaN in the tile, or a bound that is not >= 0,
 // flags every segment.  Units whose thresh turns out < 0 (negative signed
 // max: everything kept) are re-staged densely by k_transform_fallback.
+__device__ __forceinline__ bool s32_ok(const UnitDev& U) {
+    return U.lbx == 5 && U.lby == 0 && U.lbz == 5 && ((U.hx | U.hz) & 31) == 0 && (U.cell_off & 1) == 0;
+}
+
 __device__ __forceinline__ double sparse_bound(uint32_t magkey, double keep) {
     const uint32_t magbits = magkey >> 1;
     if (magbits > 0x7f800000u || (magkey & 1u)) return -1.0;  // NaN in the tile, or a negative max: dense
@@ -427,6 +435,55 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
         kmax = k > kmax ? k : kmax;
         k = coef_key(v.w, f0 + 3);
         kmax = k > kmax ? k : kmax;
+    }
+    return kmax;
+}
+
+// xform_fast_p2_sparse for the S32 shape (s32_ok), in fewer instructions:
+//  * the candidate test |c| > bound in fp32 against bf = bound rounded toward
+//    -inf (thresh_as_float: exact for every float |c|) instead of fp64;
+//  * the max key only where it can win: amax = the tile's largest non-NaN |c|
+//    bits (from phase 1's MAG, passed in; ~0u when the tile holds a NaN, then
+//    every coefficient gets its key as in xform_fast_p2_sparse); a coefficient
+//    whose |c| bits differ from amax cannot carry the tile's max key, and a NaN
+//    at flat index 0 (the kKeyNaNFirst sentinel) is checked where it can sit;
+//  * the loop unrolled over the constant shape (8 float4 per thread: row
+//    (tid >> 4) + 16 it, 4 K from (tid & 15) * 4).
+__device__ __forceinline__ unsigned long long xform_fast_p2_sparse_s32(const UnitDev& U, const XTile& td,
+                                                                       const float* lds, int tid, double bound,
+                                                                       uint32_t amax, uint8_t* __restrict__ flags,
+                                                                       float* __restrict__ dst) {
+    constexpr int lbz = 5, TZ = 32, rstride = 2 * TZ + 4;
+    const int H = U.ny, D = U.nz, hx = U.hx, hy = U.hy, hz = U.hz;
+    const int r0 = tid >> 4, col = (tid & 15) << 2;
+    const int ssz = col >> lbz, bzl = col & (TZ - 1);
+    const int K = td.bz0 + bzl + ssz * hz;
+    const int g0 = (tid & 63) & ~7;  // 8 lanes per 32-coefficient segment
+    const bool dense = !(bound >= 0.0);
+    const float bf = thresh_as_float(bound);
+    const bool allkeys = amax > 0x7f800000u;  // a NaN in the tile: every key as in the generic form
+    unsigned long long kmax = 0;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int row = r0 + 16 * it;  // row_of with lbx 5, lby 0: bxl, ssx, ssy
+        const int bxl = row & 31, ssx = (row >> 5) & 1, ssy = row >> 6;
+        const int I = td.bx0 + bxl + ssx * hx, J = (int)td.by0 + ssy * hy;
+        const int64_t f = ((int64_t)I * H + J) * D + K;
+        const float4 v = *reinterpret_cast<const float4*>(lds + row * rstride + col);
+        const bool cand = fabsf(v.x) > bf || fabsf(v.y) > bf || fabsf(v.z) > bf || fabsf(v.w) > bf;
+        const bool flag = ((__ballot(cand) >> g0) & 0xffull) != 0 || dense;
+        if (flag) *reinterpret_cast<float4*>(dst + f) = v;
+        if ((tid & 7) == 0) flags[(U.coef_off >> kSegShift) + ((uint64_t)f >> lbz)] = flag ? 1 : 0;
+        const uint32_t f0 = (uint32_t)f;
+        const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t ab = __float_as_uint(e[j]) & 0x7fffffffu;
+            if (allkeys || ab == amax || (f0 + j == 0 && ab > 0x7f800000u)) {
+                const unsigned long long k = coef_key(e[j], f0 + (uint32_t)j);
+                kmax = k > kmax ? k : kmax;
+            }
+        }
     }
     return kmax;
 }
