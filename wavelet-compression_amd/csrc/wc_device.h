@@ -44,6 +44,70 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
+// Wave reductions on DPP lane moves (row_shr 1/2/4/8 inside 16-lane rows,
+// then row_bcast 15 / 31 across them, as wave_incl_sum below): lane 63 ends
+// with the reduction over all 64 lanes, returned uniformly by readlane.  A
+// chain of six VALU ops instead of six LDS-crossbar bpermutes (__shfl_xor).
+// Lanes whose DPP source is out of range read 0, the identity of the unsigned
+// max and of the sum.
+#ifndef WC_DPP_RED
+#define WC_DPP_RED 1
+#endif
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return __builtin_amdgcn_update_dpp(0u, v, CTRL, ROW_MASK, 0xf, false);
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32_u(uint32_t v) {
+#if WC_DPP_RED
+    v = max(v, dpp_u32<0x111, 0xf>(v));
+    v = max(v, dpp_u32<0x112, 0xf>(v));
+    v = max(v, dpp_u32<0x114, 0xf>(v));
+    v = max(v, dpp_u32<0x118, 0xf>(v));
+    v = max(v, dpp_u32<0x142, 0xa>(v));
+    v = max(v, dpp_u32<0x143, 0xc>(v));
+    return __builtin_amdgcn_readlane(v, 63);
+#else
+    return wave_max_u32(v);
+#endif
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32_u(uint32_t v) {
+#if WC_DPP_RED
+    v += dpp_u32<0x111, 0xf>(v);
+    v += dpp_u32<0x112, 0xf>(v);
+    v += dpp_u32<0x114, 0xf>(v);
+    v += dpp_u32<0x118, 0xf>(v);
+    v += dpp_u32<0x142, 0xa>(v);
+    v += dpp_u32<0x143, 0xc>(v);
+    return __builtin_amdgcn_readlane(v, 63);
+#else
+    return wave_sum(v);
+#endif
+}
+
+__device__ __forceinline__ unsigned long long dpp_u64_max_step(unsigned long long v, uint32_t lo, uint32_t hi) {
+    const unsigned long long w = ((unsigned long long)hi << 32) | lo;
+    return w > v ? w : v;
+}
+
+__device__ __forceinline__ unsigned long long wave_max_u64_u(unsigned long long v) {
+#if WC_DPP_RED
+#define WC_MAX64_STEP(C, M) v = dpp_u64_max_step(v, dpp_u32<C, M>((uint32_t)v), dpp_u32<C, M>((uint32_t)(v >> 32)))
+    WC_MAX64_STEP(0x111, 0xf);
+    WC_MAX64_STEP(0x112, 0xf);
+    WC_MAX64_STEP(0x114, 0xf);
+    WC_MAX64_STEP(0x118, 0xf);
+    WC_MAX64_STEP(0x142, 0xa);
+    WC_MAX64_STEP(0x143, 0xc);
+#undef WC_MAX64_STEP
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 63), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+#else
+    return wave_max_u64(v);
+#endif
+}
+
 // Load the x-pair (x, x+1) of a row as fp32 (fp64 cells narrowed RNE,
 // src/preprocess.cpp:78).  `vec`: both elements in one aligned vector load.
 // NT: non-temporal (streaming) vector load: the cells are read exactly once.
@@ -288,7 +352,7 @@ __device__ __forceinline__ void lds_barrier() {
 template <bool LDS_ONLY = false>
 __device__ __forceinline__ void block_key_max(unsigned long long v, unsigned long long* s,
                                               unsigned long long* dst) {
-    v = wave_max_u64(v);
+    v = wave_max_u64_u(v);
     if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
     if constexpr (LDS_ONLY)
         lds_barrier();

@@ -65,7 +65,7 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
             const bool s32 = WC_K1_S32 && s32_ok(U);  // uniform
             uint32_t mag = s32 ? xform_fast_p1<T, false, true, true>(cells + U.cell_off, U, td, lds, threadIdx.x)
                                : xform_fast_p1<T, false, true>(cells + U.cell_off, U, td, lds, threadIdx.x);
-            mag = wave_max_u32(mag);
+            mag = wave_max_u32_u(mag);
             if ((threadIdx.x & 63) == 0) s_mag[threadIdx.x >> 6] = mag;
             __syncthreads();
             mag = max(max(s_mag[0], s_mag[1]), max(s_mag[2], s_mag[3]));
