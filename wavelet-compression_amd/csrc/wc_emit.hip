@@ -23,6 +23,10 @@
 // Every spin is bounded (spin_fail) and raises kErrTimeout, never a hang.
 #include "wc_xform.h"
 
+#ifndef WC_EMIT_FULL
+#define WC_EMIT_FULL 1  // full emit tiles skip the per-element range checks
+#endif
+
 namespace wc {
 
 namespace {
@@ -89,7 +93,7 @@ __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, ui
         for (uint32_t k = (uint32_t)l; k < itot; k += 64) pairs[rank + k] = stage[k];
         __builtin_amdgcn_wave_barrier();
         rank += itot;
-        prev = __shfl(lane_last, 63 - __clzll(any));
+        prev = __builtin_amdgcn_readlane(lane_last, 63 - __clzll(any));  // uniform source lane
     }
 }
 
@@ -109,11 +113,24 @@ __device__ __forceinline__ uint32_t keep_bits(const float4 (&q)[8], float tf, ui
     return kb;
 }
 
+// keep_bits of a full chunk (len == EW * 2048: every element in range).
+__device__ __forceinline__ uint32_t keep_bits_full(const float4 (&q)[8], float tf) {
+    uint32_t kb = 0;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        kb |= (uint32_t)(fabsf(q[it].x) > tf) << (it * 4);
+        kb |= (uint32_t)(fabsf(q[it].y) > tf) << (it * 4 + 1);
+        kb |= (uint32_t)(fabsf(q[it].z) > tf) << (it * 4 + 2);
+        kb |= (uint32_t)(fabsf(q[it].w) > tf) << (it * 4 + 3);
+    }
+    return kb;
+}
+
 // Per-wave kept count and last kept (chunk-relative index + 1, 0 = none).
 __device__ __forceinline__ void wave_totals(uint32_t kb, int w, int l, uint32_t& cnt, uint32_t& last) {
-    cnt = wave_sum((uint32_t)__popc(kb));
+    cnt = wave_sum_u32_u((uint32_t)__popc(kb));
     const int hb = kb ? 31 - __clz(kb) : 0;
-    last = wave_max_u32(kb ? (uint32_t)(w * 2048 + (hb >> 2) * 256 + l * 4 + (hb & 3) + 1) : 0u);
+    last = wave_max_u32_u(kb ? (uint32_t)(w * 2048 + (hb >> 2) * 256 + l * 4 + (hb & 3) + 1) : 0u);
 }
 
 // Unit E.unit's header (src/compressor.cpp:55-80: int32 W, H, D, ncoeff,
@@ -165,11 +182,19 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
     const float4* __restrict__ p4 = reinterpret_cast<const float4*>(coef + U.coef_off + start);
     if (!(tf >= 0.0f)) segf = 0xffu;
     float4 q[8];
+    uint32_t kb;
+    if (WC_EMIT_FULL && len == kTile) {  // uniform: a full tile, no range checks
 #pragma unroll
-    for (int it = 0; it < 8; ++it)
-        q[it] = ((segf >> it) & 1u) && (uint32_t)(w * 2048 + it * 256 + 4 * l) < len ? p4[w * 512 + it * 64 + l]
-                                                                                      : make_float4(0, 0, 0, 0);
-    const uint32_t kb = keep_bits(q, tf, len, w, l);
+        for (int it = 0; it < 8; ++it)
+            q[it] = ((segf >> it) & 1u) ? p4[w * 512 + it * 64 + l] : make_float4(0, 0, 0, 0);
+        kb = keep_bits_full(q, tf);
+    } else {
+#pragma unroll
+        for (int it = 0; it < 8; ++it)
+            q[it] = ((segf >> it) & 1u) && (uint32_t)(w * 2048 + it * 256 + 4 * l) < len ? p4[w * 512 + it * 64 + l]
+                                                                                          : make_float4(0, 0, 0, 0);
+        kb = keep_bits(q, tf, len, w, l);
+    }
     uint32_t wcnt, wlast;
     wave_totals(kb, w, l, wcnt, wlast);
     if (l == 0) {
@@ -212,7 +237,7 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
                 const int take = kI < kZ ? kI + 1 : kZ;  // lanes [0, take) are summed
                 if (take > 0) {
                     const bool in = l < take;
-                    ecnt += wave_sum(in ? (uint32_t)((v >> 31) & kMask31) : 0u);
+                    ecnt += wave_sum_u32_u(in ? (uint32_t)((v >> 31) & kMask31) : 0u);
                     const unsigned long long hasl = __ballot(in && (v & kMask31) != 0);
                     const uint32_t hl = __shfl((uint32_t)(v & kMask31), hasl ? __ffsll((long long)hasl) - 1 : 0);
                     if (elast == 0 && hasl) elast = hl;
