@@ -817,3 +817,44 @@ def test_inverse_unit_groups_pipelined(wc, ctx, oracle, groups):
         assert d_r2.cpu().tolist() == [0.0, 0.0]
     finally:
         ctx.set_option(WC_OPT_INV_GROUPS, 2)
+
+
+def test_s32_shape_special_values(wc, ctx, oracle):
+    """The specialised 32 x 1 x 32 transform tiles (wc_xform.h s32_ok: every C2 and
+    C5 unit) take the max key only where |c| equals the tile's largest |c|, and
+    test candidates in fp32 against the bound rounded toward -inf: the
+    reference's quirks on that shape (64 x 16 x 64 and 64^3 boxes, cells at
+    even offsets, fp32 and fp64) — NaN at flat index 0 (nothing kept), a NaN
+    later, +/-inf, ties of +M and -M in different tiles (the first in flat order
+    decides the sign: a negative max keeps everything, re-staged densely),
+    -0.0 among zeros, constant fields (every coefficient ties), denormals — at
+    keep 0.5, 0.999f, 1.0 and 1.5 (thresh < 0)."""
+    def box(shape, fill, edits=()):
+        b = np.full(shape, fill, np.float32)
+        for idx, v in edits:
+            b[idx] = v
+        return b
+    s, c = (64, 16, 64), (64, 64, 64)  # (D, H, W)
+    rng = np.random.default_rng(32)
+    noise = (rng.standard_normal(c) * 0.05 + 300.0).astype(np.float32)
+    boxes = [
+        box(s, 2.0, [((0, 0, 0), np.nan)]),                       # flat[0] NaN
+        box(s, 2.0, [((40, 9, 33), np.nan)]),                     # a later NaN never wins
+        box(s, 1.0, [((5, 3, 7), np.inf)]),
+        box(s, 1.0, [((50, 12, 60), -np.inf)]),
+        box(s, 0.0, [((9, 2, 40), 8.0), ((9, 2, 41), -8.0)]),     # +M / -M in one block
+        box(s, 0.0, [((3, 1, 2), -8.0), ((60, 14, 62), 8.0)]),    # first (negative) spike wins
+        box(s, 0.0, [((60, 14, 62), -8.0), ((3, 1, 2), 8.0)]),    # first (positive) spike wins
+        box(s, 0.0, [((7, 5, 9), np.float32(-0.0)), ((8, 5, 9), np.float32(-0.0))]),
+        box(s, 3.0),                                              # every LLL coefficient ties
+        box(s, np.float32(1e-40), [((30, 8, 30), np.float32(3e-39))]),
+        noise,
+        -noise,
+    ]
+    for keep in (0.5, KEEPS[1], 1.0, 1.5):
+        for dtype in (np.float32, np.float64):
+            got, kept = gpu_payloads(wc, ctx, [b.astype(dtype) for b in boxes], keep, dtype=dtype)
+            for i, b in enumerate(boxes):
+                want, wk = oracle.compress_payload(b, keep)
+                assert got[i] == want, (keep, dtype.__name__, i)
+                assert int(kept[i]) == wk
