@@ -86,6 +86,21 @@ __device__ __forceinline__ uint32_t wave_sum_u32_u(uint32_t v) {
 #endif
 }
 
+// Exclusive max over the lanes below this one (0 for lane 0): the inclusive
+// DPP max scan, then wave_shr:1 (a GFX9 whole-wave DPP shift).
+#ifndef WC_DPP_SHIFT
+#define WC_DPP_SHIFT 1
+#endif
+__device__ __forceinline__ uint32_t wave_excl_max_u32(uint32_t v) {
+    v = max(v, dpp_u32<0x111, 0xf>(v));
+    v = max(v, dpp_u32<0x112, 0xf>(v));
+    v = max(v, dpp_u32<0x114, 0xf>(v));
+    v = max(v, dpp_u32<0x118, 0xf>(v));
+    v = max(v, dpp_u32<0x142, 0xa>(v));
+    v = max(v, dpp_u32<0x143, 0xc>(v));
+    return dpp_u32<0x138, 0xf>(v);  // wave_shr:1
+}
+
 __device__ __forceinline__ unsigned long long dpp_u64_max_step(unsigned long long v, uint32_t lo, uint32_t hi) {
     const unsigned long long w = ((unsigned long long)hi << 32) | lo;
     return w > v ? w : v;

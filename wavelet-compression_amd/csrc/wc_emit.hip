@@ -23,6 +23,9 @@
 // Every spin is bounded (spin_fail) and raises kErrTimeout, never a hang.
 #include "wc_xform.h"
 
+#ifndef WC_EMIT_SB
+#define WC_EMIT_SB 2  // 256-element blocks whose pairs share one copy-out (stage: 256 * WC_EMIT_SB pairs per wave)
+#endif
 #ifndef WC_EMIT_FULL
 #define WC_EMIT_FULL 1  // full emit tiles skip the per-element range checks
 #endif
@@ -49,51 +52,66 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
 // prev: this wave's first pair index and the unit-relative flat index of the
 // last kept coefficient before this wave's elements (0xffffffff = none, so
 // that run = f).  32-bit arithmetic: flat indices are < 2^31.
-// The pairs of each 256-element block are first placed in this wave's
-// 256-entry LDS stage in rank order, then copied out with contiguous 8-B
-// stores (one full 512-B row per instruction instead of up to four sparse,
-// partial-line scatters).  A wave's LDS operations execute in order, so the
+// The pairs of every WC_EMIT_SB consecutive 256-element blocks are first
+// placed in this wave's LDS stage in rank order, then copied out with
+// contiguous 8-B stores (one full 512-B row per instruction instead of up to
+// four sparse, partial-line scatters; two blocks per copy-out fill the last
+// row of a copy better).  A wave's LDS operations execute in order, so the
 // stage needs no barrier.
 __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, uint32_t start, int w, int l,
                                            uint32_t rank, uint32_t prev, uint2* __restrict__ pairs, uint2* stage) {
     const unsigned long long lt = (1ull << l) - 1ull;
+    uint32_t soff = 0;  // pairs staged since the last copy-out
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
         const uint32_t nib = (kb >> (it * 4)) & 0xfu;
         const unsigned long long any = __ballot(nib != 0);
-        if (!any) continue;
-        // exclusive prefix of kept counts over lanes: one ballot per column j,
-        // counted below this lane with mbcnt (ballots live in SGPRs)
-        const unsigned long long b0 = __ballot(nib & 1u), b1 = __ballot(nib & 2u), b2 = __ballot(nib & 4u),
-                                 b3 = __ballot(nib & 8u);
-        const uint32_t pre = mbcnt64(b0) + mbcnt64(b1) + mbcnt64(b2) + mbcnt64(b3);
-        const uint32_t itot = (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
-        const uint32_t ebase = start + (uint32_t)(w * 2048 + it * 256 + l * 4);
-        const uint32_t lane_last = ebase + (nib ? 31u - (uint32_t)__clz(nib) : 0u);
-        const unsigned long long below = any & lt;
-        const uint32_t from_lane = __shfl(lane_last, below ? 63 - __clzll(below) : l);
-        uint32_t p = below ? from_lane : prev;
-        uint32_t r = pre;
-        if (nib) {
-            const float vv[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
+        if (any) {
+            // exclusive prefix of kept counts over lanes: one ballot per column j,
+            // counted below this lane with mbcnt (ballots live in SGPRs)
+            const unsigned long long b0 = __ballot(nib & 1u), b1 = __ballot(nib & 2u), b2 = __ballot(nib & 4u),
+                                     b3 = __ballot(nib & 8u);
+            const uint32_t pre = mbcnt64(b0) + mbcnt64(b1) + mbcnt64(b2) + mbcnt64(b3);
+            const uint32_t itot = (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
+            const uint32_t ebase = start + (uint32_t)(w * 2048 + it * 256 + l * 4);
+            const uint32_t lane_last = ebase + (nib ? 31u - (uint32_t)__clz(nib) : 0u);
+            const unsigned long long below = any & lt;
+#if WC_DPP_SHIFT
+            // last kept index of the nearest lower lane with a kept element:
+            // indices grow with the lane, so the exclusive max over the lanes
+            // below (lanes without one contribute 0)
+            const uint32_t from_lane = wave_excl_max_u32(nib ? lane_last : 0u);
+#else
+            const uint32_t from_lane = __shfl(lane_last, below ? 63 - __clzll(below) : l);
+#endif
+            uint32_t p = below ? from_lane : prev;
+            uint32_t r = soff + pre;
+            if (nib) {
+                const float vv[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (nib & (1u << j)) {
-                    const uint32_t f = ebase + (uint32_t)j;
-                    stage[r] = make_uint2(f - p - 1u, __float_as_uint(vv[j]));
-                    p = f;
-                    ++r;
+                for (int j = 0; j < 4; ++j) {
+                    if (nib & (1u << j)) {
+                        const uint32_t f = ebase + (uint32_t)j;
+                        stage[r] = make_uint2(f - p - 1u, __float_as_uint(vv[j]));
+                        p = f;
+                        ++r;
+                    }
                 }
             }
+            soff += itot;
+            prev = __builtin_amdgcn_readlane(lane_last, 63 - __clzll(any));  // uniform source lane
         }
-        __builtin_amdgcn_wave_barrier();
+        // copy-out every WC_EMIT_SB blocks of 256 elements (the stage holds their pairs)
+        if (it % WC_EMIT_SB == WC_EMIT_SB - 1 && soff) {
+            __builtin_amdgcn_wave_barrier();
 #ifdef WC_XP_E_NOSTORE
-        if (itot == 0x7fffffffu)
+            if (soff == 0x7fffffffu)
 #endif
-        for (uint32_t k = (uint32_t)l; k < itot; k += 64) pairs[rank + k] = stage[k];
-        __builtin_amdgcn_wave_barrier();
-        rank += itot;
-        prev = __builtin_amdgcn_readlane(lane_last, 63 - __clzll(any));  // uniform source lane
+            for (uint32_t k = (uint32_t)l; k < soff; k += 64) pairs[rank + k] = stage[k];
+            __builtin_amdgcn_wave_barrier();
+            rank += soff;
+            soff = 0;
+        }
     }
 }
 
@@ -239,7 +257,8 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
                     const bool in = l < take;
                     ecnt += wave_sum_u32_u(in ? (uint32_t)((v >> 31) & kMask31) : 0u);
                     const unsigned long long hasl = __ballot(in && (v & kMask31) != 0);
-                    const uint32_t hl = __shfl((uint32_t)(v & kMask31), hasl ? __ffsll((long long)hasl) - 1 : 0);
+                    const uint32_t hl = __builtin_amdgcn_readlane((uint32_t)(v & kMask31),
+                                                                  hasl ? __ffsll((long long)hasl) - 1 : 0);  // uniform lane
                     if (elast == 0 && hasl) elast = hl;
                 }
                 if (kI < kZ) break;
@@ -287,7 +306,7 @@ template <int EW>
 __global__ __launch_bounds__(EW * kWave, EW == 4 ? WC_EMIT_MINB : WC_EMIT_MINB8) void k_emit(EmitParams P,
                                                                            const float* __restrict__ coef) {
     __shared__ __attribute__((aligned(16))) uint32_t sm[32];
-    __shared__ uint2 stage_all[EW][256];  // per-wave pair stage (emit_pairs)
+    __shared__ uint2 stage_all[EW][256 * WC_EMIT_SB];  // per-wave pair stage (emit_pairs)
     const int tid = threadIdx.x;
     uint2* stage = stage_all[tid >> 6];
     const EmitDesc E = P.edesc[blockIdx.x];

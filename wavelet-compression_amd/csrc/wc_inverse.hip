@@ -251,7 +251,11 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDe
         const uint32_t phk = k < n ? min(sat_add(A, vr) - 1u, nc) : nc;
         const int32_t rhi = k <= n ? (int32_t)div_rows(phk, U.dmagic) : -1;
         // rhi of pair k - 1: lane l - 1, the carry in lane 0
+#if WC_DPP_SHIFT
+        const int32_t from = __builtin_amdgcn_update_dpp(0, rhi, 0x138, 0xf, 0xf, false);  // wave_shr:1
+#else
         const int32_t from = __builtin_amdgcn_ds_bpermute((l - 1) << 2, rhi);
+#endif
         const int32_t rlo = (l == 0 ? carry : from) + 1;
         const uint32_t cnt = (k <= n && rhi >= rlo) ? (uint32_t)(rhi - rlo + 1) : 0u;
 #ifdef WC_XP_NOROWS
