@@ -355,7 +355,7 @@ size_t rix_lds_bytes(const UnitDev& d) { return sizeof(float) * 4 * (size_t)rix_
 bool set_rix_tiling(UnitDev& d, int budget, int max_lx) {
     d.rix = 0;
     if (!d.fast || d.ncells == 0) return false;
-    auto floats = [&](int tx, int ty) { return (int64_t)4 * (tx * ((int64_t)ty * d.nz + 4) + 16); };
+    auto floats = [&](int tx, int ty) { return (int64_t)4 * rix_wr(ceil_log2(tx), ceil_log2(ty), d.nz); };
     int lx = std::min(max_lx, ceil_log2(d.hx));  // 16 blocks: 128-B output rows; the rest of the budget to TY
     while (lx > 0 && floats(1 << lx, 1) > budget) --lx;
     if (floats(1 << lx, 1) > budget) return false;

@@ -68,8 +68,14 @@ struct RTile {
 
 // LDS layout of a K6r tile: 4 wave regions of TX ranges of RS = TY*D + 4
 // floats, regions 16 floats apart (bank offset), 16-B aligned.
-__host__ __device__ inline int rix_rs(int lby, int D) { return (D << lby) + 4; }
-__host__ __device__ inline int rix_wr(int lbx, int lby, int D) { return (rix_rs(lby, D) << lbx) + 16; }
+#ifndef WC_RIX_RSPAD
+#define WC_RIX_RSPAD 4   // floats between ranges (bank offset)
+#endif
+#ifndef WC_RIX_WRPAD
+#define WC_RIX_WRPAD 16  // floats between wave regions
+#endif
+__host__ __device__ inline int rix_rs(int lby, int D) { return (D << lby) + WC_RIX_RSPAD; }
+__host__ __device__ inline int rix_wr(int lbx, int lby, int D) { return (rix_rs(lby, D) << lbx) + WC_RIX_WRPAD; }
 
 // A flat tile: kFlatTile consecutive coefficients (flat order) of one unit.
 struct FTile {

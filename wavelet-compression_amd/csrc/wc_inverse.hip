@@ -766,7 +766,10 @@ __device__ __forceinline__ void synth_block(const float (&c)[2][2][2], float (&V
 // sum goes to part[4 * tile + wave] and k_rmse_rows_final sums a unit's in
 // order.  A pass of its own keeps the synthesis' registers untouched.
 template <int OT>
-__global__ __launch_bounds__(kThreads, 4) void k_inverse_rows(const RTile* __restrict__ tiles, uint32_t ntiles,
+#ifndef WC_RIX_MINW
+#define WC_RIX_MINW 4  // K6r: waves per SIMD the register budget is sized for (4-wave blocks: workgroups per CU)
+#endif
+__global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RTile* __restrict__ tiles, uint32_t ntiles,
                                                          const uint8_t* __restrict__ payload,
                                                          const uint64_t* __restrict__ offsets,
                                                          const uint2* __restrict__ rowinfo, float* __restrict__ out,
