@@ -90,6 +90,7 @@ struct Plan {
     size_t lds_rows = 0;
     bool any_sparse = false;
     uint64_t coef_extent = 0;  // floats of staged coefficient scratch
+    uint64_t flag_bytes = 0;   // bytes of sparse-staging segment flags (UnitDev::flag_off ranges + slack)
     size_t lds_gen = 0, lds_fast = 0, lds_inverse = 0;
     size_t state_bytes = 0;    // forward per-call state: 16 | key[n] | tickets[n] | status[netiles]
     DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_edesc, d_ixtiles, d_rtiles, d_rdtiles;
@@ -337,6 +338,7 @@ void build_etiles(Plan& P, int n) {
                     e.nz = d.nz;
                     e.sparse = d.sparse;
                     e.lbz = d.lbz;
+                    e.flag_off = (uint32_t)d.flag_off;
                     P.edesc.push_back(e);
                 }
         }
@@ -430,7 +432,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     P.rtiles.clear();
     P.rowinfo_entries = 0;
     std::vector<XTile> gen, fast;
-    uint64_t coef_cursor = 0, pay_cursor = 4;
+    uint64_t coef_cursor = 0, pay_cursor = 4, flag_cursor = 0;
     for (int i = 0; i < n; ++i) {
         const wc_unit& u = units[i];
         UnitDev& d = P.units[i];
@@ -460,6 +462,11 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         // Sparse staging (wc_xform.h xform_fast_p2_sparse): z tiles of >= 16
         // blocks whose flat segments of TZ coefficients each belong to one tile.
         d.sparse = (d.fast && d.lbz >= kSegShift && d.hz % (1 << d.lbz) == 0) ? 1u : 0u;
+        if (d.sparse) {  // flag range: whole 2048-coefficient blocks (flag_pos), 8-B aligned
+            d.flag_off = flag_cursor;
+            flag_cursor += round_up(d.ncells, 2048) >> d.lbz;
+            if (flag_cursor >= (uint64_t(1) << 32)) d.sparse = 0;  // EmitDesc keeps 32 bits: stage densely
+        }
         P.any_sparse |= d.sparse != 0;
         d.xt_begin = (uint32_t)before;  // rebased below for fast units
         if (d.fast)
@@ -591,6 +598,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         }
     }
     P.coef_extent = coef_cursor ? coef_cursor + kFlatTile : 0;  // slack: flat tiles read whole float4 groups
+    P.flag_bytes = flag_cursor + kEmitTileBig;                  // slack: a partial last tile's flag loads
     build_etiles(P, n);
     int rc;
     if ((rc = upload(c, P.d_units, P.units.data(), sizeof(UnitDev) * P.units.size(), "upload units")) ||
@@ -637,7 +645,7 @@ int ensure_scratch(wc_ctx* c) {
     const size_t nft = P.ftiles.size();
     int rc;
     if ((rc = ensure(c, c->coef, sizeof(float) * std::max<uint64_t>(P.coef_extent, 1))) ||
-        (rc = ensure(c, c->flags, (P.coef_extent >> kSegShift) + kEmitTileBig)) ||
+        (rc = ensure(c, c->flags, P.flag_bytes)) ||
         (rc = ensure(c, c->part, sizeof(double) * std::max<size_t>(nft, 4 * P.rtiles.size()))) ||
         (rc = ensure(c, c->rowinfo, sizeof(uint32_t) * 2 * std::max<uint64_t>(P.rowinfo_entries, 1))) ||
         (rc = ensure_zeroed(c, c->istate, istate_bytes(P))) ||

@@ -182,11 +182,18 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
     uint32_t segf = 0xffu;  // bit it: group it may hold kept coefficients
     if (sparse) {
         // one flag byte per segment of TZ = 2^lbz coefficients (16 or 32)
-        const uint8_t* fl = P.flags + (U.coef_off >> kSegShift) + (((uint64_t)index * kTile) >> U.lbz);
+        const uint8_t* fl = P.flags + U.flag_off + (((uint64_t)index * kTile) >> U.lbz);
         const int sh = U.lbz;
+#if WC_FLAG_PERM
+        // this thread's 8 flags in 8 consecutive bytes (flag_pos): bytes 0 / 1
+        const uint2 f8 = *reinterpret_cast<const uint2*>(fl + ((uint32_t)w << (11 - sh)) + ((((uint32_t)l << 2) >> sh) << 3));
+        segf = (f8.x & 1u) | ((f8.x >> 7) & 2u) | ((f8.x >> 14) & 4u) | ((f8.x >> 21) & 8u) | ((f8.y & 1u) << 4) |
+               ((f8.y >> 3) & 0x20u) | ((f8.y >> 10) & 0x40u) | ((f8.y >> 17) & 0x80u);
+#else
         segf = 0;
 #pragma unroll
         for (int it = 0; it < 8; ++it) segf |= (uint32_t)(fl[(w * 2048 + it * 256 + 4 * l) >> sh] != 0) << it;
+#endif
     }
     // the unit key: a finished earlier launch wrote it, one uniform load
     const float tf = unit_thresh(P, P.key[u]);

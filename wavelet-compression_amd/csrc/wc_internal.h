@@ -20,7 +20,7 @@ constexpr int kFlatPerThread = kFlatTile / kThreads;  // 16 = 4 x float4
 // pass-through "tail" block at b = n/2.
 struct UnitDev {
     uint64_t cell_off;   // element offset of the unit's cells
-    uint64_t coef_off;   // element offset in the flat coefficient scratch (128-B aligned)
+    uint64_t coef_off;   // element offset in the flat coefficient scratch (512-B aligned)
     uint64_t ncells;     // W*H*D
     int32_t nx, ny, nz;  // W, H, D
     int32_t hx, hy, hz;  // n/2 per axis (number of pairs)
@@ -45,6 +45,7 @@ struct UnitDev {
     uint32_t rt_begin;      // first K6r tile of the unit (row-indexed units)
     uint32_t nrt;           // K6r tiles of the unit
     uint64_t dmagic;        // m | (31 + l) << 32: row = floor(position / D) = (position * m) >> (31 + l)
+    uint64_t flag_off;      // sparse units: byte offset of the segment flags (whole 2048-coefficient blocks, flag_pos)
 };
 
 // A transform tile: a (1<<lbx) x (1<<lby) x (1<<lbz) box of 2x2x2 blocks.
@@ -113,7 +114,7 @@ struct EmitDesc {
     int32_t nx, ny, nz;
     uint32_t sparse;    // UnitDev::sparse
     int32_t lbz;        // log2 of the staged segment length (UnitDev::lbz)
-    uint32_t pad;
+    uint32_t flag_off;  // UnitDev::flag_off (the plan keeps every flag range below 4 GiB)
 };
 
 struct EmitParams {
@@ -135,6 +136,27 @@ struct EmitParams {
 };
 
 constexpr int kSegShift = 4;    // sparse staging: flag index space of 16 coefficients per byte (min segment)
+#ifndef WC_FLAG_PERM
+#define WC_FLAG_PERM 1
+#endif
+// Byte position of sparse-staging segment s (= flat index >> sh, sh = log2 of
+// the segment length, 4 or 5) in its unit's flag range.  WC_FLAG_PERM: within
+// each 2048-coefficient block of a unit (one emit wave's share of a tile) the
+// 8 flags one emit thread reads (element groups it = 0..7: segment it * G + g,
+// G = 256 >> sh, g = its lane group) sit in 8 consecutive bytes, g * 8 + it:
+// one 8-B load instead of eight byte loads (wc_emit.hip).  Each sparse unit's
+// flag range (UnitDev::flag_off) is 8-B aligned and spans whole blocks, so
+// permuted positions never leave it.
+__host__ __device__ inline uint64_t flag_pos(uint64_t s, int sh) {
+#if WC_FLAG_PERM
+    const int lb = 11 - sh, lg = 8 - sh;
+    const uint64_t sw = s & ((1ull << lb) - 1);
+    return (s & ~((1ull << lb) - 1)) | ((sw & ((1ull << lg) - 1)) << 3) | (sw >> lg);
+#else
+    (void)sh;
+    return s;
+#endif
+}
 #ifndef WC_RIX_TILE
 #define WC_RIX_TILE 4096
 #endif

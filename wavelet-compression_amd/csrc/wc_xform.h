@@ -373,7 +373,7 @@ __device__ __forceinline__ unsigned long long xform_fast_p2(const UnitDev& U, co
 // thresh < 0 keeps everything); the others flag their unit (spos), so only a
 // unit with a negative max AND a sparsely staged tile needs the re-staging
 // fallback.  Flag byte of segment s of a unit: (coef_off >> 4) + s,
-// inside the unit's 16-coefficient index range (coef_off is a multiple of 32).  With m = the tile's max |c| (from phase 1), bound = m * (1 - keep)
+// inside the unit's 16-coefficient index range (UnitDev::flag_off; byte order: flag_pos).  With m = the tile's max |c| (from phase 1), bound = m * (1 - keep)
 // (fp64, as src/compressor.cpp:216) is <= the unit's thresh whenever
 // thresh >= 0 (|tile max| <= |unit max|), so a segment with no |c| > bound
 // holds no kept coefficient.  A NaN in the tile, or a bound that is not >= 0,
@@ -425,7 +425,7 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
         // bound < 0 (dense tile): every segment, all-NaN ones included
         const bool flag = ((__ballot(cand) >> g0) & gmask) != 0 || !(bound >= 0.0);
         if (flag) st(f, v);
-        if ((tid & (glanes - 1)) == 0) flags[(U.coef_off >> kSegShift) + ((uint64_t)f >> lbz)] = flag ? 1 : 0;
+        if ((tid & (glanes - 1)) == 0) flags[U.flag_off + flag_pos((uint64_t)f >> lbz, lbz)] = flag ? 1 : 0;
         const uint32_t f0 = (uint32_t)f;
         unsigned long long k = coef_key(v.x, f0);
         kmax = k > kmax ? k : kmax;
@@ -473,7 +473,7 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse_s32(const Uni
         const bool cand = fabsf(v.x) > bf || fabsf(v.y) > bf || fabsf(v.z) > bf || fabsf(v.w) > bf;
         const bool flag = ((__ballot(cand) >> g0) & 0xffull) != 0 || dense;
         if (flag) *reinterpret_cast<float4*>(dst + f) = v;
-        if ((tid & 7) == 0) flags[(U.coef_off >> kSegShift) + ((uint64_t)f >> lbz)] = flag ? 1 : 0;
+        if ((tid & 7) == 0) flags[U.flag_off + flag_pos((uint64_t)f >> lbz, lbz)] = flag ? 1 : 0;
         const uint32_t f0 = (uint32_t)f;
         const float e[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
