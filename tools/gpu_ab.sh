@@ -1,32 +1,19 @@
 #!/bin/bash
-# A/B of library variants (tools/variants/<name>/, "default" = the in-tree lib)
-# over the wc_bench shapes, after the -m gpu suite; optional PMC passes.
-# usage: tools/gpu_ab.sh [--no-tests] [--pmc COUNTER] variant...
-S="tools/bin/wc_bench"
-tests=1; pmc=""
-while [ $# -gt 0 ]; do
-  case "$1" in
-    --no-tests) tests=0; shift;;
-    --pmc) pmc="$2"; shift 2;;
-    *) break;;
-  esac
-done
+# Generic A/B of libwavelet_amd.so variants (tools/build_variants.sh) on wc_bench:
+#   VARIANTS='a b'  variants besides the default build, REPS (2), INV (0 forward
+#   only, 1 + inverse, 2 + fused inverse/RMSE), TESTS=1 runs -m gpu first,
+#   SHAPES (default 'c2 c5 f32').  tools/ab_report.py gpurun_out summarises.
+S=tools/bin/wc_bench
+declare -A ARGS=([c2]="1024 64 f64 0.999" [c5]="512 128 f32 0.9999" [f32]="1024 64 f32 0.999" [s32]="4096 32 f64 0.999" [s16]="16384 16 f64 0.999")
 steps=()
-[ $tests = 1 ] && steps+=("tests:300:python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread")
-for rep in 1 2; do
-  for v in "$@"; do
+[ "${TESTS:-0}" = 1 ] && steps+=("tests:400:python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread")
+steps+=("chk_c2:90:$S 1024 64 f64 0.999 3 1 ${INV:-0} 1" "chk_c5:90:$S 64 128 f32 0.9999 3 1 ${INV:-0} 1")
+for rep in $(seq 1 ${REPS:-2}); do
+  for v in default ${VARIANTS}; do
     if [ $v = default ]; then lp=""; else lp="LD_LIBRARY_PATH=tools/variants/$v"; fi
-    [ $rep = 1 ] && steps+=("ab_${v}_c2chk:60:$lp $S 1024 64 f64 0.999 5 2 1 1 1 1 1")
-    steps+=("ab_${v}_c2_$rep:60:$lp $S 1024 64 f64 0.999 20 3 1 0 1 1 1")
-    steps+=("ab_${v}_c5_$rep:60:$lp $S 64 128 f32 0.9999 20 3 1 0 1 1 1")
-    steps+=("ab_${v}_s32_$rep:60:$lp $S 8192 32 f64 0.999 20 3 1 0 1 1 1")
-    steps+=("ab_${v}_s16_$rep:60:$lp $S 32768 16 f64 0.999 20 3 1 0 1 1 1")
+    for s in ${SHAPES:-c2 c5 f32}; do
+      steps+=("ab_${v}_${s}_$rep:90:$lp $S ${ARGS[$s]} 10 2 ${INV:-0} 0")
+    done
   done
 done
-if [ -n "$pmc" ]; then
-  for v in "$@"; do
-    if [ $v = default ]; then lp=""; else lp="LD_LIBRARY_PATH=tools/variants/$v"; fi
-    steps+=("pmc_${v}:90:$lp rocprofv3 --pmc $pmc --output-format csv -d gpurun_out/pmc_ab -o $v -- $S 1024 64 f64 0.999 3 1 1 0 1 1 1")
-  done
-fi
 exec tools/gpu_run.sh "${steps[@]}"
