@@ -29,6 +29,9 @@
 #ifndef WC_EMIT_FULL
 #define WC_EMIT_FULL 1  // full emit tiles skip the per-element range checks
 #endif
+#ifndef WC_EMIT_KEYPAR
+#define WC_EMIT_KEYPAR 1  // the unit key loads beside the flags (bit 0: 4-wave launch, bit 1: 8-wave: +11 VGPRs there)
+#endif
 
 namespace wc {
 
@@ -179,6 +182,14 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
     const int w = tid >> 6, l = tid & 63;
     // Sparse staging: this thread's 8 segment flags, loaded before the key.
     const bool sparse = P.flags && U.sparse;
+    constexpr bool kKeyPar = (WC_EMIT_KEYPAR >> (EW == 4 ? 0 : 1)) & 1;
+    // The key's scalar load is issued with the flag load, and the threshold is
+    // needed only by the keep test: the chain before the coefficient loads is
+    // descriptor -> flags (not descriptor -> flags -> key).  A unit whose
+    // thresh is < 0 (densely re-staged, k_transform_fallback) loads the
+    // segments its flags skipped once the threshold is known (rare).
+    unsigned long long ukey = 0;
+    if constexpr (kKeyPar) ukey = P.key[u];
     uint32_t segf = 0xffu;  // bit it: group it may hold kept coefficients
     if (sparse) {
         // one flag byte per segment of TZ = 2^lbz coefficients (16 or 32)
@@ -196,7 +207,8 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
 #endif
     }
     // the unit key: a finished earlier launch wrote it, one uniform load
-    const float tf = unit_thresh(P, P.key[u]);
+    float tf = 0.0f;
+    if constexpr (!kKeyPar) tf = unit_thresh(P, P.key[u]);
     const uint32_t start = index * kTile;
     const uint32_t len = (uint32_t)min((uint64_t)kTile, U.ncells - start);
 
@@ -205,19 +217,36 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
     // with thresh >= 0 skip unflagged segments (never stored); thresh < 0
     // units were re-staged densely (k_transform_fallback).
     const float4* __restrict__ p4 = reinterpret_cast<const float4*>(coef + U.coef_off + start);
-    if (!(tf >= 0.0f)) segf = 0xffu;
+    if constexpr (!kKeyPar)
+        if (!(tf >= 0.0f)) segf = 0xffu;
     float4 q[8];
     uint32_t kb;
     if (WC_EMIT_FULL && len == kTile) {  // uniform: a full tile, no range checks
 #pragma unroll
         for (int it = 0; it < 8; ++it)
             q[it] = ((segf >> it) & 1u) ? p4[w * 512 + it * 64 + l] : make_float4(0, 0, 0, 0);
+        if constexpr (kKeyPar) {
+            tf = unit_thresh(P, ukey);
+            if (!(tf >= 0.0f) && sparse) {  // uniform: the densely re-staged unit, every segment
+#pragma unroll
+                for (int it = 0; it < 8; ++it) q[it] = p4[w * 512 + it * 64 + l];
+            }
+        }
         kb = keep_bits_full(q, tf);
     } else {
 #pragma unroll
         for (int it = 0; it < 8; ++it)
             q[it] = ((segf >> it) & 1u) && (uint32_t)(w * 2048 + it * 256 + 4 * l) < len ? p4[w * 512 + it * 64 + l]
                                                                                           : make_float4(0, 0, 0, 0);
+        if constexpr (kKeyPar) {
+            tf = unit_thresh(P, ukey);
+            if (!(tf >= 0.0f) && sparse) {
+#pragma unroll
+                for (int it = 0; it < 8; ++it)
+                    q[it] = (uint32_t)(w * 2048 + it * 256 + 4 * l) < len ? p4[w * 512 + it * 64 + l]
+                                                                          : make_float4(0, 0, 0, 0);
+            }
+        }
         kb = keep_bits(q, tf, len, w, l);
     }
     uint32_t wcnt, wlast;
