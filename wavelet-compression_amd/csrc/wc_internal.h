@@ -157,6 +157,17 @@ __host__ __device__ inline uint64_t flag_pos(uint64_t s, int sh) {
     return s;
 #endif
 }
+// flag_pos on 32-bit segment indices (K1's S32 form: units of < 2^30 cells).
+__host__ __device__ inline uint32_t flag_pos32(uint32_t s, int sh) {
+#if WC_FLAG_PERM
+    const int lb = 11 - sh, lg = 8 - sh;
+    const uint32_t sw = s & ((1u << lb) - 1);
+    return (s & ~((1u << lb) - 1)) | ((sw & ((1u << lg) - 1)) << 3) | (sw >> lg);
+#else
+    (void)sh;
+    return s;
+#endif
+}
 #ifndef WC_RIX_TILE
 #define WC_RIX_TILE 4096
 #endif

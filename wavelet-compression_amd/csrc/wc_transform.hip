@@ -74,7 +74,7 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
             // mag >> 1: the tile's largest |c| bits (NaN patterns above +inf's)
             const unsigned long long kmax =
                 s32 ? xform_fast_p2_sparse_s32(U, td, lds, threadIdx.x, bound, mag >> 1, flags, dst)
-                    : xform_fast_p2_sparse(U, td, lds, threadIdx.x, bound, flags,
+                    : xform_fast_p2_sparse(U, td, lds, threadIdx.x, bound, mag >> 1, flags,
                                            [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
             block_key_max(kmax, s_key, unit_key + td.unit);
             return;

@@ -380,7 +380,8 @@ __device__ __forceinline__ unsigned long long xform_fast_p2(const UnitDev& U, co
 // flags every segment.  Units whose thresh turns out < 0 (negative signed
 // max: everything kept) are re-staged densely by k_transform_fallback.
 __device__ __forceinline__ bool s32_ok(const UnitDev& U) {
-    return U.lbx == 5 && U.lby == 0 && U.lbz == 5 && ((U.hx | U.hz) & 31) == 0 && (U.cell_off & 1) == 0;
+    return U.lbx == 5 && U.lby == 0 && U.lbz == 5 && ((U.hx | U.hz) & 31) == 0 && (U.cell_off & 1) == 0 &&
+           U.ncells < (1ull << 30);  // 32-bit byte offsets of the flat coefficients
 }
 
 __device__ __forceinline__ double sparse_bound(uint32_t magkey, double keep) {
@@ -390,13 +391,40 @@ __device__ __forceinline__ double sparse_bound(uint32_t magkey, double keep) {
     return b >= 0.0 ? b : -1.0;
 }
 
+// Branch-free max key (WC_K1_BFKEY): with amax = the tile's largest |c| bits
+// and no NaN in the tile, only coefficients with |c| bits == amax can carry
+// the tile's max key, and among those coef_key orders by the low word alone
+// ((0x7fffffff - f) << 1 | sign: smallest flat index first).  So each
+// coefficient costs a compare and a select into one 32-bit running max
+// (`best`, 0 = none) instead of a branch around a 64-bit key; the key is
+// (amax << 32) | best.  A tile holding a NaN (amax > +inf's bits) takes the
+// per-coefficient coef_key pass instead (kKeyNaNFirst at flat index 0).
+#ifndef WC_K1_BFKEY
+#define WC_K1_BFKEY 1
+#endif
+#ifndef WC_K1_IDX32
+#define WC_K1_IDX32 1  // S32 phase 2: 32-bit flat indices with uniform per-row steps
+#endif
+__device__ __forceinline__ uint32_t key_lo_max(uint32_t best, float c, uint32_t f, uint32_t amax) {
+    const uint32_t bits = __float_as_uint(c);
+    const uint32_t lo = ((0x7fffffffu - f) << 1) | (bits >> 31);
+    return (bits & 0x7fffffffu) == amax ? max(best, lo) : best;
+}
+
+__device__ __forceinline__ unsigned long long key_from_lo(uint32_t amax, uint32_t best) {
+    return best ? ((unsigned long long)amax << 32) | best : 0ull;
+}
+
 // Phase 2 with sparse staging: stores only segments with some |c| > bound,
 // writes EVERY segment's flag byte (the emit skips the others' loads), and
 // returns this thread's max key over all its coefficients.
 template <class Store4>
 __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev& U, const XTile& td,
                                                                    const float* lds, int tid, double bound,
-                                                                   uint8_t* __restrict__ flags, Store4 st) {
+                                                                   uint32_t amax, uint8_t* __restrict__ flags,
+                                                                   Store4 st) {
+    const bool bf = WC_K1_BFKEY && amax <= 0x7f800000u;  // uniform: no NaN in the tile
+    uint32_t best = 0;
     const int H = U.ny, D = U.nz;
     const int hx = U.hx, hy = U.hy, hz = U.hz;
     const int lbx = U.lbx, lby = U.lby, lbz = U.lbz;
@@ -427,6 +455,13 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
         if (flag) st(f, v);
         if ((tid & (glanes - 1)) == 0) flags[U.flag_off + flag_pos((uint64_t)f >> lbz, lbz)] = flag ? 1 : 0;
         const uint32_t f0 = (uint32_t)f;
+        if (bf) {
+            best = key_lo_max(best, v.x, f0, amax);
+            best = key_lo_max(best, v.y, f0 + 1, amax);
+            best = key_lo_max(best, v.z, f0 + 2, amax);
+            best = key_lo_max(best, v.w, f0 + 3, amax);
+            continue;
+        }
         unsigned long long k = coef_key(v.x, f0);
         kmax = k > kmax ? k : kmax;
         k = coef_key(v.y, f0 + 1);
@@ -436,7 +471,7 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
         k = coef_key(v.w, f0 + 3);
         kmax = k > kmax ? k : kmax;
     }
-    return kmax;
+    return bf ? key_from_lo(amax, best) : kmax;
 }
 
 // xform_fast_p2_sparse for the S32 shape (s32_ok), in fewer instructions:
@@ -463,19 +498,41 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse_s32(const Uni
     const float bf = thresh_as_float(bound);
     const bool allkeys = amax > 0x7f800000u;  // a NaN in the tile: every key as in the generic form
     unsigned long long kmax = 0;
+    uint32_t best = 0;  // WC_K1_BFKEY running low word
+#if WC_K1_IDX32
+    // 32-bit unit-relative indices (s32_ok: < 2^30 cells): row r0 + 16 it has
+    // flat index fb + (it & 1) 16 H D + ssx hx H D + ssy hy D, uniform steps;
+    // stores through the uniform bases with 32-bit offsets.
+    const uint32_t HD = (uint32_t)H * (uint32_t)D;
+    const uint32_t fb = ((uint32_t)(td.bx0 + r0) * (uint32_t)H + td.by0) * (uint32_t)D + (uint32_t)K;
+    const uint32_t dA = 16u * HD, dB = (uint32_t)hx * HD, dC = (uint32_t)hy * (uint32_t)D;
+    uint8_t* __restrict__ fl = flags + U.flag_off;
+    char* __restrict__ dstb = reinterpret_cast<char*>(dst);
+#endif
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
         const int row = r0 + 16 * it;  // row_of with lbx 5, lby 0: bxl, ssx, ssy
-        const int bxl = row & 31, ssx = (row >> 5) & 1, ssy = row >> 6;
-        const int I = td.bx0 + bxl + ssx * hx, J = (int)td.by0 + ssy * hy;
-        const int64_t f = ((int64_t)I * H + J) * D + K;
         const float4 v = *reinterpret_cast<const float4*>(lds + row * rstride + col);
         const bool cand = fabsf(v.x) > bf || fabsf(v.y) > bf || fabsf(v.z) > bf || fabsf(v.w) > bf;
         const bool flag = ((__ballot(cand) >> g0) & 0xffull) != 0 || dense;
+#if WC_K1_IDX32
+        const uint32_t f0 = fb + ((it & 1) ? dA : 0u) + (((it >> 1) & 1) ? dB : 0u) + ((it >> 2) ? dC : 0u);
+        if (flag) *reinterpret_cast<float4*>(dstb + (f0 << 2)) = v;
+        if ((tid & 7) == 0) fl[flag_pos32(f0 >> lbz, lbz)] = flag ? 1 : 0;
+#else
+        const int bxl = row & 31, ssx = (row >> 5) & 1, ssy = row >> 6;
+        const int I = td.bx0 + bxl + ssx * hx, J = (int)td.by0 + ssy * hy;
+        const int64_t f = ((int64_t)I * H + J) * D + K;
         if (flag) *reinterpret_cast<float4*>(dst + f) = v;
         if ((tid & 7) == 0) flags[U.flag_off + flag_pos((uint64_t)f >> lbz, lbz)] = flag ? 1 : 0;
         const uint32_t f0 = (uint32_t)f;
+#endif
         const float e[4] = {v.x, v.y, v.z, v.w};
+#if WC_K1_BFKEY
+        (void)allkeys;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) best = key_lo_max(best, e[j], f0 + (uint32_t)j, amax);
+#else
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t ab = __float_as_uint(e[j]) & 0x7fffffffu;
@@ -484,7 +541,26 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse_s32(const Uni
                 kmax = k > kmax ? k : kmax;
             }
         }
+#endif
     }
+#if WC_K1_BFKEY
+    if (!allkeys) return key_from_lo(amax, best);
+    // a NaN in the tile (rare): every coefficient's key, as the generic form
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+        const int row = r0 + 16 * it;
+        const int bxl = row & 31, ssx = (row >> 5) & 1, ssy = row >> 6;
+        const int I = td.bx0 + bxl + ssx * hx, J = (int)td.by0 + ssy * hy;
+        const uint32_t f0 = (uint32_t)(((int64_t)I * H + J) * D + K);
+        const float4 v = *reinterpret_cast<const float4*>(lds + row * rstride + col);
+        const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const unsigned long long k = coef_key(e[j], f0 + (uint32_t)j);
+            kmax = k > kmax ? k : kmax;
+        }
+    }
+#endif
     return kmax;
 }
 
