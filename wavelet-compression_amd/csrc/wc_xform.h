@@ -402,6 +402,9 @@ __device__ __forceinline__ double sparse_bound(uint32_t magkey, double keep) {
 #ifndef WC_K1_BFKEY
 #define WC_K1_BFKEY 1
 #endif
+#ifndef WC_K1_HITSKIP
+#define WC_K1_HITSKIP 1  // S32 phase 2: key work only in waves holding the tile max
+#endif
 #ifndef WC_K1_IDX32
 #define WC_K1_IDX32 1  // S32 phase 2: 32-bit flat indices with uniform per-row steps
 #endif
@@ -513,7 +516,9 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse_s32(const Uni
     for (int it = 0; it < 8; ++it) {
         const int row = r0 + 16 * it;  // row_of with lbx 5, lby 0: bxl, ssx, ssy
         const float4 v = *reinterpret_cast<const float4*>(lds + row * rstride + col);
-        const bool cand = fabsf(v.x) > bf || fabsf(v.y) > bf || fabsf(v.z) > bf || fabsf(v.w) > bf;
+        // largest |c| of the four (NaNs ignored, as the per-element compares)
+        const float m4 = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+        const bool cand = m4 > bf;
         const bool flag = ((__ballot(cand) >> g0) & 0xffull) != 0 || dense;
 #if WC_K1_IDX32
         const uint32_t f0 = fb + ((it & 1) ? dA : 0u) + (((it >> 1) & 1) ? dB : 0u) + ((it >> 2) ? dC : 0u);
@@ -530,8 +535,12 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse_s32(const Uni
         const float e[4] = {v.x, v.y, v.z, v.w};
 #if WC_K1_BFKEY
         (void)allkeys;
+        // only a wave with a lane holding the tile's largest |c| can raise the
+        // key (no NaN here: allkeys tiles redo every key below)
+        if (!WC_K1_HITSKIP || __ballot(__float_as_uint(m4) == amax)) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) best = key_lo_max(best, e[j], f0 + (uint32_t)j, amax);
+            for (int j = 0; j < 4; ++j) best = key_lo_max(best, e[j], f0 + (uint32_t)j, amax);
+        }
 #else
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
