@@ -29,6 +29,9 @@
 #ifndef WC_EMIT_FULL
 #define WC_EMIT_FULL 1  // full emit tiles skip the per-element range checks
 #endif
+#ifndef WC_EMIT_RUNLATE
+#define WC_EMIT_RUNLATE 1  // pairs staged as (flat index, value); runs taken at the copy-out (no per-block scan)
+#endif
 #ifndef WC_EMIT_KEYPAR
 #define WC_EMIT_KEYPAR 1  // the unit key loads beside the flags (bit 0: 4-wave launch, bit 1: 8-wave: +11 VGPRs there)
 #endif
@@ -51,7 +54,8 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
 
 // Emit the kept coefficients of one kEmitTile chunk held in q (thread (w, l)
 // owns elements w*2048 + it*256 + 4l + j; kb bit it*4 + j = kept) as (run,
-// value) pairs: ranks from per-column ballots, run = f - prev - 1.  rank /
+// value) pairs: ranks from per-column ballots, run = f - prev - 1 (taken at
+// the copy-out from the staged indices, WC_EMIT_RUNLATE).  rank /
 // prev: this wave's first pair index and the unit-relative flat index of the
 // last kept coefficient before this wave's elements (0xffffffff = none, so
 // that run = f).  32-bit arithmetic: flat indices are < 2^31.
@@ -63,8 +67,10 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
 // stage needs no barrier.
 __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, uint32_t start, int w, int l,
                                            uint32_t rank, uint32_t prev, uint2* __restrict__ pairs, uint2* stage) {
-    const unsigned long long lt = (1ull << l) - 1ull;
     uint32_t soff = 0;  // pairs staged since the last copy-out
+#if !WC_EMIT_RUNLATE
+    const unsigned long long lt = (1ull << l) - 1ull;
+#endif
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
         const uint32_t nib = (kb >> (it * 4)) & 0xfu;
@@ -77,18 +83,23 @@ __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, ui
             const uint32_t pre = mbcnt64(b0) + mbcnt64(b1) + mbcnt64(b2) + mbcnt64(b3);
             const uint32_t itot = (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
             const uint32_t ebase = start + (uint32_t)(w * 2048 + it * 256 + l * 4);
+            uint32_t r = soff + pre;
+#if WC_EMIT_RUNLATE
+            // staged as (flat index, value); runs are taken at the copy-out
+            if (nib) {
+                const float vv[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (nib & (1u << j)) stage[r++] = make_uint2(ebase + (uint32_t)j, __float_as_uint(vv[j]));
+            }
+#else
             const uint32_t lane_last = ebase + (nib ? 31u - (uint32_t)__clz(nib) : 0u);
             const unsigned long long below = any & lt;
-#if WC_DPP_SHIFT
             // last kept index of the nearest lower lane with a kept element:
             // indices grow with the lane, so the exclusive max over the lanes
             // below (lanes without one contribute 0)
             const uint32_t from_lane = wave_excl_max_u32(nib ? lane_last : 0u);
-#else
-            const uint32_t from_lane = __shfl(lane_last, below ? 63 - __clzll(below) : l);
-#endif
             uint32_t p = below ? from_lane : prev;
-            uint32_t r = soff + pre;
             if (nib) {
                 const float vv[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
 #pragma unroll
@@ -101,8 +112,9 @@ __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, ui
                     }
                 }
             }
-            soff += itot;
             prev = __builtin_amdgcn_readlane(lane_last, 63 - __clzll(any));  // uniform source lane
+#endif
+            soff += itot;
         }
         // copy-out every WC_EMIT_SB blocks of 256 elements (the stage holds their pairs)
         if (it % WC_EMIT_SB == WC_EMIT_SB - 1 && soff) {
@@ -110,7 +122,26 @@ __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, ui
 #ifdef WC_XP_E_NOSTORE
             if (soff == 0x7fffffffu)
 #endif
+#if WC_EMIT_RUNLATE
+            {
+                // run = f - (previous pair's f) - 1: the previous pair is lane
+                // l - 1's (a whole-wave DPP shift), for lane 0 the carry (the
+                // last pair of the previous round, or prev)
+                uint32_t carry = prev;
+                uint2 e = make_uint2(0u, 0u);
+                for (uint32_t k0 = 0; k0 < soff; k0 += 64) {  // uniform rounds, every lane active
+                    const uint32_t k = k0 + (uint32_t)l;
+                    e = k < soff ? stage[k] : make_uint2(0u, 0u);
+                    const uint32_t left = dpp_u32<0x138, 0xf>(e.x);  // wave_shr:1
+                    const uint32_t pf = l == 0 ? carry : left;
+                    if (k < soff) pairs[rank + k] = make_uint2(e.x - pf - 1u, e.y);
+                    carry = __builtin_amdgcn_readlane(e.x, 63);
+                }
+                prev = __builtin_amdgcn_readlane(e.x, (soff - 1u) & 63u);  // the last pair's index
+            }
+#else
             for (uint32_t k = (uint32_t)l; k < soff; k += 64) pairs[rank + k] = stage[k];
+#endif
             __builtin_amdgcn_wave_barrier();
             rank += soff;
             soff = 0;
