@@ -281,7 +281,7 @@ uint64_t round_up(uint64_t v, uint64_t m) { return (v + m - 1) / m * m; }
 // and C4 batches, where the reverse-order Infinity-Cache reuse matters
 // (profiles/r03/experiments/gpu_emit_group.txt): kept at 8192 / 4096.
 #ifndef WC_EMIT_GROUP
-#define WC_EMIT_GROUP 8192      // emit tiles per dispatch group, 4-wave launch
+#define WC_EMIT_GROUP (8192 * 4 / WC_EMIT_EW)  // emit tiles per dispatch group, small-unit launch
 #endif
 #ifndef WC_EMIT_GROUP_BIG
 #define WC_EMIT_GROUP_BIG 4096  // the 8-wave launch (units of >= kEmitBigCells)

@@ -213,7 +213,7 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
     const int w = tid >> 6, l = tid & 63;
     // Sparse staging: this thread's 8 segment flags, loaded before the key.
     const bool sparse = P.flags && U.sparse;
-    constexpr bool kKeyPar = (WC_EMIT_KEYPAR >> (EW == 4 ? 0 : 1)) & 1;
+    constexpr bool kKeyPar = (WC_EMIT_KEYPAR >> (EW == 8 ? 1 : 0)) & 1;
     // The key's scalar load is issued with the flag load, and the threshold is
     // needed only by the keep test: the chain before the coefficient loads is
     // descriptor -> flags (not descriptor -> flags -> key).  A unit whose
@@ -370,7 +370,7 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const float* __re
 // the units of a group, groups in reverse transform order (wc_capi.cpp
 // build_etiles); units of kEmitBigCells or more cells form the 8-wave launch.
 template <int EW>
-__global__ __launch_bounds__(EW * kWave, EW == 4 ? WC_EMIT_MINB : WC_EMIT_MINB8) void k_emit(EmitParams P,
+__global__ __launch_bounds__(EW * kWave, EW == 8 ? WC_EMIT_MINB8 : WC_EMIT_MINB) void k_emit(EmitParams P,
                                                                            const float* __restrict__ coef) {
     __shared__ __attribute__((aligned(16))) uint32_t sm[32];
     __shared__ uint2 stage_all[EW][256 * WC_EMIT_SB];  // per-wave pair stage (emit_pairs)
@@ -388,8 +388,8 @@ __global__ __launch_bounds__(EW * kWave, EW == 4 ? WC_EMIT_MINB : WC_EMIT_MINB8)
 }
 
 hipError_t launch_emit(hipStream_t st, const EmitParams& p, const float* coef, uint32_t nsmall, uint32_t nbig) {
-    static_assert(kEmitTile == 4 * 2048 && kEmitTileBig == 8 * 2048, "emit tile sizes");
-    if (nsmall) k_emit<4><<<nsmall, 4 * kWave, 0, st>>>(p, coef);
+    static_assert(kEmitTile == WC_EMIT_EW * 2048 && kEmitTileBig == 8 * 2048, "emit tile sizes");
+    if (nsmall) k_emit<WC_EMIT_EW><<<nsmall, WC_EMIT_EW * kWave, 0, st>>>(p, coef);
     if (nbig) {
         EmitParams q = p;
         q.edesc = p.edesc + nsmall;

@@ -95,7 +95,10 @@ constexpr uint32_t kErrTimeout = 8u;     // a look-back wait between workgroups 
 
 constexpr uint32_t kEpochMask = 0x3fffffffu;  // epoch bits of a look-back granule (wc_device.h granule_e)
 
-constexpr int kEmitTile = 8192;          // coefficients per emit tile (4 waves, 32 per thread)
+#ifndef WC_EMIT_EW
+#define WC_EMIT_EW 4  // waves per emit block of the small-unit launch (2048 coefficients per wave)
+#endif
+constexpr int kEmitTile = WC_EMIT_EW * 2048;  // coefficients per emit tile (32 per thread)
 constexpr int kEmitTileBig = 16384;      // emit tile of units of >= kEmitBigCells (8 waves)
 constexpr uint64_t kEmitBigCells = uint64_t(1) << 21;  // 128^3: longer tiles pay
 
