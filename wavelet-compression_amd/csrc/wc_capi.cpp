@@ -286,6 +286,9 @@ uint64_t round_up(uint64_t v, uint64_t m) { return (v + m - 1) / m * m; }
 #ifndef WC_EMIT_GROUP_BIG
 #define WC_EMIT_GROUP_BIG 4096  // the 8-wave launch (units of >= kEmitBigCells)
 #endif
+#ifndef WC_EMIT_ILV
+#define WC_EMIT_ILV 0  // units interleaved per run of emit blocks within a group (0: every unit of the group)
+#endif
 void build_etiles(Plan& P, int n) {
     auto big = [](const UnitDev& d) { return d.ncells >= kEmitBigCells; };
     uint32_t total = 0;
@@ -317,11 +320,14 @@ void build_etiles(Plan& P, int n) {
             groups.emplace_back(g0, g1);
             g0 = g1;
         }
-        for (auto g = groups.rbegin(); g != groups.rend(); ++g) {
+        for (auto g = groups.rbegin(); g != groups.rend(); ++g)
+          for (size_t s0 = g->first; s0 < g->second; s0 += (WC_EMIT_ILV ? WC_EMIT_ILV : g->second - g->first)) {
+            // interleave by tile index across WC_EMIT_ILV units at a time (0: the whole group)
+            const size_t s1 = WC_EMIT_ILV ? std::min<size_t>(g->second, s0 + WC_EMIT_ILV) : g->second;
             uint32_t gmax = 0;
-            for (size_t k = g->first; k < g->second; ++k) gmax = std::max(gmax, P.units[us[k]].net);
+            for (size_t k = s0; k < s1; ++k) gmax = std::max(gmax, P.units[us[k]].net);
             for (uint32_t t = 0; t < gmax; ++t)
-                for (size_t k = g->first; k < g->second; ++k) {
+                for (size_t k = s0; k < s1; ++k) {
                     const int i = us[k];
                     const UnitDev& d = P.units[i];
                     if (t >= d.net) continue;

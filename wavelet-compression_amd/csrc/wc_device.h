@@ -243,6 +243,12 @@ __device__ __forceinline__ void add_rlx(uint32_t* p, uint32_t v) {
 // 37-71 %), so re-polls slow down from ~0.2 us to ~1.7 us.  err[0] is the
 // context's error word, err[1] its poll bound (WC_OPT_SPIN_LIMIT; 0 = the
 // default kSpinLimit), read only by a wave that is already waiting.
+#ifndef WC_SPIN_S0
+#define WC_SPIN_S0 8  // s_sleep units (64 clocks) before re-polls 1-3
+#endif
+#ifndef WC_SPIN_S1
+#define WC_SPIN_S1 24  // ... before re-polls 4-15
+#endif
 __device__ __forceinline__ bool spin_fail(uint32_t& spins, uint32_t* err) {
     const uint32_t lim = __hip_atomic_load(err + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (++spins >= (lim ? lim : kSpinLimit)) {  // lim 1: the first unanswered poll fails
@@ -250,9 +256,9 @@ __device__ __forceinline__ bool spin_fail(uint32_t& spins, uint32_t* err) {
         return true;
     }
     if (spins < 4)
-        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(WC_SPIN_S0);
     else if (spins < 16)
-        __builtin_amdgcn_s_sleep(24);
+        __builtin_amdgcn_s_sleep(WC_SPIN_S1);
     else
         __builtin_amdgcn_s_sleep(64);
     return false;
