@@ -47,7 +47,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-ALL_LEGS = ("inverse", "host", "c3", "c5", "c4")
+ALL_LEGS = ("inverse", "host", "f32_64", "c3", "c5", "c4")
 
 
 def parse(argv=None):
@@ -55,10 +55,10 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2",
+    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5", "f32_64"), default="c2",
                     help="headline workload (default: BASELINE configs[1], C2)")
     ap.add_argument("--legs", default=",".join(ALL_LEGS),
-                    help="comma list of extra legs (inverse,c3,c5,c4) or 'none'")
+                    help="comma list of extra legs (inverse,host,f32_64,c3,c5,c4) or 'none'")
     ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of each extra leg")
     ap.add_argument("--hist-quantile", type=float, default=0.7,
                     help="c4 leg: quantile of the opt-in global-threshold mode (NOT the reference rule)")
@@ -475,16 +475,18 @@ def round_trip_leg(args, d: Dist, name):
     return out
 
 
-def sharded_forward_leg(args, d: Dist, name, hist=False):
+def sharded_forward_leg(args, d: Dist, name, hist=False, inverse=False):
     """C5 / C4: the workload's units split over ranks (plan_shards), forward timed
-    as the headline; C4 adds the opt-in global-threshold mode (one all-reduce)."""
+    as the headline; C4 adds the opt-in global-threshold mode (one all-reduce).
+    f32_64: C2's shape in fp32 per GPU (weak).  inverse: also wc_inverse of the
+    leg's payloads (rle_decode + inverse transform, src/decompressor.cpp:238-255)."""
     import bench_workloads as bw
     import torch
     import wcamd
     spec = bw.WORKLOADS[name]
     units, span = rank_units(name, d)
     ctx = new_context(args, d)
-    b = Batch(d, units, spec["dtype"], spec["keep"])
+    b = Batch(d, units, spec["dtype"], spec["keep"], inverse=inverse)
     secs = timed(d, ctx, lambda: b.forward(ctx), args.leg_steps, 2)
     st = stage_times(ctx, lambda: b.forward(ctx), args.leg_steps)
     kept = b.kept_total()
@@ -504,7 +506,7 @@ def sharded_forward_leg(args, d: Dist, name, hist=False):
     out = {"workload": spec["desc"], "units_total": int(m["boxes"]), "units_this_rank": b.n,
            "rank0_span": list(span), "cells_total": int(m["cells"]), "dtype": spec["dtype"], "keep": spec["keep"],
            "kept_fraction": m["kept"] / max(m["cells"], 1), "ms_per_step": ms,
-           "value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "scaling": "strong",
+           "value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "scaling": "weak" if spec["per_gpu"] else "strong",
            "rank_cell_balance": m["max_rank_cells"] / max(m["min_rank_cells"], 1),
            "per_rank": per_rank,
            "stage_ms_per_launch": {k: round(v[0], 4) for k, v in st.items()},
@@ -516,10 +518,30 @@ def sharded_forward_leg(args, d: Dist, name, hist=False):
                                     "note": "counter summaries are for the one-GPU workload"}})}}
     if hist:
         out["global_hist"] = global_hist_leg(args, d, ctx, b)
+    if inverse:
+        out["inverse"] = sharded_inverse(args, d, ctx, b, name)
     ctx.close()
     del b
     torch.cuda.empty_cache()
     return out
+
+
+def sharded_inverse(args, d: Dist, ctx, b: Batch, name):
+    """wc_inverse of a leg's payloads, timed as the forward; SURVEY §8(d) inverse
+    bytes per rank; counter traffic from the workload's PMC summary (one GPU)."""
+    kept = b.kept_total()
+    secs = timed(d, ctx, lambda: b.inverse(ctx), args.leg_steps, 2)
+    st = stage_times(ctx, lambda: b.inverse(ctx), args.leg_steps)
+    m = d.reduce({"seconds": secs, "cells": b.ncells})
+    ms = m["seconds"] / args.leg_steps * 1e3
+    alg = alg_bytes_inverse(b.ncells, kept, b.n)
+    return {"value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
+            "stage_ms_per_launch": {k: round(v[0], 4) for k, v in st.items()},
+            "roofline_path": {"achieved_per_gpu": alg / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                              "frac": alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, "bytes_per_step": alg,
+                              **(path_traffic(args.pmc, name, "f64" if b.s_in == 8 else "f32", INV_STAGES, alg)
+                                 if d.world == 1 else {"traffic": None, "traffic_source": {
+                                     "note": "counter summaries are for the one-GPU workload"}})}}
 
 
 def global_hist_leg(args, d: Dist, ctx, b: Batch):
@@ -719,8 +741,10 @@ def main():
     torch.cuda.empty_cache()
     if "c3" in args.legs_set and d.world == 1:
         out["c3"] = round_trip_leg(args, d, "c3")
+    if "f32_64" in args.legs_set:
+        out["f32_64"] = sharded_forward_leg(args, d, "f32_64")
     if "c5" in args.legs_set:
-        out["c5"] = sharded_forward_leg(args, d, "c5")
+        out["c5"] = sharded_forward_leg(args, d, "c5", inverse=True)
     if "c4" in args.legs_set:
         out["c4"] = sharded_forward_leg(args, d, "c4", hist=True)
     if d.rank == 0:

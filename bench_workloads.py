@@ -89,6 +89,10 @@ WORKLOADS = {
                desc="10 timesteps x the C3 4-level layout x 8 components, keep 0.999, box-sharded"),
     "c5": dict(units=lambda: cube_units(512, 128), dtype="f32", keep=0.9999, per_gpu=False,
                desc="512 x 128^3 fp32 boxes in total, keep 0.9999, box-sharded"),
+    # the drop-in compress() input type: Box3D holds fp32 cells (reference src/box-structs.h:7),
+    # so the reference's own hot call (src/compressor.cpp:192) runs the fp32 forward on C2's shape
+    "f32_64": dict(units=lambda: cube_units(1024, 64), dtype="f32", keep=0.999, per_gpu=True,
+                   desc="1024 x 64^3 fp32 boxes per GPU (Box3D fp32, the drop-in compress() input), keep 0.999"),
 }
 
 

@@ -77,7 +77,10 @@ void wc_ctx_destroy(wc_ctx* ctx);
 const char* wc_last_error(const wc_ctx* ctx);
 
 /* Run on an external hipStream_t (e.g. a torch stream); NULL restores the
- * context's own stream. */
+ * context's own stream.  Switching drains the previous stream first (kernels
+ * queued there may still read the plan and scratch that later calls reuse), so
+ * a caller must switch away from its stream BEFORE destroying it.  The switch
+ * takes effect even when that drain fails (the error is still returned). */
 int wc_set_stream(wc_ctx* ctx, void* hip_stream);
 int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side errors of earlier async calls */
 

@@ -781,6 +781,7 @@ def test_inverse_unit_groups_pipelined(wc, ctx, oracle, groups):
     units, n, extent, cells = pack(wc, boxes)
     payload, offs, kept = ctx.forward_host(cells, units, n, keep)
     want = [oracle.decompress_payload(wc.capi.unit_payload(payload, offs, kept, i)).ravel() for i in range(n)]
+    before = ctx.get_option(WC_OPT_INV_GROUPS)  # the session-scoped context keeps the library default afterwards
     ctx.set_option(WC_OPT_INV_GROUPS, groups)
     try:
         regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
@@ -816,7 +817,7 @@ def test_inverse_unit_groups_pipelined(wc, ctx, oracle, groups):
         ctx.synchronize()
         assert d_r2.cpu().tolist() == [0.0, 0.0]
     finally:
-        ctx.set_option(WC_OPT_INV_GROUPS, 2)
+        ctx.set_option(WC_OPT_INV_GROUPS, before)
 
 
 def test_s32_shape_special_values(wc, ctx, oracle):

@@ -471,7 +471,10 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         if (d.sparse) {  // flag range: whole 2048-coefficient blocks (flag_pos), 8-B aligned
             d.flag_off = flag_cursor;
             flag_cursor += round_up(d.ncells, 2048) >> d.lbz;
-            if (flag_cursor >= (uint64_t(1) << 32)) d.sparse = 0;  // EmitDesc keeps 32 bits: stage densely
+            if (flag_cursor >= (uint64_t(1) << 32)) {  // EmitDesc keeps 32 bits: stage densely
+                flag_cursor = d.flag_off;                // (and later units may still fit)
+                d.sparse = 0;
+            }
         }
         P.any_sparse |= d.sparse != 0;
         d.xt_begin = (uint32_t)before;  // rebased below for fast units
@@ -871,6 +874,7 @@ void wc_ctx_destroy(wc_ctx* c) {
     }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->aux) (void)hipStreamSynchronize(c->aux);
     DevBuf* bufs[] = {&c->coef,          &c->part,           &c->errflag,        &c->state,
                       &c->flags,         &c->h_cells,        &c->h_payload,      &c->h_packed,
                       &c->h_offsets,     &c->h_poff,         &c->h_kept,         &c->h_out,
@@ -903,12 +907,12 @@ int wc_set_stream(wc_ctx* c, void* s) {
     // Kernels queued on the old stream may still read the plan's descriptors
     // and the scratch, which later calls rebuild or reuse in stream order on
     // the new stream: drain the old one first.
-    if (next != c->stream) {
-        hipError_t e = hipStreamSynchronize(c->stream);
-        if (e != hipSuccess) return hip_fail(c, e, "wc_set_stream: synchronize the previous stream");
-    }
+    // The switch happens even when the drain fails (a stale handle must not
+    // stay the context's stream); the failure is still reported.
+    hipError_t e = hipSuccess;
+    if (next != c->stream) e = hipStreamSynchronize(c->stream);
     c->stream = next;
-    return WC_OK;
+    return e == hipSuccess ? WC_OK : hip_fail(c, e, "wc_set_stream: synchronize the previous stream");
 }
 
 int wc_set_option(wc_ctx* c, int option, int64_t value) {
@@ -984,6 +988,9 @@ int wc_get_option(const wc_ctx* c, int option, int64_t* value) {
 int wc_synchronize(wc_ctx* c) {
     if (!c) return WC_ERR_INVALID;
     hipError_t e = hipStreamSynchronize(c->stream);
+    // the pipelined inverse's second stream joins c->stream on success; drain it
+    // too, so no queued work outlives a synchronize on any path
+    if (e == hipSuccess && c->aux) e = hipStreamSynchronize(c->aux);
     if (e != hipSuccess) return hip_fail(c, e, "hipStreamSynchronize");
     return check_kernel_errors(c);
 }
@@ -1175,7 +1182,12 @@ int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets,
         if (e == hipSuccess)
             e = launch_inverse(c->stream, (const float*)c->coef.p, 0, (const UnitDev*)P.d_units.p,
                                (const XTile*)P.d_ixtiles.p, P.ign, P.lds_inverse, P.ifast, P.lds_fast, d_out);
-        if (e != hipSuccess) return hip_fail(c, e, "inverse launch");
+        if (e != hipSuccess) {
+            // K6r work already queued on the aux stream still reads the payload
+            // and the row index: drain it before the scratch can be reused
+            (void)hipStreamSynchronize(c->aux);
+            return hip_fail(c, e, "inverse launch");
+        }
         c->err_check_pending = true;
         return rc;
     }

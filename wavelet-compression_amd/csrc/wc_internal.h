@@ -20,7 +20,7 @@ constexpr int kFlatPerThread = kFlatTile / kThreads;  // 16 = 4 x float4
 // pass-through "tail" block at b = n/2.
 struct UnitDev {
     uint64_t cell_off;   // element offset of the unit's cells
-    uint64_t coef_off;   // element offset in the flat coefficient scratch (512-B aligned)
+    uint64_t coef_off;   // element offset in the flat coefficient scratch (128-B aligned)
     uint64_t ncells;     // W*H*D
     int32_t nx, ny, nz;  // W, H, D
     int32_t hx, hy, hz;  // n/2 per axis (number of pairs)

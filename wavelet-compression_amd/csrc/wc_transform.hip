@@ -61,7 +61,7 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
     const uint64_t obase = out_base(U, out_mode);
     float* __restrict__ dst = out + obase;
     if constexpr (KEYS) {
-        if (flags && U.sparse) {  // uniform; coef_off is 512-B aligned here
+        if (flags && U.sparse) {  // uniform; coef_off is 128-B aligned here
             const bool s32 = WC_K1_S32 && s32_ok(U);  // uniform
             uint32_t mag = s32 ? xform_fast_p1<T, false, true, true>(cells + U.cell_off, U, td, lds, threadIdx.x)
                                : xform_fast_p1<T, false, true>(cells + U.cell_off, U, td, lds, threadIdx.x);
