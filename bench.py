@@ -293,7 +293,7 @@ def stage_times(ctx, step, steps):
     return {k: (ms / cnt, cnt / steps) for k, (ms, cnt) in ctx.profile_read().items()}
 
 
-FWD_STAGES = ("transform", "fallback", "emit")
+FWD_STAGES = ("transform", "fallback", "emit", "cohort")
 INV_STAGES = ("rowindex", "decode", "inverse", "rmse")
 
 
@@ -352,7 +352,8 @@ def headline(args, d: Dist, ctx):
                   "payload_bytes": 8 * kept + 20 * b.n})
     elapsed = m["seconds"]
     # roofline of the dominant kernel: its algorithmic bytes per launch / its launch time
-    own = {"transform": b.s_in * b.ncells, "emit": 8 * kept + 20 * b.n}
+    own = {"transform": b.s_in * b.ncells, "emit": 8 * kept + 20 * b.n,
+           "cohort": alg_bytes_forward(b.s_in, b.ncells, kept, b.n)}  # the cohort launch is the whole forward
     dominant = max(stages, key=lambda k: stages[k][0])
     dom_ms = stages[dominant][0]
     achieved = own.get(dominant, 0) / (dom_ms * 1e-3) / 1e9

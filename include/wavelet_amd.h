@@ -135,6 +135,14 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  *   and offsets out; 0 = one run.  wc_inverse_host runs the same way (run
  *   r+1's payload bytes upload while run r decodes and run r-1's boxes
  *   download).
+ * WC_OPT_COHORT (default 0 = off), WC_OPT_COHORT_LAG (default 2): the cohort
+ *   forward for batches whose every unit is large (>= 2^21 cells) and of the
+ *   32 x 1 x 32-block transform shape (hx, hz multiples of 32, even cell
+ *   offset): transform and pack in ONE persistent launch, units in cohorts of
+ *   WC_OPT_COHORT, the pack of cohort p - lag beside the transform of cohort
+ *   p, staged coefficients in a ring of (lag + 2) * cohort units that stays in
+ *   the Infinity Cache.  Same bytes out; no dispatch-order assumption (items
+ *   are dequeued in list order).
  */
 #define WC_OPT_SPARSE 12
 #define WC_OPT_ORDERED 13
@@ -147,6 +155,8 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
 #define WC_OPT_TICKETS 20
 #define WC_OPT_RIX_XCD 22
 #define WC_OPT_INV_GROUPS 23
+#define WC_OPT_COHORT 24
+#define WC_OPT_COHORT_LAG 25
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 int wc_get_option(const wc_ctx* ctx, int option, int64_t* value);
 
@@ -247,6 +257,7 @@ int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* 
 #define WC_STAGE_INVERSE 3    /* K6  inverse transform */
 #define WC_STAGE_RMSE 4       /* K7  */
 #define WC_STAGE_HIST 5       /* coefficient-magnitude histogram (wc_forward_stage with d_hist) */
+#define WC_STAGE_COHORT 6     /* cohort forward: K1 + K2 in one persistent launch (WC_OPT_COHORT) */
 #define WC_NUM_STAGES 6
 int wc_profile_enable(wc_ctx* ctx, int on);
 int wc_profile_read(wc_ctx* ctx, double* total_ms, uint32_t* launches, int nstages);

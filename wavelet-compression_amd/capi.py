@@ -41,9 +41,11 @@ WC_OPT_SPIN_LIMIT = 19  # polls before a look-back wait is declared timed out (0
 WC_OPT_TICKETS = 20  # 1: ticket form whatever WC_OPT_ORDERED says (set by a look-back timeout: sticky)
 WC_OPT_RIX_XCD = 22  # row-indexed inverse tiles dealt to XCDs in contiguous runs (default 0)
 WC_OPT_INV_GROUPS = 23  # row-indexed inverse in N unit groups, row index of g+1 beside K6r of g (default 1)
+WC_OPT_COHORT = 24  # cohort forward: units per cohort (0 = off); large S32-shape units only
+WC_OPT_COHORT_LAG = 25  # cohort forward: pack of cohort p - lag beside the transform of cohort p (default 2)
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*).
-STAGES = ("transform", "emit", "decode", "inverse", "rmse", "hist")
+STAGES = ("transform", "emit", "decode", "inverse", "rmse", "hist", "cohort")
 
 
 class WcUnit(ctypes.Structure):

@@ -49,6 +49,8 @@ hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDe
 hipError_t launch_emit(hipStream_t, const EmitParams&, const float*, uint32_t, uint32_t);
 hipError_t launch_hist(hipStream_t, const UnitDev*, const FTile*, uint32_t, const float*, uint32_t,
                        unsigned long long*);
+hipError_t launch_cohort(hipStream_t, const CohortParams&, const void*, int, uint32_t);
+uint32_t cohort_grid(int dtype);
 }  // namespace wc
 
 using namespace wc;
@@ -82,6 +84,17 @@ struct Plan {
     // [ig_rd[g], ig_rd[g+1]) and its K6r tiles rtiles [ig_rt[g], ig_rt[g+1])
     std::vector<uint32_t> ig_rd, ig_rt;
     std::vector<EmitDesc> edesc;  // [units of kEmitTile tiles | units of kEmitTileBig tiles]
+    // cohort forward (wc_cohort.hip, build_cohort): every unit large and of the
+    // S32 shape; work list, emit descriptors (kEmitTile tiles, coef_off = ring
+    // slot offsets), ring of coh_ring units of coh_slot floats
+    int coh_size = 0, coh_lag = 0;    // WC_OPT_COHORT / WC_OPT_COHORT_LAG the plan was built with
+    bool coh = false;
+    std::vector<uint32_t> citems;
+    std::vector<EmitDesc> cedesc;
+    uint32_t coh_ring = 0;
+    uint64_t coh_slot = 0;
+    uint64_t coh_net = 0;              // cohort emit tiles (look-back granules)
+    size_t coh_state_bytes = 0;        // head (16) | key[n] | kdone[n] | edone[n] | status[coh_net]
     uint32_t nedesc_small = 0;
     uint32_t ngen = 0, nfast = 0, netiles = 0;
     uint32_t ign = 0, ifast = 0;  // ixtiles split
@@ -93,7 +106,7 @@ struct Plan {
     uint64_t flag_bytes = 0;   // bytes of sparse-staging segment flags (UnitDev::flag_off ranges + slack)
     size_t lds_gen = 0, lds_fast = 0, lds_inverse = 0;
     size_t state_bytes = 0;    // forward per-call state: 16 | key[n] | tickets[n] | status[netiles]
-    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_edesc, d_ixtiles, d_rtiles, d_rdtiles;
+    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_edesc, d_ixtiles, d_rtiles, d_rdtiles, d_citems, d_cedesc;
 };
 
 int ceil_log2(int64_t v) {
@@ -123,6 +136,8 @@ struct wc_ctx {
     bool opt_rix_blocked = false; // WC_OPT_RIX_BLOCKED
     bool opt_rix_xcd = false;     // WC_OPT_RIX_XCD
     int opt_inv_groups = 1;       // WC_OPT_INV_GROUPS
+    int opt_cohort = 0;           // WC_OPT_COHORT (units per cohort; 0 = off)
+    int opt_cohort_lag = 2;       // WC_OPT_COHORT_LAG
     hipStream_t aux = nullptr;    // second stream of the pipelined inverse
     std::vector<hipEvent_t> iev;  // its events
     // A kernel that may raise error bits ran since the last check.  Kernels
@@ -136,7 +151,7 @@ struct wc_ctx {
     bool sparse_staged = false;  // the last stage_transform used sparse staging
     uint64_t plan_gen = 0;  // bumped whenever get_plan rebuilds the plan
     // scratch (grow-only)
-    DevBuf coef, part, errflag, state, flags, rowinfo;
+    DevBuf coef, part, errflag, state, flags, rowinfo, ring;
     // row index (wc_inverse): epoch-tagged look-back granules, zeroed when
     // allocated and never again (a granule of an earlier call reads as
     // unpublished); epoch: the call counter they are tagged with
@@ -352,6 +367,88 @@ void build_etiles(Plan& P, int n) {
     }
 }
 
+// The cohort forward's plan (wc_cohort.hip).  Eligible: every unit has the
+// S32 transform shape (32 x 1 x 32-block tiles, hx and hz multiples of 32,
+// even cell offset) and at least kEmitBigCells (< 2^30) cells.  Units form
+// cohorts of S in batch order; phase p lists cohort p's K1 tiles (unit-major)
+// merged evenly with cohort p - lag's emit tiles (interleaved by tile index
+// across the cohort's units: a unit's consecutive tiles are S apart, so a
+// look-back usually finds its predecessors published).  Ring slot of unit u:
+// u mod R, R = (lag + 2) S — a slot is rewritten two phases after its unit's
+// emit tiles were listed.
+void build_cohort(Plan& P, int n, int S, int lag) {
+    P.coh = false;
+    P.coh_size = S;
+    P.coh_lag = lag;
+    P.citems.clear();
+    P.cedesc.clear();
+    if (S <= 0 || n <= 0) return;
+    uint64_t maxc = 0;
+    for (int i = 0; i < n; ++i) {
+        const UnitDev& d = P.units[i];
+        const bool s32 = d.fast && d.lbx == 5 && d.lby == 0 && d.lbz == 5 && d.hx % 32 == 0 && d.hz % 32 == 0 &&
+                         (d.cell_off & 1) == 0;
+        if (!s32 || d.ncells < kEmitBigCells || d.ncells >= (uint64_t(1) << 30)) return;
+        maxc = std::max(maxc, d.ncells);
+    }
+    const uint32_t R = (uint32_t)std::min<int64_t>((int64_t)(lag + 2) * S, n);
+    const uint64_t slot = round_up(maxc, 32);
+    if ((uint64_t)R * slot * 4 >= (uint64_t(1) << 31)) return;  // buffer-resource range: 31 bits
+    std::vector<uint32_t> cet(n + 1, 0);
+    for (int i = 0; i < n; ++i) cet[i + 1] = cet[i] + (uint32_t)((P.units[i].ncells + kEmitTile - 1) / kEmitTile);
+    P.coh_net = cet[n];
+    for (int i = 0; i < n; ++i) {
+        const UnitDev& d = P.units[i];
+        for (uint32_t t = 0; t < cet[i + 1] - cet[i]; ++t) {
+            EmitDesc e{};
+            e.coef_off = (uint64_t)(i % R) * slot;
+            e.pay_off = d.pay_off;
+            e.ncells = d.ncells;
+            e.unit = (uint32_t)i;
+            e.index = t;
+            e.et_begin = cet[i];
+            e.net = cet[i + 1] - cet[i];
+            e.nx = d.nx;
+            e.ny = d.ny;
+            e.nz = d.nz;
+            e.sparse = 0;
+            e.lbz = d.lbz;
+            P.cedesc.push_back(e);
+        }
+    }
+    const int C = (n + S - 1) / S;
+    std::vector<uint32_t> k1, em;
+    for (int p = 0; p < C + lag; ++p) {
+        k1.clear();
+        em.clear();
+        if (p < C)
+            for (int i = p * S; i < std::min(n, (p + 1) * S); ++i)
+                for (uint32_t t = 0; t < P.units[i].ntx; ++t) k1.push_back(P.units[i].xt_begin + t);
+        const int q = p - lag;
+        if (q >= 0 && q < C) {
+            const int a = q * S, b = std::min(n, (q + 1) * S);
+            uint32_t tmax = 0;
+            for (int i = a; i < b; ++i) tmax = std::max(tmax, cet[i + 1] - cet[i]);
+            for (uint32_t t = 0; t < tmax; ++t)
+                for (int i = a; i < b; ++i)
+                    if (t < cet[i + 1] - cet[i]) em.push_back(0x80000000u | (cet[i] + t));
+        }
+        // merge evenly: K1 item j of the phase at about position j * (|k1| + |em|) / |k1|
+        size_t x = 0, y = 0;
+        const uint64_t A = k1.size(), B = em.size();
+        while (x < A || y < B) {
+            if (y >= B || (x < A && (uint64_t)x * B <= (uint64_t)y * A))
+                P.citems.push_back(k1[x++]);
+            else
+                P.citems.push_back(em[y++]);
+        }
+    }
+    P.coh_ring = R;
+    P.coh_slot = slot;
+    P.coh_state_bytes = round_up(16 + 16ull * n, 8) + 8ull * P.coh_net;
+    P.coh = true;
+}
+
 // K6r tiling (wc_inverse.hip k_inverse_rows): TX x TY blocks in (x, y), all of
 // z; the tile's LDS is 4 TX ranges of TY*D + 4 floats, at most kRixLds.  TX
 // up to 16 blocks (32-cell = 128-B output rows), then TY as large as fits
@@ -377,13 +474,14 @@ bool set_rix_tiling(UnitDev& d, int budget, int max_lx) {
 
 bool plan_matches(const wc_ctx* c, const Plan& P, const wc_unit* units, int n) {
     return P.inv_rows == c->opt_inv_rows && P.rix_lds == c->opt_rix_lds && P.rix_lx == c->opt_rix_lx &&
-           P.rix_xcd == c->opt_rix_xcd && P.inv_groups == c->opt_inv_groups &&
+           P.rix_xcd == c->opt_rix_xcd && P.inv_groups == c->opt_inv_groups && P.coh_size == c->opt_cohort &&
+           P.coh_lag == c->opt_cohort_lag &&
            (int)P.key.size() == n && (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0);
 }
 
 void free_plan(Plan& P) {
-    DevBuf* bufs[] = {&P.d_units,   &P.d_xtiles, &P.d_ftiles, &P.d_dtiles,
-                      &P.d_edesc,   &P.d_ixtiles, &P.d_rtiles, &P.d_rdtiles};
+    DevBuf* bufs[] = {&P.d_units,   &P.d_xtiles, &P.d_ftiles, &P.d_dtiles, &P.d_edesc,
+                      &P.d_ixtiles, &P.d_rtiles, &P.d_rdtiles, &P.d_citems, &P.d_cedesc};
     for (DevBuf* b : bufs) {
         if (b->p) (void)hipFree(b->p);
         *b = DevBuf{};
@@ -609,6 +707,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     P.coef_extent = coef_cursor ? coef_cursor + kFlatTile : 0;  // slack: flat tiles read whole float4 groups
     P.flag_bytes = flag_cursor + kEmitTileBig;                  // slack: a partial last tile's flag loads
     build_etiles(P, n);
+    build_cohort(P, n, c->opt_cohort, c->opt_cohort_lag);
     int rc;
     if ((rc = upload(c, P.d_units, P.units.data(), sizeof(UnitDev) * P.units.size(), "upload units")) ||
         (rc = upload(c, P.d_xtiles, P.xtiles.data(), sizeof(XTile) * P.xtiles.size(), "upload xtiles")) ||
@@ -617,7 +716,9 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         (rc = upload(c, P.d_dtiles, P.dtiles.data(), sizeof(FTile) * P.dtiles.size(), "upload dtiles")) ||
         (rc = upload(c, P.d_edesc, P.edesc.data(), sizeof(EmitDesc) * P.edesc.size(), "upload edesc")) ||
         (rc = upload(c, P.d_rtiles, P.rtiles.data(), sizeof(RTile) * P.rtiles.size(), "upload rtiles")) ||
-        (rc = upload(c, P.d_rdtiles, P.rdtiles.data(), sizeof(FTile) * P.rdtiles.size(), "upload rdtiles")))
+        (rc = upload(c, P.d_rdtiles, P.rdtiles.data(), sizeof(FTile) * P.rdtiles.size(), "upload rdtiles")) ||
+        (rc = upload(c, P.d_citems, P.citems.data(), sizeof(uint32_t) * P.citems.size(), "upload citems")) ||
+        (rc = upload(c, P.d_cedesc, P.cedesc.data(), sizeof(EmitDesc) * P.cedesc.size(), "upload cedesc")))
         return rc;
     // The host vectors back the async copies: finish them before returning.
     hipError_t e = hipStreamSynchronize(c->stream);
@@ -658,18 +759,20 @@ int ensure_scratch(wc_ctx* c) {
         (rc = ensure(c, c->part, sizeof(double) * std::max<size_t>(nft, 4 * P.rtiles.size()))) ||
         (rc = ensure(c, c->rowinfo, sizeof(uint32_t) * 2 * std::max<uint64_t>(P.rowinfo_entries, 1))) ||
         (rc = ensure_zeroed(c, c->istate, istate_bytes(P))) ||
-        (rc = ensure(c, c->state, std::max<size_t>(P.state_bytes, decode_state_bytes(P)))))
+        (rc = ensure(c, c->state, std::max({P.state_bytes, decode_state_bytes(P), P.coh_state_bytes}))) ||
+        (P.coh && (rc = ensure(c, c->ring, (size_t)P.coh_ring * P.coh_slot * sizeof(float)))))
         return rc;
     return WC_OK;
 }
 
 // Resident workgroups of a persistent kernel (which: 0 k_transform_fast_pf,
-// 1 k_inverse_rows) for an LDS size, cached per context (one device).
+// 1 k_inverse_rows, 2 + dtype k_cohort) for an LDS size, cached per context
+// (one device).
 uint32_t persistent_grid(wc_ctx* c, int which, size_t lds) {
     auto key = std::make_pair(which, lds);
     auto it = c->grids.find(key);
     if (it != c->grids.end()) return it->second;
-    const uint32_t g = which == 0 ? transform_pf_grid(lds) : inverse_rows_grid(lds);
+    const uint32_t g = which == 0 ? transform_pf_grid(lds) : which == 1 ? inverse_rows_grid(lds) : cohort_grid(which - 2);
     c->grids[key] = g;
     return g;
 }
@@ -810,8 +913,51 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
     return WC_OK;
 }
 
+// The cohort forward (wc_cohort.hip): K1 + emit of every unit in one
+// persistent launch, staging through the Infinity-Cache-resident ring.
+int forward_cohort(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
+                   uint64_t* d_offsets, uint32_t* d_kept) {
+    Plan& P = c->plan;
+    uint8_t* st = (uint8_t*)c->state.p;
+    hipError_t e = hipMemsetAsync(st, 0, P.coh_state_bytes, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "memset cohort state");
+    CohortParams p{};
+    unsigned long long* key = (unsigned long long*)(st + 16);
+    p.E.units = (const UnitDev*)P.d_units.p;
+    p.E.edesc = (const EmitDesc*)P.d_cedesc.p;
+    p.E.n = n;
+    p.E.ordered = 1;
+    p.E.key = key;
+    p.E.status = (unsigned long long*)(st + round_up(16 + 16ull * n, 8));
+    p.E.payload = d_payload;
+    p.E.offsets = d_offsets;
+    p.E.kept = d_kept;
+    p.E.err = (uint32_t*)c->errflag.p;
+    p.E.keep = keep;
+    p.units = (const UnitDev*)P.d_units.p;
+    p.xtiles = (const XTile*)P.d_xtiles.p;
+    p.items = (const uint32_t*)P.d_citems.p;
+    p.nitems = (uint32_t)P.citems.size();
+    p.ring_units = P.coh_ring;
+    p.head = (uint32_t*)st;
+    p.key = key;
+    p.kdone = (uint32_t*)(st + 16 + 8ull * n);
+    p.edone = (uint32_t*)(st + 16 + 12ull * n);
+    p.ring = (float*)c->ring.p;
+    p.ring_bytes = (uint32_t)(P.coh_ring * P.coh_slot * sizeof(float));
+    {
+        StageTimer t(c, WC_STAGE_COHORT);
+        e = launch_cohort(c->stream, p, d_cells, dtype, persistent_grid(c, 2 + dtype, 0));
+    }
+    if (e != hipSuccess) return hip_fail(c, e, "cohort launch");
+    c->sparse_staged = false;
+    c->err_check_pending = true;  // a wait that timed out surfaces at wc_synchronize
+    return WC_OK;
+}
+
 int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
                    uint64_t* d_offsets, uint32_t* d_kept) {
+    if (c->plan.coh) return forward_cohort(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
     int rc = stage_transform(c, d_cells, dtype, keep, c->opt_sparse);
     return rc ? rc : stage_emit(c, n, keep, nullptr, d_payload, d_offsets, d_kept);
 }
@@ -880,7 +1026,8 @@ void wc_ctx_destroy(wc_ctx* c) {
                       &c->h_offsets,     &c->h_poff,         &c->h_kept,         &c->h_out,
                       &c->plan.d_units,  &c->plan.d_xtiles,  &c->plan.d_ftiles,  &c->plan.d_dtiles,
                       &c->plan.d_edesc, &c->plan.d_ixtiles, &c->plan.d_rtiles,
-                      &c->plan.d_rdtiles, &c->rowinfo, &c->istate};
+                      &c->plan.d_rdtiles, &c->plan.d_citems, &c->plan.d_cedesc, &c->rowinfo, &c->istate,
+                      &c->ring};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (Plan& P : c->plan_cache) free_plan(P);
@@ -962,6 +1109,14 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
         case WC_OPT_TICKETS:
             c->force_tickets = value != 0;
             return WC_OK;
+        case WC_OPT_COHORT:
+            if (value < 0 || value > 64) return fail(c, WC_ERR_INVALID, "WC_OPT_COHORT: 0..64 units");
+            c->opt_cohort = (int)value;
+            return WC_OK;
+        case WC_OPT_COHORT_LAG:
+            if (value < 1 || value > 8) return fail(c, WC_ERR_INVALID, "WC_OPT_COHORT_LAG: 1..8 cohorts");
+            c->opt_cohort_lag = (int)value;
+            return WC_OK;
         default:
             return fail(c, WC_ERR_INVALID, "unknown option");
     }
@@ -981,6 +1136,8 @@ int wc_get_option(const wc_ctx* c, int option, int64_t* value) {
         case WC_OPT_HOST_CHUNK: *value = c->opt_host_chunk; return WC_OK;
         case WC_OPT_SPIN_LIMIT: *value = c->opt_spin_limit; return WC_OK;
         case WC_OPT_TICKETS: *value = c->force_tickets ? 1 : 0; return WC_OK;
+        case WC_OPT_COHORT: *value = c->opt_cohort; return WC_OK;
+        case WC_OPT_COHORT_LAG: *value = c->opt_cohort_lag; return WC_OK;
         default: return WC_ERR_INVALID;
     }
 }
