@@ -258,7 +258,7 @@ int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* 
 #define WC_STAGE_RMSE 4       /* K7  */
 #define WC_STAGE_HIST 5       /* coefficient-magnitude histogram (wc_forward_stage with d_hist) */
 #define WC_STAGE_COHORT 6     /* cohort forward: K1 + K2 in one persistent launch (WC_OPT_COHORT) */
-#define WC_NUM_STAGES 6
+#define WC_NUM_STAGES 7
 int wc_profile_enable(wc_ctx* ctx, int on);
 int wc_profile_read(wc_ctx* ctx, double* total_ms, uint32_t* launches, int nstages);
 

@@ -1,0 +1,126 @@
+"""BASELINE.json configs[4] (C5) at full size on one GPU, checked against the
+CPU oracle: all 512 x 128^3 fp32 units (bench_workloads.WORKLOADS["c5"]) at
+keep 0.9999f in ONE wc_forward (the reference's own loop runs them one by one,
+src/compressor.cpp:192-248 per box, src/modes.cpp:100-103):
+  * every unit: header (W, H, D, ncoeff, nrle), 0 <= kept <= ncoeff, and the
+    worst-case slot offsets;
+  * payload bytes equal the oracle's on 10 units (first, last, random ones);
+  * the staged two-kernel path and the cohort forward (WC_OPT_COHORT) write
+    identical bytes for ALL 512 units (zeroed payload buffers compared whole);
+  * wc_inverse of the whole batch reproduces the oracle's decompress()
+    (rle_decode + inverse_wavelet_decompose, src/decompressor.cpp:14-159) on 2
+    sampled units bit for bit.
+"""
+import numpy as np
+import pytest
+from wavelet_compression_amd.capi import WC_OPT_COHORT, WC_OPT_COHORT_LAG
+
+pytestmark = pytest.mark.gpu
+
+KEEP = float(np.float32(0.9999))
+
+
+@pytest.fixture(scope="module")
+def c5_run(wc):
+    import torch
+    import bench_workloads as bw
+    units = bw.WORKLOADS["c5"]["units"]()
+    assert len(units) == 512 and all(u.cells == 128 ** 3 for u in units)
+    dev = torch.device("cuda", 0)
+    cells, offs, extent = bw.synth_cells(torch, dev, units, "f32")
+    tab, n, _ = bw.units_array(wc.capi, units, offs)
+    ctx = wc.capi.Context(0)
+    cap = wc.capi.payload_bound(tab, n)
+    payload = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    kept = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ctx.forward(cells.data_ptr(), wc.capi.WC_F32, tab, n, KEEP, payload.data_ptr(), cap, offsets.data_ptr(),
+                kept.data_ptr())
+    ctx.synchronize()
+    r = dict(units=units, offs=offs, cells=cells, payload=payload, offsets_dev=offsets,
+             offsets=offsets.cpu().numpy(), kept=kept.cpu().numpy(), tab=tab, n=n, ctx=ctx, dev=dev, cap=cap,
+             extent=extent)
+    yield r
+    ctx.close()
+    del r, cells, payload
+    torch.cuda.empty_cache()
+
+
+def _box(r, i):
+    u = r["units"][i]
+    o = r["offs"][i]
+    return r["cells"][o:o + u.cells].cpu().numpy().reshape(u.D, u.H, u.W)
+
+
+def _payload(r, i):
+    po = int(r["offsets"][i])
+    return r["payload"][po:po + 20 + 8 * int(r["kept"][i])].cpu().numpy().tobytes()
+
+
+def _sample(n, k=10, seed=5):
+    rng = np.random.default_rng(seed)
+    return sorted({0, n - 1, *rng.choice(np.arange(1, n - 1), size=k - 2, replace=False).tolist()})
+
+
+def test_c5_every_unit_header_kept_and_slots(c5_run):
+    import torch
+    r = c5_run
+    n = r["n"]
+    idx = r["offsets_dev"][:n].view(n, 1) + torch.arange(20, device=r["dev"]).view(1, 20)
+    hdr = r["payload"][idx.reshape(-1)].cpu().numpy().reshape(n, 20).copy().view("<i4")
+    assert np.array_equal(hdr[:, :4], np.tile(np.array([128, 128, 128, 128 ** 3], np.int32), (n, 1)))
+    assert np.array_equal(hdr[:, 4], r["kept"].astype(np.int32))
+    assert np.all(r["kept"] >= 0) and np.all(r["kept"].astype(np.int64) <= 128 ** 3)
+    slots = 4 + np.arange(n, dtype=np.int64) * (24 + 8 * 128 ** 3)
+    assert np.array_equal(r["offsets"][:n].astype(np.int64), slots)
+    assert int(r["offsets"][n]) == int(slots[-1]) + 20 + 8 * int(r["kept"][-1])
+    frac = r["kept"].astype(np.int64).sum() / (n * 128 ** 3)
+    assert 0.3 < frac < 0.6  # SURVEY §8(d) field at keep 0.9999: ~45 % kept
+
+
+def test_c5_payloads_match_oracle(c5_run, oracle):
+    r = c5_run
+    for i in _sample(r["n"]):
+        want, k = oracle.compress_payload(_box(r, i), KEEP)
+        assert _payload(r, i) == want, i
+        assert int(r["kept"][i]) == k
+
+
+@pytest.mark.parametrize("cohort,lag", [(0, 2), (2, 2), (4, 1)])
+def test_c5_paths_identical_all_units(c5_run, wc, cohort, lag):
+    """The default path's bytes for all 512 units against the staged two-kernel
+    path (cohort 0) and the cohort forward: whole zeroed buffers compared."""
+    import torch
+    r = c5_run
+    other = torch.zeros_like(r["payload"])
+    offs = torch.zeros_like(r["offsets_dev"])
+    kept = torch.zeros(r["n"], dtype=torch.int32, device=r["dev"])
+    c = wc.capi.Context(0)
+    try:
+        c.set_option(WC_OPT_COHORT, cohort)
+        c.set_option(WC_OPT_COHORT_LAG, lag)
+        c.forward(r["cells"].data_ptr(), wc.capi.WC_F32, r["tab"], r["n"], KEEP, other.data_ptr(), r["cap"],
+                  offs.data_ptr(), kept.data_ptr())
+        c.synchronize()
+    finally:
+        c.close()
+    assert np.array_equal(kept.cpu().numpy(), r["kept"])
+    assert np.array_equal(offs.cpu().numpy(), r["offsets"])
+    assert torch.equal(other, r["payload"])
+    del other
+    torch.cuda.empty_cache()
+
+
+def test_c5_inverse_sampled_units_match_oracle(c5_run, oracle):
+    import torch
+    r = c5_run
+    regen = torch.empty(r["extent"], dtype=torch.float32, device=r["dev"])
+    r["ctx"].inverse(r["payload"].data_ptr(), r["offsets_dev"].data_ptr(), r["tab"], r["n"], regen.data_ptr())
+    r["ctx"].synchronize()
+    for i in (1, r["n"] - 2):
+        want = oracle.decompress_payload(_payload(r, i)).ravel()
+        o = r["offs"][i]
+        assert regen[o:o + 128 ** 3].cpu().numpy().tobytes() == want.tobytes(), i
+    del regen
+    torch.cuda.empty_cache()

@@ -81,7 +81,7 @@ def test_cohort_special_values(wc, ctx, oracle):
     b[0][0, 0, 0] = np.nan
     b[0][0, 0, 1] = np.nan
     b[1][5, 7, 9] = np.nan
-    b[2] -= 50.0  # mean far below 0: the largest |c| (the DC-like sub-band) is negative
+    b[2] = -(np.abs(b[2]) + 1.0)  # every cell negative: the largest |c| (the low-pass sub-band) is negative
     b[3][:] = 0.0
     b[4][3, 3, 3] = np.inf
     b[4][9, 9, 9] = -np.inf
@@ -107,6 +107,21 @@ def test_cohort_not_taken_for_ineligible_batches(wc, ctx, oracle):
     assert "cohort" not in st and "emit" in st
     for i in range(n):
         assert got[i] == oracle.compress_payload(boxes[i].astype(np.float32), KEEPS[0])[0], i
+
+
+def test_cohort_not_taken_in_ticket_form(wc, ctx, oracle, batch):
+    """The cohort launch relies on in-order dispatch (one block per item); the
+    ticket form (WC_OPT_ORDERED 0, shared devices) runs the two-kernel path."""
+    from wavelet_compression_amd.capi import WC_OPT_ORDERED
+    boxes, packed = batch
+    units, n, cells = packed[np.float32]
+    ctx.set_option(WC_OPT_ORDERED, 0)
+    try:
+        got, st = _run(wc, ctx, units, n, cells, KEEPS[1], 4, 1)
+    finally:
+        ctx.set_option(WC_OPT_ORDERED, 1)
+    assert "cohort" not in st and "emit" in st
+    assert got[3] == oracle.compress_payload(boxes[3].astype(np.float32), KEEPS[1])[0]
 
 
 def test_cohort_wait_timeout_reported_then_exact(wc, oracle):

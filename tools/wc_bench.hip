@@ -167,6 +167,13 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "options: %s\n", wc_last_error(ctx));
         return 2;
     }
+    // WCB_COHORT=S, WCB_COHORT_LAG=L: the cohort forward (WC_OPT_COHORT / _LAG)
+    const int cohort = std::getenv("WCB_COHORT") ? std::atoi(std::getenv("WCB_COHORT")) : 0;
+    const int cohort_lag = std::getenv("WCB_COHORT_LAG") ? std::atoi(std::getenv("WCB_COHORT_LAG")) : 2;
+    if (wc_set_option(ctx, WC_OPT_COHORT, cohort) != WC_OK || wc_set_option(ctx, WC_OPT_COHORT_LAG, cohort_lag) != WC_OK) {
+        std::fprintf(stderr, "options: %s\n", wc_last_error(ctx));
+        return 2;
+    }
     // WCB_CHUNK=k (uniform cubes only, diagnostic): the forward as boxes/k calls of k
     // units each (same unit list, cells/payload pointers advanced per call), so the
     // context's coefficient staging is one k-unit buffer reused by every call.
@@ -254,11 +261,13 @@ int main(int argc, char** argv) {
         run(off_a, k_a, pa, ra);
         wc_set_option(ctx, WC_OPT_ORDERED, 0);
         wc_set_option(ctx, WC_OPT_SPARSE, 0);
+        wc_set_option(ctx, WC_OPT_COHORT, 0);
         wc_set_option(ctx, WC_OPT_INVERSE_ROWS, 0);
         run(off_b, k_b, pb, rb);
         wc_set_option(ctx, WC_OPT_ORDERED, ordered);
         wc_set_option(ctx, WC_OPT_SPARSE, sparse);
         wc_set_option(ctx, WC_OPT_INVERSE_ROWS, rows);
+        wc_set_option(ctx, WC_OPT_COHORT, cohort);
         identical = 1;
         for (int i = 0; i < boxes && identical; ++i) {
             if (k_a[i] != k_b[i] || off_a[i] != off_b[i]) identical = 0;
@@ -272,12 +281,12 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(hk.data(), kept, 4 * boxes, hipMemcpyDeviceToHost));
     double ksum = 0;
     for (uint32_t k : hk) ksum += k;
-    const char* names[WC_NUM_STAGES] = {"transform", "emit", "decode", "inverse", "rmse", "hist"};
+    const char* names[WC_NUM_STAGES] = {"transform", "emit", "decode", "inverse", "rmse", "hist", "cohort"};
     std::printf("{\"boxes\": %d, \"dim\": %d, \"dtype\": \"%s\", \"keep\": %.17g, \"steps\": %d, "
                 "\"ms_per_step\": %.4f, \"cells_per_s\": %.6e, \"kept_fraction\": %.6f, \"payload_bytes\": %llu, "
-                "\"ordered\": %d, \"sparse\": %d, \"rows\": %d, \"rix\": [%d, %d, %d], \"paths_identical\": %d, \"stage_ms\": {",
+                "\"ordered\": %d, \"sparse\": %d, \"cohort\": [%d, %d], \"rows\": %d, \"rix\": [%d, %d, %d], \"paths_identical\": %d, \"stage_ms\": {",
                 boxes, dim, f64 ? "f64" : "f32", keep, steps, step_ms, ncells / (step_ms * 1e-3),
-                ksum / (double)ncells, (unsigned long long)total, ordered, sparse, rows, rix_lds, rix_tx, rix_blocked, identical);
+                ksum / (double)ncells, (unsigned long long)total, ordered, sparse, cohort, cohort_lag, rows, rix_lds, rix_tx, rix_blocked, identical);
     bool first = true;
     for (int s = 0; s < WC_NUM_STAGES; ++s)
         if (cnt[s]) {

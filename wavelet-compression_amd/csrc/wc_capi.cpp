@@ -49,8 +49,7 @@ hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDe
 hipError_t launch_emit(hipStream_t, const EmitParams&, const float*, uint32_t, uint32_t);
 hipError_t launch_hist(hipStream_t, const UnitDev*, const FTile*, uint32_t, const float*, uint32_t,
                        unsigned long long*);
-hipError_t launch_cohort(hipStream_t, const CohortParams&, const void*, int, uint32_t);
-uint32_t cohort_grid(int dtype);
+hipError_t launch_cohort(hipStream_t, const CohortParams&, const void*, int);
 }  // namespace wc
 
 using namespace wc;
@@ -94,7 +93,7 @@ struct Plan {
     uint32_t coh_ring = 0;
     uint64_t coh_slot = 0;
     uint64_t coh_net = 0;              // cohort emit tiles (look-back granules)
-    size_t coh_state_bytes = 0;        // head (16) | key[n] | kdone[n] | edone[n] | status[coh_net]
+    size_t coh_state_bytes = 0;        // 16 (spare) | key[n] | kdone[n] | edone[n] | status[coh_net]
     uint32_t nedesc_small = 0;
     uint32_t ngen = 0, nfast = 0, netiles = 0;
     uint32_t ign = 0, ifast = 0;  // ixtiles split
@@ -376,6 +375,9 @@ void build_etiles(Plan& P, int n) {
 // look-back usually finds its predecessors published).  Ring slot of unit u:
 // u mod R, R = (lag + 2) S — a slot is rewritten two phases after its unit's
 // emit tiles were listed.
+#ifndef WC_COH_RUN
+#define WC_COH_RUN 1  // items of one kind per run of the cohort work list (8 measured slower: gpu_cohort_runs.txt)
+#endif
 void build_cohort(Plan& P, int n, int S, int lag) {
     P.coh = false;
     P.coh_size = S;
@@ -433,14 +435,17 @@ void build_cohort(Plan& P, int n, int S, int lag) {
                 for (int i = a; i < b; ++i)
                     if (t < cet[i + 1] - cet[i]) em.push_back(0x80000000u | (cet[i] + t));
         }
-        // merge evenly: K1 item j of the phase at about position j * (|k1| + |em|) / |k1|
-        size_t x = 0, y = 0;
-        const uint64_t A = k1.size(), B = em.size();
+        // merge evenly in runs of WC_COH_RUN items of one kind: blocks are dealt
+        // round-robin to the 8 XCDs, so a run of 8 spreads each kind over all
+        // of them (alternating single items put every K1 tile on 4 XCDs and
+        // every emit tile on the other 4: profiles/r04/experiments/gpu_cohort_xp.txt)
+        const uint64_t A = (k1.size() + WC_COH_RUN - 1) / WC_COH_RUN, B = (em.size() + WC_COH_RUN - 1) / WC_COH_RUN;
+        uint64_t x = 0, y = 0;
         while (x < A || y < B) {
-            if (y >= B || (x < A && (uint64_t)x * B <= (uint64_t)y * A))
-                P.citems.push_back(k1[x++]);
-            else
-                P.citems.push_back(em[y++]);
+            const bool k = y >= B || (x < A && x * B <= y * A);
+            const std::vector<uint32_t>& v = k ? k1 : em;
+            const size_t a = (size_t)(k ? x++ : y++) * WC_COH_RUN;
+            P.citems.insert(P.citems.end(), v.begin() + a, v.begin() + std::min(v.size(), a + WC_COH_RUN));
         }
     }
     P.coh_ring = R;
@@ -766,13 +771,12 @@ int ensure_scratch(wc_ctx* c) {
 }
 
 // Resident workgroups of a persistent kernel (which: 0 k_transform_fast_pf,
-// 1 k_inverse_rows, 2 + dtype k_cohort) for an LDS size, cached per context
-// (one device).
+// 1 k_inverse_rows) for an LDS size, cached per context (one device).
 uint32_t persistent_grid(wc_ctx* c, int which, size_t lds) {
     auto key = std::make_pair(which, lds);
     auto it = c->grids.find(key);
     if (it != c->grids.end()) return it->second;
-    const uint32_t g = which == 0 ? transform_pf_grid(lds) : which == 1 ? inverse_rows_grid(lds) : cohort_grid(which - 2);
+    const uint32_t g = which == 0 ? transform_pf_grid(lds) : inverse_rows_grid(lds);
     c->grids[key] = g;
     return g;
 }
@@ -939,7 +943,6 @@ int forward_cohort(wc_ctx* c, const void* d_cells, int dtype, int n, double keep
     p.items = (const uint32_t*)P.d_citems.p;
     p.nitems = (uint32_t)P.citems.size();
     p.ring_units = P.coh_ring;
-    p.head = (uint32_t*)st;
     p.key = key;
     p.kdone = (uint32_t*)(st + 16 + 8ull * n);
     p.edone = (uint32_t*)(st + 16 + 12ull * n);
@@ -947,7 +950,7 @@ int forward_cohort(wc_ctx* c, const void* d_cells, int dtype, int n, double keep
     p.ring_bytes = (uint32_t)(P.coh_ring * P.coh_slot * sizeof(float));
     {
         StageTimer t(c, WC_STAGE_COHORT);
-        e = launch_cohort(c->stream, p, d_cells, dtype, persistent_grid(c, 2 + dtype, 0));
+        e = launch_cohort(c->stream, p, d_cells, dtype);
     }
     if (e != hipSuccess) return hip_fail(c, e, "cohort launch");
     c->sparse_staged = false;
@@ -957,7 +960,9 @@ int forward_cohort(wc_ctx* c, const void* d_cells, int dtype, int n, double keep
 
 int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
                    uint64_t* d_offsets, uint32_t* d_kept) {
-    if (c->plan.coh) return forward_cohort(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
+    // the cohort launch relies on in-order dispatch (one block per item): the
+    // ticket form runs the two-kernel path
+    if (c->plan.coh && use_ordered(c)) return forward_cohort(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
     int rc = stage_transform(c, d_cells, dtype, keep, c->opt_sparse);
     return rc ? rc : stage_emit(c, n, keep, nullptr, d_payload, d_offsets, d_kept);
 }

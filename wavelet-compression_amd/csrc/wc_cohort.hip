@@ -16,12 +16,15 @@
 //
 // Work list (host-built, wc_capi.cpp build_cohort): units in cohorts of S;
 // phase p lists cohort p's K1 tiles interleaved with the emit tiles of cohort
-// p - lag; unit u stages into ring slot u mod R, R = (lag + 2) S.  Workgroups
-// dequeue items in list order (one atomic per CLAIM items), so every item
-// waits only on items dequeued before it — a K1 tile on the emit tiles of the
-// slot's previous unit (edone), an emit tile on its unit's K1 tiles (kdone)
-// and on its unit's earlier emit tiles (look-back) — which are held by running
-// workgroups: forward progress whatever the dispatch order or residency.
+// p - lag; unit u stages into ring slot u mod R, R = (lag + 2) S.  Block b
+// runs item b, so every item waits only on items of lower block ids — a K1
+// tile on the emit tiles of the slot's previous unit (edone), an emit tile on
+// its unit's K1 tiles (kdone) and on its unit's earlier emit tiles
+// (look-back).  Those sit 1-2 phases (>= 2 resident-block windows) back, so
+// the waits rarely block.  A persistent dequeue form (workgroups claiming
+// items from one counter: progress whatever the dispatch order) was built and
+// measured 5-240x slower: claimed-but-queued items make convoys
+// (profiles/r04/experiments/gpu_cohort_dequeue.txt).
 //
 // Hand-offs inside the launch (MI355X_MICROARCH.md Valid forms, row 1): every
 // staged coefficient is stored write-through (sc1) and every emit load of it
@@ -31,10 +34,11 @@
 // atomicMax read with an agent-scope load (never the scalar path).
 #include "wc_emit.h"
 
-#include <algorithm>
-
-#ifndef WC_COH_CLAIM
-#define WC_COH_CLAIM 4  // items per dequeue (one head word serves ~88 dequeues/us)
+// Diagnostic builds (tools/build_variants.sh; timing only, results invalid):
+//   WC_COH_XP_NOWAIT  no kdone / edone waits;  WC_COH_XP_AUX=0  plain (not sc1)
+//   ring loads and stores;  WC_COH_XP_K1ONLY / WC_COH_XP_EONLY  one item kind only.
+#ifndef WC_COH_XP_AUX
+#define WC_COH_XP_AUX 16
 #endif
 
 namespace wc {
@@ -50,6 +54,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ring_rsrc(const CohortParams& 
 
 // One lane waits until *cnt >= want (relaxed agent-scope polls, bounded).
 __device__ __forceinline__ void wait_geq(const uint32_t* cnt, uint32_t want, uint32_t* err) {
+#ifdef WC_COH_XP_NOWAIT
+    return;
+#endif
     for (uint32_t spins = 0; ld_rlx(cnt) < want;)
         if (spin_fail(spins, err)) break;
 }
@@ -62,7 +69,7 @@ struct RingTile {
     __amdgpu_buffer_rsrc_t rs;
     uint32_t base;  // byte offset of the tile's first coefficient in the ring
     __device__ __forceinline__ float4 operator[](int i) const {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, base + (uint32_t)i * 16u, 0, 16);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, base + (uint32_t)i * 16u, 0, WC_COH_XP_AUX);
         return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
     }
 };
@@ -103,7 +110,7 @@ __device__ __forceinline__ unsigned long long xform_s32_p2_ring(const UnitDev& U
         const float4 v = *reinterpret_cast<const float4*>(lds + row * rstride + col);
         const uint32_t f0 = fb + ((it & 1) ? dA : 0u) + (((it >> 1) & 1) ? dB : 0u) + ((it >> 2) ? dC : 0u);
         const u32x4 w = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-        __builtin_amdgcn_raw_buffer_store_b128(w, rs, slot_bytes + (f0 << 2), 0, 16);  // sc1: write-through
+        __builtin_amdgcn_raw_buffer_store_b128(w, rs, slot_bytes + (f0 << 2), 0, WC_COH_XP_AUX);  // sc1: write-through
         const float m4 = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
         if (__ballot(__float_as_uint(m4) == amax)) {
             best = key_lo_max(best, v.x, f0, amax);
@@ -135,7 +142,7 @@ struct alignas(16) CohShared {
     uint32_t sm[32];                       // emit_tile words
     unsigned long long key[kThreads / kWave];
     uint32_t mag[kThreads / kWave];
-    uint32_t claim[4];
+    uint32_t pad[4];
 };
 
 template <typename T>
@@ -144,14 +151,16 @@ __device__ __forceinline__ void cohort_k1(const CohortParams& C, const T* __rest
     const XTile td = C.xtiles[xt];
     const uint32_t u = td.unit;
     const UnitDev& U = C.units[u];
-    if (u >= C.ring_units) {  // the slot's previous unit: every emit tile has read it
-        const uint32_t v = u - C.ring_units;
-        if (tid == 0) wait_geq(C.edone + v, (uint32_t)((C.units[v].ncells + kEmitTile - 1) / kEmitTile), C.E.err);
-        __syncthreads();
-    }
     uint32_t mag = xform_fast_p1<T, false, true, true>(cells + U.cell_off, U, td, lds, tid);
     mag = wave_max_u32_u(mag);
     if ((tid & 63) == 0) sh.mag[tid >> 6] = mag;
+    // the slot's previous unit: every emit tile has read it.  Waited for only
+    // now (phase 1 reads cells and writes LDS): the poll's round trip overlaps
+    // the cell loads instead of preceding them.
+    if (u >= C.ring_units && tid == 0) {
+        const uint32_t v = u - C.ring_units;
+        wait_geq(C.edone + v, (uint32_t)((C.units[v].ncells + kEmitTile - 1) / kEmitTile), C.E.err);
+    }
     __syncthreads();
     mag = max(max(sh.mag[0], sh.mag[1]), max(sh.mag[2], sh.mag[3]));
     const uint32_t slot_bytes = (u % C.ring_units) * (uint32_t)(C.ring_bytes / C.ring_units);
@@ -175,39 +184,28 @@ __device__ __forceinline__ void cohort_emit(const CohortParams& C, uint32_t ei, 
 
 }  // namespace
 
-// Persistent: each workgroup claims CLAIM consecutive items per dequeue (the
-// next claim issued while the current items run) until the list is done.
+// One block per item, items in list order (blockIdx.x): the in-flight items
+// are the resident blocks (~1024 consecutive items), and with the per-XCD
+// in-order dispatch the other look-back kernels also rely on (DESIGN.md
+// §Forward progress) every item waits only on blocks dispatched before it.
+// wc_capi.cpp takes this path only where the launch-order form is in use;
+// the ticket form runs the two-kernel path instead.
 template <typename T>
 __global__ __launch_bounds__(kThreads, 4) void k_cohort(CohortParams C, const T* __restrict__ cells) {
     extern __shared__ __attribute__((aligned(16))) float lds[];  // K1 rows | emit pair stage
     __shared__ CohShared sh;
     const int tid = threadIdx.x;
-    if (tid == 0) sh.claim[0] = atomicAdd(C.head, (uint32_t)WC_COH_CLAIM);
-    __syncthreads();
-    uint32_t base = __builtin_amdgcn_readfirstlane(sh.claim[0]);
-    while (base < C.nitems) {
-        uint32_t next = 0;
-        if (tid == 0) next = atomicAdd(C.head, (uint32_t)WC_COH_CLAIM);
-        for (uint32_t k = 0; k < (uint32_t)WC_COH_CLAIM && base + k < C.nitems; ++k) {
-            const uint32_t it = cst(C.items)[base + k];
-#ifndef WC_COH_XP_NOK1
-            if (it >> 31)
+    const uint32_t it = cst(C.items)[blockIdx.x];
+#ifdef WC_COH_XP_K1ONLY
+    if (it >> 31) return;
 #endif
-#ifndef WC_COH_XP_NOEMIT
-                cohort_emit(C, it & 0x7fffffffu, lds, sh, tid);
+#ifdef WC_COH_XP_EONLY
+    if (!(it >> 31)) return;
 #endif
-#if !defined(WC_COH_XP_NOK1) && !defined(WC_COH_XP_NOEMIT)
-            else
-#endif
-#ifndef WC_COH_XP_NOK1
-                cohort_k1<T>(C, cells, it, lds, sh, tid);
-#endif
-            __syncthreads();  // LDS reused by the next item
-        }
-        if (tid == 0) sh.claim[0] = next;
-        __syncthreads();
-        base = __builtin_amdgcn_readfirstlane(sh.claim[0]);
-    }
+    if (it >> 31)
+        cohort_emit(C, it & 0x7fffffffu, lds, sh, tid);
+    else
+        cohort_k1<T>(C, cells, it, lds, sh, tid);
 }
 
 size_t cohort_lds_bytes() {
@@ -216,20 +214,9 @@ size_t cohort_lds_bytes() {
     return k1 > em ? k1 : em;
 }
 
-uint32_t cohort_grid(int dtype) {
-    int per_cu = 0, ncu = 0, dev = 0;
-    (void)hipGetDevice(&dev);
-    const void* f = dtype == 1 ? (const void*)k_cohort<double> : (const void*)k_cohort<float>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, kThreads, cohort_lds_bytes()) != hipSuccess ||
-        per_cu < 1)
-        per_cu = 2;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
-    return (uint32_t)per_cu * (uint32_t)ncu;
-}
-
-hipError_t launch_cohort(hipStream_t st, const CohortParams& p, const void* cells, int dtype, uint32_t grid) {
+hipError_t launch_cohort(hipStream_t st, const CohortParams& p, const void* cells, int dtype) {
     if (p.nitems == 0) return hipSuccess;
-    const uint32_t g = std::min<uint32_t>(grid, (p.nitems + WC_COH_CLAIM - 1) / WC_COH_CLAIM);
+    const uint32_t g = p.nitems;
     if (dtype == 1)
         k_cohort<double><<<g, kThreads, cohort_lds_bytes(), st>>>(p, (const double*)cells);
     else

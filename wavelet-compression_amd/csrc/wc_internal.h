@@ -139,8 +139,8 @@ struct EmitParams {
 };
 
 // Parameter block of k_cohort (wc_cohort.hip), filled by wc_capi.cpp
-// forward_cohort: the cohort forward's work list, its per-unit counters and
-// the staging ring.
+// forward_cohort: the cohort forward's work list (one block per item), its
+// per-unit counters and the staging ring.
 struct CohortParams {
     EmitParams E;                  // emit fields: edesc = cohort emit descriptors (8192-coefficient tiles)
     const UnitDev* units;
@@ -148,8 +148,7 @@ struct CohortParams {
     const uint32_t* items;         // work list: bit 31 set = emit (cohort edesc index), else xtile index
     uint32_t nitems;
     uint32_t ring_units;           // R: unit u stages into slot u mod R
-    uint32_t* head;                // dequeue counter        } zeroed per call
-    unsigned long long* key;       // unit max keys (= E.key) }
+    unsigned long long* key;       // unit max keys (= E.key) } zeroed per call
     uint32_t* kdone;               // K1 tiles finished      }
     uint32_t* edone;               // emit tiles that have read their staging }
     float* ring;                   // staging ring (E.edesc coef_off are slot offsets into it)
