@@ -423,11 +423,19 @@ void build_cohort(Plan& P, int n, int S, int lag) {
     for (int p = 0; p < C + lag; ++p) {
         k1.clear();
         em.clear();
+#ifndef WC_COH_XP_ELIST
         if (p < C)
+#else
+        if (false)  // diagnostic (timing only): emit items only
+#endif
             for (int i = p * S; i < std::min(n, (p + 1) * S); ++i)
                 for (uint32_t t = 0; t < P.units[i].ntx; ++t) k1.push_back(P.units[i].xt_begin + t);
         const int q = p - lag;
+#ifdef WC_COH_XP_K1LIST
+        if (false) {  // diagnostic (timing only): K1 items only
+#else
         if (q >= 0 && q < C) {
+#endif
             const int a = q * S, b = std::min(n, (q + 1) * S);
             uint32_t tmax = 0;
             for (int i = a; i < b; ++i) tmax = std::max(tmax, cet[i + 1] - cet[i]);
