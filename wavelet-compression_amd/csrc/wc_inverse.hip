@@ -756,6 +756,40 @@ __device__ __forceinline__ void synth_block(const float (&c)[2][2][2], float (&V
         }
 }
 
+#ifndef WC_RIX_RMSE_INLINE
+#define WC_RIX_RMSE_INLINE 1  // fp64 originals: fused RMSE summed inside the x-quad synthesis (no re-read of the output)
+#endif
+#ifndef WC_RIX_RMSE_ROUNDS_LESS
+#define WC_RIX_RMSE_ROUNDS_LESS 5  // prefetch rounds given up by the fused-RMSE forms (no spills)
+#endif
+// Original cells of one z-block pair of an x-quad column (fused RMSE): at
+// cell index base + sy dy + sz dz, 4 consecutive x cells, narrowed to float
+// as calc_rmse_per_box sees them (src/calc-loss.cpp:12-43 on Box3D floats).
+template <int OT>
+__device__ __forceinline__ void rix_load_orig(const void* __restrict__ orig, int64_t base, int64_t sy, int64_t sz,
+                                              float (&o)[2][2][4]) {
+#pragma unroll
+    for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) {
+            const int64_t i = base + sy * dy + sz * dz;
+            if constexpr (OT == 1) {
+                const f64x2* p = reinterpret_cast<const f64x2*>(static_cast<const double*>(orig) + i);
+                const f64x2 a = p[0], b = p[1];
+                o[dz][dy][0] = (float)a.x;
+                o[dz][dy][1] = (float)a.y;
+                o[dz][dy][2] = (float)b.x;
+                o[dz][dy][3] = (float)b.y;
+            } else {
+                const float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(orig) + i);
+                o[dz][dy][0] = a.x;
+                o[dz][dy][1] = a.y;
+                o[dz][dy][2] = a.z;
+                o[dz][dy][3] = a.w;
+            }
+        }
+}
+
 // Tiles of workgroup b: blocked (a contiguous run of ceil(ntiles / G) tiles:
 // consecutive tiles share the payload lines at their range boundaries and the
 // unit's row entries) or strided (b, b + G, ...).
@@ -791,7 +825,7 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
     const uint2* pr = reinterpret_cast<const uint2*>(payload + offsets[T.unit] + 20);
     RixRange R = rix_load_range(T, rowinfo, w, l);
     RixPlan PL = rix_plan(T, R, l);
-    constexpr int NR = OT ? kRixRounds - 5 : kRixRounds;  // the RMSE pass needs registers
+    constexpr int NR = OT ? kRixRounds - WC_RIX_RMSE_ROUNDS_LESS : kRixRounds;  // the RMSE sums need registers
     uint2 q[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r)
@@ -857,6 +891,8 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
         }
 
         // 3. synthesis of tile t
+        bool f4 = false;
+        double racc = 0.0;  // fused RMSE of the x-quad path: this thread's squared differences
         {
             const int lbx = T.lbx, TYv = T.tyv;
             const int W = T.W, H = T.H, D = T.D, hx = W >> 1, hz = D >> 1;
@@ -866,7 +902,8 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
 #ifdef WC_XP_NOPHASEC
             if (tid < 0)
 #endif
-            if (WC_RIX_F4 && TX >= 2 && ((T.cell_off & 3) == 0) && ((W & 3) == 0)) {
+            f4 = WC_RIX_F4 && TX >= 2 && ((T.cell_off & 3) == 0) && ((W & 3) == 0);  // uniform
+            if (f4) {
                 // two x-blocks x two z-blocks per thread: 16-B x-quad stores
                 const int nq = (TX >> 1) * TYv * (hz >> 1);
                 for (int ci = tid; ci < nq; ci += kThreads) {
@@ -874,6 +911,11 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
                     const int byl = rest % TYv, bq = rest / TYv;
                     const int bxl = 2 * bp, by = T.by0 + byl, bzb = 2 * bq;
                     if (T.bx0 + bxl >= hx) continue;
+                    // fused RMSE (WC_RIX_RMSE_INLINE): the original cells of z-block
+                    // pair qb = 0, issued before the LDS reads (qb = 1: after qb 0)
+                    float og[2][2][2][4];  // [qb][dz][dy][4 x-cells], original cells narrowed to float
+                    if constexpr (OT == 1 && WC_RIX_RMSE_INLINE)
+                        rix_load_orig<OT>(orig, T.cell_off + lo + 2 * bxl + sy * (2 * by) + sz * (2 * bzb), sy, sz, og[0]);
                     float c[2][2][2][2][2];  // [x-block][sz][sy][sx][z-block]
 #pragma unroll
                     for (int e = 0; e < 2; ++e)
@@ -914,6 +956,23 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
                                 *reinterpret_cast<float4*>(p) =
                                     make_float4(V[0][dz][dy][0], V[0][dz][dy][1], V[1][dz][dy][0], V[1][dz][dy][1]);
                             }
+                        if constexpr (OT == 1 && WC_RIX_RMSE_INLINE) {
+                            if (qb == 0)  // the second z-block pair's originals, in flight during this one's sums
+                                rix_load_orig<OT>(orig, T.cell_off + lo + 2 * bxl + sy * (2 * by) + sz * (2 * (bzb + 1)),
+                                                  sy, sz, og[1]);
+#pragma unroll
+                            for (int dz = 0; dz < 2; ++dz)
+#pragma unroll
+                                for (int dy = 0; dy < 2; ++dy) {
+                                    const float v[4] = {V[0][dz][dy][0], V[0][dz][dy][1], V[1][dz][dy][0],
+                                                        V[1][dz][dy][1]};
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k) {
+                                        const float d = og[qb][dz][dy][k] - v[k];  // float - float, then widened
+                                        racc += (double)d * (double)d;
+                                    }
+                                }
+                        }
                     }
                 }
             } else {
@@ -966,7 +1025,13 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
             }
         }
         __syncthreads();
-        if constexpr (OT != 0) {  // 4. calc_rmse_per_box over tile t's cells (src/calc-loss.cpp:12-43)
+        if constexpr (OT == 1 && WC_RIX_RMSE_INLINE) {
+            if (f4) {  // uniform: the x-quad synthesis summed its own cells
+                const double acc = wave_sum(racc);
+                if (l == 0) part[4 * (uint64_t)T.nat + w] = acc;
+            }
+        }
+        if constexpr (OT != 0) if (!(OT == 1 && WC_RIX_RMSE_INLINE && f4)) {  // 4. calc_rmse_per_box over tile t's cells (src/calc-loss.cpp:12-43)
             const int TX = 1 << T.lbx, txv = min(TX, (T.W >> 1) - T.bx0), ny2 = 2 * T.tyv;
             const uint32_t nc = (uint32_t)(T.D * ny2) << T.lbx;
             const int64_t sy = T.W, sz = (int64_t)T.W * T.H;
