@@ -616,19 +616,19 @@ __global__ __launch_bounds__(kThreads) void k_inverse_fast(const float* __restri
 //
 // Wave w owns the ranges g = w + 4j (lane j holds range j's row entries; every
 // sub-band class in every wave) and an LDS region of its own.  It zeroes the
-// region and walks its ranges one at a time, 64 pairs per round: round rr
-// belongs to range j = (number of ranges whose rounds end at or before rr) — a
-// ballot and a popcount, uniform — and lane l holds pair m*64 + l of it.
-// Position in the range = first + (inclusive DPP scan of run + 1 over the
-// range's pairs after its first); the value is dropped into LDS.  Then one
-// block barrier, and X, Y, Z synthesis per 2x2x2 block
-// (src/decompressor.cpp:89-156) from float4 sub-band reads (4 z-blocks per
-// thread) with 8-B x-pair stores.
+// region and walks its ranges one at a time, 64 pairs per round (range j's
+// round m: lane l holds pair m*64 + l; rix_scatter_range).  Position in the
+// range = first + (inclusive DPP scan of run + 1 over the range's pairs after
+// its first); the value is dropped into LDS.  Then one block barrier, and X, Y,
+// Z synthesis per 2x2x2 block (src/decompressor.cpp:89-156) from LDS sub-band
+// reads with 16-B x-quad stores (8-B x-pair stores where the output is not
+// 16-B aligned); with fp64 originals the fused RMSE sums the squared
+// differences of the cells each thread has just synthesised.
 //
 // Persistent: workgroup b runs tiles b, b + G, ...  The latency of the
 // dependent loads (tile record -> row entries + payload offset -> pairs) is
 // hidden by a two-stage prefetch: while tile t is synthesised, the pairs of
-// tile t + G are in flight (the first kRixRounds rounds; the rest are loaded
+// tile t + G are in flight (the first round of each range; the rest are loaded
 // when scattered) and the row entries of tile t + 2G.
 //
 // The row index of a unit is complete and monotone whatever the payload
@@ -638,7 +638,7 @@ __global__ __launch_bounds__(kThreads) void k_inverse_fast(const float* __restri
 // checked against the range: a malformed payload (reported by K5) gives
 // garbage cells, never an out-of-bounds access.
 #ifndef WC_RIX_ROUNDS
-#define WC_RIX_ROUNDS 20  // 128 VGPRs with the x-quad synthesis: 4 waves per SIMD, no spills
+#define WC_RIX_ROUNDS 16  // prefetch slots (one per range): 128 VGPRs with the x-quad synthesis, 4 waves per SIMD, no spills
 #endif
 #ifndef WC_RIX_F4
 #define WC_RIX_F4 1  // x-quad (16-B) stores where the output allows them
@@ -668,65 +668,57 @@ __device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* 
     return R;
 }
 
-// Per-lane range plan of a wave: pair count, and the inclusive prefix of the
-// ranges' round counts (rin; rounds of range j are [rin_j - rounds_j, rin_j)).
+// Per-lane range plan of a wave: pair count of range l (lanes < TX).
 struct RixPlan {
-    uint32_t cnt, rin, nrounds;
+    uint32_t cnt;
 };
 
 __device__ __forceinline__ RixPlan rix_plan(const RTile& T, const RixRange& R, int l) {
     const uint32_t rlen = (uint32_t)(T.tyv * T.D);
     RixPlan p;
     p.cnt = (l < (1 << T.lbx) && R.e > R.ks) ? min(R.e - R.ks, rlen) : 0u;
-    const uint32_t rounds = (p.cnt + 63) >> 6;
-    p.rin = wave_incl_sum32(rounds);
-    p.nrounds = __builtin_amdgcn_readlane(p.rin, 63);
     return p;
 }
 
-// Range j and round m within it of wave round rr (uniform).
-__device__ __forceinline__ void rix_round(const RixPlan& p, int l, uint32_t rr, int& j, uint32_t& m) {
-    (void)l;
-    j = __popcll(__ballot(p.rin <= rr));  // ranges whose rounds all come before rr
-    const uint32_t rin = __builtin_amdgcn_readlane(p.rin, j);
-    const uint32_t cnt = __builtin_amdgcn_readlane(p.cnt, j);
-    m = rr - (rin - ((cnt + 63) >> 6));
+// Rounds of 64 pairs, range-major (round 4; before: rounds in flat order over
+// the wave's ranges, each round finding its range by a ballot and popcount,
+// measured equal at C2 and 4 % slower at C5, profiles/r04/experiments/
+// gpu_rangemajor.txt): prefetch slot j holds the first 64 pairs of range j
+// (lane l: pair l), so a round's range is a compile-time constant of the
+// unrolled loops and the row fields come from immediate-lane readlanes.  Later
+// rounds of a range (more than 64 pairs) and ranges past the prefetch slots
+// are loaded when scattered.
+template <int J>
+__device__ __forceinline__ uint2 rix_load_first(const uint2* __restrict__ pr, const RixRange& R, const RixPlan& p,
+                                                int l) {
+    const uint32_t cnt = __builtin_amdgcn_readlane(p.cnt, J);
+    const uint32_t ks = __builtin_amdgcn_readlane(R.ks, J);
+    return (uint32_t)l < cnt ? pr[ks + (uint32_t)l] : make_uint2(0u, 0u);
 }
 
-__device__ __forceinline__ uint2 rix_load_round(const uint2* __restrict__ pr, const RixRange& R, const RixPlan& p,
-                                                int l, uint32_t rr) {
-    int j;
-    uint32_t m;
-    rix_round(p, l, rr, j, m);
-    const uint32_t i = m * 64 + (uint32_t)l;
+// Scatter range j's pairs into its LDS range (q0: its first 64 pairs, or
+// loaded here when !have0).
+__device__ __forceinline__ void rix_scatter_range(float* __restrict__ reg, int RS, uint32_t rlen, uint2 q0, bool have0,
+                                                  const uint2* __restrict__ pr, const RixRange& R, const RixPlan& p,
+                                                  int l, int j) {
     const uint32_t cnt = __builtin_amdgcn_readlane(p.cnt, j);
     const uint32_t ks = __builtin_amdgcn_readlane(R.ks, j);
-#ifdef WC_XP_NOPAIRS
-    return make_uint2(i & 1, ks);
-#endif
-    return i < cnt ? pr[ks + i] : make_uint2(0u, 0u);
-}
-
-// Scatter wave round rr into the wave's LDS region; carry: the scan through
-// the previous round of the same range (uniform).
-__device__ __forceinline__ void rix_scatter_round(float* __restrict__ reg, int RS, uint32_t rlen, uint2 q,
-                                                  const RixRange& R, const RixPlan& p, int l, uint32_t rr,
-                                                  uint32_t& carry) {
-    int j;
-    uint32_t m;
-    rix_round(p, l, rr, j, m);
-    const uint32_t i = m * 64 + (uint32_t)l;
-    const uint32_t cnt = __builtin_amdgcn_readlane(p.cnt, j);
-    const int32_t run = (int32_t)q.x;
-    const uint32_t x = (i < cnt && i > 0) ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
-    if (m == 0) carry = 0;
-    const uint32_t S = carry + wave_incl_sum32(x);
-    carry = __builtin_amdgcn_readlane(S, 63);
-    const uint32_t pos = (uint32_t)__builtin_amdgcn_readlane(R.c0, j) + S;
+    const uint32_t c0 = __builtin_amdgcn_readlane(R.c0, j);
+    float* __restrict__ rg = reg + j * RS;
+    uint32_t carry = c0;
+    for (uint32_t m0 = 0; m0 < cnt; m0 += 64) {  // uniform
+        const uint32_t i = m0 + (uint32_t)l;
+        uint2 q = q0;
+        if (m0 != 0 || !have0) q = i < cnt ? pr[ks + i] : make_uint2(0u, 0u);
+        const int32_t run = (int32_t)q.x;
+        const uint32_t x = (i < cnt && i > 0) ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
+        const uint32_t pos = carry + wave_incl_sum32(x);
+        carry = __builtin_amdgcn_readlane(pos, 63);
 #ifdef WC_XP_NOSCATTER
-    if (q.y == 0x12345u)
+        if (q.y == 0x12345u)
 #endif
-    if (i < cnt && pos < rlen) reg[j * RS + pos] = __uint_as_float(q.y);
+        if (i < cnt && pos < rlen) rg[pos] = __uint_as_float(q.y);
+    }
 }
 
 // Inverse of one 2x2x2 block (src/decompressor.cpp:89-156: X, then Y, then Z
@@ -756,11 +748,23 @@ __device__ __forceinline__ void synth_block(const float (&c)[2][2][2], float (&V
         }
 }
 
+// The prefetch of a tile's pairs into q: the first round of each range.
+template <int NR>
+__device__ __forceinline__ void rix_prefetch(uint2 (&q)[NR], const uint2* __restrict__ pr, const RixRange& R,
+                                             const RixPlan& p, const RTile& T, int l) {
+    const int TX = 1 << T.lbx;
+#define WC_RIX_PF(J) if (J < NR && J < TX) q[J < NR ? J : 0] = rix_load_first<J>(pr, R, p, l);
+    WC_RIX_PF(0) WC_RIX_PF(1) WC_RIX_PF(2) WC_RIX_PF(3) WC_RIX_PF(4) WC_RIX_PF(5) WC_RIX_PF(6) WC_RIX_PF(7)
+    WC_RIX_PF(8) WC_RIX_PF(9) WC_RIX_PF(10) WC_RIX_PF(11) WC_RIX_PF(12) WC_RIX_PF(13) WC_RIX_PF(14) WC_RIX_PF(15)
+#undef WC_RIX_PF
+    static_assert(NR <= 16, "rix_prefetch: extend WC_RIX_PF");
+}
+
 #ifndef WC_RIX_RMSE_INLINE
 #define WC_RIX_RMSE_INLINE 1  // fp64 originals: fused RMSE summed inside the x-quad synthesis (no re-read of the output)
 #endif
 #ifndef WC_RIX_RMSE_ROUNDS_LESS
-#define WC_RIX_RMSE_ROUNDS_LESS 5  // prefetch rounds given up by the fused-RMSE forms (no spills)
+#define WC_RIX_RMSE_ROUNDS_LESS 3  // prefetch slots given up by the fused-RMSE forms (no spills)
 #endif
 // Original cells of one z-block pair of an x-quad column (fused RMSE): at
 // cell index base + sy dy + sz dz, 4 consecutive x cells, narrowed to float
@@ -825,11 +829,11 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
     const uint2* pr = reinterpret_cast<const uint2*>(payload + offsets[T.unit] + 20);
     RixRange R = rix_load_range(T, rowinfo, w, l);
     RixPlan PL = rix_plan(T, R, l);
-    constexpr int NR = OT ? kRixRounds - WC_RIX_RMSE_ROUNDS_LESS : kRixRounds;  // the RMSE sums need registers
+    // prefetch slots, one per range (a wave owns at most 16 ranges at the
+    // default WC_OPT_RIX_TX); the RMSE sums need registers
+    constexpr int NR = OT ? kRixRounds - WC_RIX_RMSE_ROUNDS_LESS : kRixRounds;
     uint2 q[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r)
-        if ((uint32_t)r < PL.nrounds) q[r] = rix_load_round(pr, R, PL, l, r);
+    rix_prefetch<NR>(q, pr, R, PL, T, l);
     uint32_t t1 = t + G;
     RTile T1 = T;
     RixRange R1{0u, 0u, 0u};
@@ -850,22 +854,11 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
             float4* r4 = reinterpret_cast<float4*>(reg);
             const uint32_t n4 = (uint32_t)(TX * RS) >> 2;
             for (uint32_t i = l; i < n4; i += 64) r4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-            uint32_t carry = 0;
 #ifndef WC_XP_NOSCANS
 #pragma unroll
-            for (int r = 0; r < NR; ++r)
-                if ((uint32_t)r < PL.nrounds) rix_scatter_round(reg, RS, rlen, q[r], R, PL, l, r, carry);
-            // rounds past the prefetch window (dense tiles): batches of
-            // NR loads in flight together, then their scatters (q is
-            // free until the next tile's prefetch below)
-            for (uint32_t r0 = NR; r0 < PL.nrounds; r0 += NR) {
-#pragma unroll
-                for (int r = 0; r < NR; ++r)
-                    if (r0 + r < PL.nrounds) q[r] = rix_load_round(pr, R, PL, l, r0 + r);
-#pragma unroll
-                for (int r = 0; r < NR; ++r)
-                    if (r0 + r < PL.nrounds) rix_scatter_round(reg, RS, rlen, q[r], R, PL, l, r0 + r, carry);
-            }
+            for (int j = 0; j < NR; ++j)
+                if (j < TX) rix_scatter_range(reg, RS, rlen, q[j], true, pr, R, PL, l, j);
+            for (int j = NR; j < TX; ++j) rix_scatter_range(reg, RS, rlen, q[0], false, pr, R, PL, l, j);
 #else
             if (q[0].x == 77u && q[5].y == 3u) reg[0] = 1.0f;
 #endif
@@ -877,12 +870,10 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
         RTile T2 = T1;
         RixRange R2{0u, 0u, 0u};
         const uint2* pr2 = pr1;
-        RixPlan PL1{0u, 0u, 0u};
+        RixPlan PL1{0u};
         if (t1 < tend) {
             PL1 = rix_plan(T1, R1, l);
-#pragma unroll
-            for (int r = 0; r < NR; ++r)
-                if ((uint32_t)r < PL1.nrounds) q[r] = rix_load_round(pr1, R1, PL1, l, r);
+            rix_prefetch<NR>(q, pr1, R1, PL1, T1, l);
             if (t2 < tend) {
                 T2 = tiles[t2];
                 pr2 = reinterpret_cast<const uint2*>(payload + offsets[T2.unit] + 20);
