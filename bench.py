@@ -65,7 +65,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="time budget of each CPU-baseline sample (boxes run until it is spent)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r03"),
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r04"),
                     help="PMC traffic summaries (tools/pmc_summary.py): a file or a directory of pmc_*.json, "
                          "one per workload; merged into roofline.traffic and each leg's roofline_path.traffic "
                          "when measured on the same workload AND the same kernel sources")

@@ -676,6 +676,9 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         uint64_t rix_cells = 0;
         for (UnitDev& d : P.units) {
             d.ndt = d.rix ? (uint32_t)(d.ncells / kRixTile) + 1 : d.nftiles;
+#ifdef WC_XP_RIX_CAP  // diagnostic (timing only): row-index tiles for a kept fraction of at most this
+            if (d.rix) d.ndt = std::min(d.ndt, (uint32_t)((double)d.ncells * WC_XP_RIX_CAP / kRixTile) + 2);
+#endif
             d.dt_begin = total;
             total += d.ndt;
             maxt = std::max(maxt, d.ndt);
