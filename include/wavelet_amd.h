@@ -143,6 +143,15 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  *   p, staged coefficients in a ring of (lag + 2) * cohort units that stays in
  *   the Infinity Cache.  Same bytes out; no dispatch-order assumption (items
  *   are dequeued in list order).
+ * WC_OPT_HOST_THREADS (default: OMP_NUM_THREADS, else the cores, at most 16):
+ *   wc_forward_host / wc_inverse_host make the pages of each destination span
+ *   of the caller's host buffer resident (MADV_POPULATE_WRITE, no byte
+ *   changed) from this many threads just before the device-to-host copy into
+ *   it: a copy into never-touched pageable memory otherwise takes the page
+ *   faults on its own thread (C2 payloads: 12-20 GB/s instead of the link's
+ *   57).  0 = leave the faults to the copy.  Whole pages inside a span only.
+ * WC_OPT_HOST_THP (default 1): advise transparent huge pages
+ *   (MADV_HUGEPAGE) on the 2-MiB-aligned interior of those spans first.
  */
 #define WC_OPT_SPARSE 12
 #define WC_OPT_ORDERED 13
@@ -157,6 +166,8 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
 #define WC_OPT_INV_GROUPS 23
 #define WC_OPT_COHORT 24
 #define WC_OPT_COHORT_LAG 25
+#define WC_OPT_HOST_THREADS 27
+#define WC_OPT_HOST_THP 28
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
 int wc_get_option(const wc_ctx* ctx, int option, int64_t* value);
 

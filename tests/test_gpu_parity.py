@@ -695,6 +695,50 @@ def test_inverse_host_pipelined_runs(wc, ctx, oracle):
                 assert not regen[~owned].any(), chunk  # gap cells untouched
 
 
+@pytest.mark.parametrize("threads,thp", [(0, 1), (1, 0), (4, 1), (-1, 1), (-1, 0)])
+def test_host_destination_prefault(wc, ctx, oracle, threads, thp):
+    """WC_OPT_HOST_THREADS / WC_OPT_HOST_THP: the _host calls fault in each
+    destination span of the caller's buffer just before its device-to-host
+    copy (csrc/wc_hostmem.h).  Into caller buffers that already hold data,
+    over pipelined runs: the payload bytes before 4 and past offsets[n] and
+    the output's gap cells (whole pages of sentinels between the units) keep
+    their values, and every setting gives the same bytes as the oracle."""
+    from wavelet_compression_amd.capi import WC_OPT_HOST_CHUNK, WC_OPT_HOST_THP, WC_OPT_HOST_THREADS
+    keep = KEEPS[1]
+    boxes = synth(oracle, [(64, 64, 64), (32, 64, 128), (64, 64, 64), (16, 16, 16), (64, 32, 64)], seed0=41)
+    boxes = [b.astype(np.float32) for b in boxes]
+    gap = 3 * 4096 + 5  # cells: more than two whole pages between units
+    offsets = np.cumsum([0] + [int(b.size) + gap for b in boxes[:-1]]).tolist()
+    units, n, extent, cells = pack(wc, boxes, np.float32, offsets)
+    cap = wc.capi.payload_bound(units, n)
+    payload = np.full(cap, 0xAB, np.uint8)
+    offs = np.zeros(n + 1, np.uint64)
+    kept = np.zeros(n, np.uint32)
+    out = np.full(extent, 7.0, np.float32)
+    ctx.set_option(WC_OPT_HOST_THREADS, threads)
+    ctx.set_option(WC_OPT_HOST_THP, thp)
+    ctx.set_option(WC_OPT_HOST_CHUNK, 1 << 18)
+    try:
+        ctx._check(ctx._L.wc_forward_host(ctx._h, cells.ctypes.data, wc.capi.WC_F32, units, n, float(keep),
+                                          payload.ctypes.data, cap, offs.ctypes.data, kept.ctypes.data))
+        ctx._check(ctx._L.wc_inverse_host(ctx._h, payload.ctypes.data, offs.ctypes.data, units, n,
+                                          out.ctypes.data))
+    finally:
+        ctx.set_option(WC_OPT_HOST_THREADS, -1)
+        ctx.set_option(WC_OPT_HOST_THP, 1)
+        ctx.set_option(WC_OPT_HOST_CHUNK, 1 << 25)
+    end = int(offs[n])
+    assert np.all(payload[:4] == 0xAB) and np.all(payload[end + 4:] == 0xAB)
+    owned = np.zeros(extent, bool)
+    for i, b in enumerate(boxes):
+        want = oracle_payload(oracle, b, keep)
+        assert wc.capi.unit_payload(payload, offs, kept, i) == want, i
+        o = units[i].cell_offset
+        owned[o:o + b.size] = True
+        assert out[o:o + b.size].tobytes() == oracle.decompress_payload(want).ravel().tobytes(), i
+    assert np.all(out[~owned] == 7.0)
+
+
 def test_plan_cache_eviction(wc, ctx, oracle):
     """More distinct batches than the plan cache holds (16), each twice: plans
     are swapped back in, evicted, and rebuilt into an evicted plan's buffers;

@@ -4,8 +4,10 @@ here the host library, the CLI and the host-IO test are rebuilt with ASan +
 UBSan (`make asan`) and with TSan (`make tsan`) and run over the host-only
 paths: the xz thread pool (parallel encode == serial bytes, decode round trip,
 presets 0/1/6 across 4 encode and 3 decode threads), plotfile read/write and
-the reference fixtures, .raw side files, parameters, file selection, and the
-CLI's argument errors.  Any sanitizer report fails the test (halt_on_error)."""
+the reference fixtures, .raw side files, parameters, file selection, the
+CLI's argument errors, and the core library's host pool + destination
+prefault of the _host entry points (csrc/wc_hostmem.cpp, tests/cpp/
+test_hostmem.cpp).  Any sanitizer report fails the test (halt_on_error)."""
 import lzma
 import os
 import subprocess
@@ -80,3 +82,15 @@ def test_cli_argument_errors_under_sanitizer(san_bins, san, tmp_path):
     r = subprocess.run([cli, f"compresseddir={tmp_path}/", "-d"], capture_output=True, text=True, timeout=120, env=env)
     check_clean(r, f"{san} cli missing params")
     assert "Missing out directory!" in r.stderr
+
+
+@pytest.mark.parametrize("san", SANS)
+def test_host_pool_and_prefault_under_sanitizer(san_bins, san, tmp_path):
+    """wc_hostmem: every pool task runs once (0..15 workers, 0..5000 tasks, 60
+    jobs back to back); populate_for_write changes no byte (written data, never
+    touched zeros, unaligned edges, both the MADV_POPULATE_WRITE and the
+    per-page touch path) and leaves every whole page of the range resident."""
+    r = subprocess.run([str(san_bins[san] / "test_hostmem")], capture_output=True, text=True, timeout=300,
+                       env=san_env(tmp_path))
+    check_clean(r, f"{san} test_hostmem")
+    assert r.returncode == 0 and "checks passed" in r.stdout, r.stdout + r.stderr

@@ -43,6 +43,8 @@ WC_OPT_RIX_XCD = 22  # row-indexed inverse tiles dealt to XCDs in contiguous run
 WC_OPT_INV_GROUPS = 23  # row-indexed inverse in N unit groups, row index of g+1 beside K6r of g (default 1)
 WC_OPT_COHORT = 24  # cohort forward: units per cohort (0 = off); large S32-shape units only
 WC_OPT_COHORT_LAG = 25  # cohort forward: pack of cohort p - lag beside the transform of cohort p (default 2)
+WC_OPT_HOST_THREADS = 27  # _host calls: threads that fault in a copy's host destination first (0 = off)
+WC_OPT_HOST_THP = 28  # _host calls: advise huge pages on those destinations (default 1)
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*).
 STAGES = ("transform", "emit", "decode", "inverse", "rmse", "hist", "cohort")

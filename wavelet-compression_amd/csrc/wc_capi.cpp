@@ -13,6 +13,7 @@
 // offsets[u].  Inverse: K5 k_decode -> dense flat scratch -> K6 k_inverse{,_fast}.
 #include "wavelet_amd.h"
 #include "wc_internal.h"
+#include "wc_hostmem.h"
 
 #include <algorithm>
 #include <cmath>
@@ -20,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -164,6 +166,10 @@ struct wc_ctx {
     std::vector<hipEvent_t> hev;
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
+    // host pages of a copy's destination faulted in ahead of it (wc_hostmem.h)
+    int opt_host_threads = -1;    // WC_OPT_HOST_THREADS (-1: not yet resolved from the environment)
+    bool opt_host_thp = true;     // WC_OPT_HOST_THP
+    std::unique_ptr<wc::HostPool> hpool;
     // plans of earlier batches (most recent last), swapped in when a batch recurs
     std::vector<Plan> plan_cache;
     // persistent-grid sizes (resident workgroups for an LDS size) on this device
@@ -1078,6 +1084,8 @@ int wc_set_stream(wc_ctx* c, void* s) {
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "wc_set_stream: synchronize the previous stream");
 }
 
+static int host_threads_default();
+
 int wc_set_option(wc_ctx* c, int option, int64_t value) {
     if (!c) return WC_ERR_INVALID;
     switch (option) {
@@ -1133,6 +1141,13 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
             if (value < 1 || value > 8) return fail(c, WC_ERR_INVALID, "WC_OPT_COHORT_LAG: 1..8 cohorts");
             c->opt_cohort_lag = (int)value;
             return WC_OK;
+        case WC_OPT_HOST_THREADS:
+            if (value < -1 || value > 256) return fail(c, WC_ERR_INVALID, "WC_OPT_HOST_THREADS: -1..256");
+            c->opt_host_threads = (int)value;
+            return WC_OK;
+        case WC_OPT_HOST_THP:
+            c->opt_host_thp = value != 0;
+            return WC_OK;
         default:
             return fail(c, WC_ERR_INVALID, "unknown option");
     }
@@ -1154,6 +1169,10 @@ int wc_get_option(const wc_ctx* c, int option, int64_t* value) {
         case WC_OPT_TICKETS: *value = c->force_tickets ? 1 : 0; return WC_OK;
         case WC_OPT_COHORT: *value = c->opt_cohort; return WC_OK;
         case WC_OPT_COHORT_LAG: *value = c->opt_cohort_lag; return WC_OK;
+        case WC_OPT_HOST_THREADS:
+            *value = c->opt_host_threads < 0 ? host_threads_default() : c->opt_host_threads;
+            return WC_OK;
+        case WC_OPT_HOST_THP: *value = c->opt_host_thp; return WC_OK;
         default: return WC_ERR_INVALID;
     }
 }
@@ -1506,6 +1525,25 @@ static std::vector<int> host_runs(const wc_ctx* c, const wc_unit* units, int n) 
     return rb;
 }
 
+// WC_OPT_HOST_THREADS unset: the job's CPU share (OMP_NUM_THREADS, 16 per GPU
+// on the MI355X boxes, where nproc shows the whole host) or the cores, <= 16.
+static int host_threads_default() {
+    int t = 0;
+    if (const char* e = std::getenv("OMP_NUM_THREADS")) t = std::atoi(e);
+    if (t <= 0) t = (int)std::thread::hardware_concurrency();
+    return std::clamp(t, 1, 16);
+}
+
+// Fault in the pages of a host destination before a device-to-host copy lands
+// there (wc_hostmem.h: the copy's own thread faults at 12–20 GB/s).
+static void host_populate(wc_ctx* c, void* p, size_t bytes) {
+    if (c->opt_host_threads < 0) c->opt_host_threads = host_threads_default();
+    if (c->opt_host_threads == 0 || bytes == 0) return;
+    if (!c->hpool || c->hpool->threads() != c->opt_host_threads)
+        c->hpool = std::make_unique<wc::HostPool>(c->opt_host_threads - 1);
+    wc::populate_for_write(c->hpool.get(), p, bytes, c->opt_host_thp);
+}
+
 // The copy streams (when there is more than one run) and 2 events per run.
 static int host_streams(wc_ctx* c, int nr) {
     hipError_t e;
@@ -1610,6 +1648,7 @@ static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_u
         const uint64_t span = po[m] - 4;
         if (R - 4 + po[m] > cap) return fail(c, WC_ERR_INVALID, "payload_capacity");
         hipStream_t ds = nr > 1 ? c->down : c->stream;
+        host_populate(c, payload + R, span);
         if (span && (e = hipMemcpyAsync(payload + R, (const uint8_t*)c->h_packed.p + pbase[r] + 4, span,
                                         hipMemcpyDeviceToHost, ds)) != hipSuccess)
             return hip_fail(c, e, "payload readback");
@@ -1671,13 +1710,16 @@ static int inverse_host_once(wc_ctx* c, const uint8_t* payload, const uint64_t* 
         if ((rc = wc_inverse(c, (const uint8_t*)c->h_payload.p, (const uint64_t*)c->h_offsets.p + a, units + a, m,
                              (float*)c->h_out.p)))
             return rc;
-        hipStream_t ds = c->stream;
-        if (nr > 1) {
-            if ((e = hipEventRecord(c->hev[2 * r + 1], c->stream)) != hipSuccess ||
-                (e = hipStreamWaitEvent(c->down, c->hev[2 * r + 1], 0)) != hipSuccess)
-                return hip_fail(c, e, "decode event");
-            ds = c->down;
-        }
+        if (nr > 1 && (e = hipEventRecord(c->hev[2 * r + 1], c->stream)) != hipSuccess)
+            return hip_fail(c, e, "decode event");
+    }
+    // Every upload and decode is queued; the boxes download run by run, each
+    // destination span faulted in just before its copy (host_populate).
+    for (int r = 0; r < nr; ++r) {
+        const int a = rb[r], m = rb[r + 1] - rb[r];
+        hipStream_t ds = nr > 1 ? c->down : c->stream;
+        if (nr > 1 && (e = hipStreamWaitEvent(c->down, c->hev[2 * r + 1], 0)) != hipSuccess)
+            return hip_fail(c, e, "decode event");
         // Copy back exactly the cells the units own (the caller's buffer may
         // have gaps), one copy per span of back-to-back units.
         for (int i = a; i < a + m;) {
@@ -1689,6 +1731,7 @@ static int inverse_host_once(wc_ctx* c, const uint8_t* payload, const uint64_t* 
                 if (cj && units[j].cell_offset != end) break;
                 end += cj;
             }
+            if (end > o) host_populate(c, out + o, sizeof(float) * (end - o));
             if (end > o && (e = hipMemcpyAsync(out + o, (float*)c->h_out.p + o, sizeof(float) * (end - o),
                                                hipMemcpyDeviceToHost, ds)) != hipSuccess)
                 return hip_fail(c, e, "box readback");
