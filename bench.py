@@ -574,32 +574,51 @@ def global_hist_leg(args, d: Dist, ctx, b: Batch):
 
 def host_leg(args, d: Dist, ctx, b: Batch):
     """C2 through wc_forward_host: the cells start in pinned host memory, the
-    packed payloads end in (pageable) host memory; includes both PCIe copies."""
+    packed payloads end in pageable host memory; includes both PCIe copies.
+    `ms_per_step`: a streaming caller that reuses its output buffers across
+    batches; `fresh_ms_per_step`: new output arrays every call, as
+    Context.forward_host allocates them (page faults in the call, the previous
+    result's free in the loop: the host's mmap/munmap cost, not the link's)."""
+    import numpy as np
     import torch
     pinned = torch.empty(b.cells_dev.numel(), dtype=b.cells_dev.dtype, pin_memory=True)
     pinned.copy_(b.cells_dev)
     torch.cuda.synchronize()
     arr = pinned.numpy()
-    payload, offs, _ = ctx.forward_host(arr, b.tab, b.n, b.keep)  # warm-up: host staging buffers
     steps = max(1, min(args.leg_steps, 5))
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        payload, offs, _ = ctx.forward_host(arr, b.tab, b.n, b.keep)
-    ms = (time.perf_counter() - t0) / steps * 1e3
+    bufs = (np.empty(b.capi.payload_bound(b.tab, b.n), np.uint8), np.zeros(b.n + 1, np.uint64),
+            np.zeros(max(b.n, 1), np.uint32))
+    out = np.zeros(arr.size, np.float32)
+
+    def timed(fn):
+        fn()  # warm-up: host staging buffers, destination pages
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        return (time.perf_counter() - t0) / steps * 1e3
+
+    ms = timed(lambda: ctx.forward_host(arr, b.tab, b.n, b.keep, out=bufs))
+    payload, offs = bufs[0], bufs[1]
     h2d = arr.nbytes
     d2h = int(offs[b.n])
-    # wc_inverse_host over the same payloads (host bytes in, fp32 boxes out to host memory)
-    ctx.inverse_host(payload, offs[:b.n], b.tab, b.n, arr.size)  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        ctx.inverse_host(payload, offs[:b.n], b.tab, b.n, arr.size)
-    ims = (time.perf_counter() - t0) / steps * 1e3
+    ims = timed(lambda: ctx.inverse_host(payload, offs[:b.n], b.tab, b.n, arr.size, out=out))
+    # fresh result arrays per call (the previous call's freed inside the loop)
+    res = {}
+    fms = timed(lambda: res.update(r=ctx.forward_host(arr, b.tab, b.n, b.keep)))
+    fims = timed(lambda: res.update(o=ctx.inverse_host(payload, offs[:b.n], b.tab, b.n, arr.size)))
+    assert np.array_equal(res["r"][0][:d2h + 4], payload[:d2h + 4]) and np.array_equal(res["o"], out[:arr.size])
+    del res
     return {"value": b.ncells / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
             "h2d_bytes": h2d, "d2h_bytes": d2h, "host_GBps": (h2d + d2h) / (ms * 1e-3) / 1e9,
+            "fresh_ms_per_step": fms,
             "inverse": {"value": b.ncells / (ims * 1e-3), "unit": "cells/s", "ms_per_step": ims,
                         "h2d_bytes": d2h, "d2h_bytes": 4 * b.ncells,
-                        "host_GBps": (d2h + 4 * b.ncells) / (ims * 1e-3) / 1e9},
-            "note": "PCIe-inclusive (pinned host cells in, packed payloads out to host memory), one rank; "
+                        "host_GBps": (d2h + 4 * b.ncells) / (ims * 1e-3) / 1e9, "fresh_ms_per_step": fims},
+            "link_bound_ms": {"forward": h2d / 57e9 * 1e3, "inverse": 4 * b.ncells / 57e9 * 1e3,
+                              "note": "bytes of the larger direction / 57 GB/s (the box's measured PCIe rate "
+                                      "per direction, profiles/r04/experiments/gpu_pcie.txt)"},
+            "note": "PCIe-inclusive (pinned host cells in, packed payloads out to reused pageable host buffers), "
+                    "one rank; fresh_ms_per_step allocates new result arrays per call; "
                     "`value` above is the HBM-resident rate"}
 
 

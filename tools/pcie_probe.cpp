@@ -109,6 +109,85 @@ int main() {
     CK(hipMemset(dev_down, 4, boxes));
     CK(hipDeviceSynchronize());
 
+    if (std::getenv("PCIE_PROBE_FREE")) {
+        // what freeing a destination costs: populated only, after a pageable
+        // D2H into it (the runtime pins pageable pages for its DMA), after a
+        // D2H into pinned bounce chunks + threaded memcpy into it
+        const size_t chunk = size_t(64) << 20;
+        char* bounce[2];
+        CK(hipHostMalloc((void**)&bounce[0], chunk, hipHostMallocDefault));
+        CK(hipHostMalloc((void**)&bounce[1], chunk, hipHostMallocDefault));
+        for (int rep = 0; rep < 3; ++rep) {
+            for (int mode = 0; mode < 3; ++mode) {
+                char* f = fresh(boxes, true);
+                prefault(f, boxes, 16);
+                double c = 0;
+                if (mode == 1) {
+                    c = copy_once(f, dev_down, boxes, hipMemcpyDeviceToHost, a);
+                } else if (mode == 2) {
+                    const double t0 = now();
+                    for (size_t o = 0, k = 0; o < boxes; o += chunk, ++k) {
+                        const size_t len = std::min(chunk, boxes - o);
+                        char* bb = bounce[k & 1];
+                        CK(hipMemcpyAsync(bb, (char*)dev_down + o, len, hipMemcpyDeviceToHost, a));
+                        CK(hipStreamSynchronize(a));
+                        par_memcpy(f + o, bb, len, 16);
+                    }
+                    c = now() - t0;
+                }
+                const double t0 = now();
+                munmap(f, boxes);
+                const double t1 = now();
+                const char* names[] = {"munmap 1.07 GB populated only", "munmap 1.07 GB after pageable d2h",
+                                       "munmap 1.07 GB after bounce d2h (serial, T=16)"};
+                if (mode) report(mode == 1 ? "  pageable d2h" : "  bounce d2h serial", boxes, c);
+                report(names[mode], boxes, t1 - t0);
+            }
+        }
+        return 0;
+    }
+    if (std::getenv("PCIE_PROBE_H2D")) {
+        // pageable sources as a caller has them (a new buffer each call, written
+        // by the caller), straight vs through pinned bounce chunks filled by T
+        // threads while the previous chunk's DMA runs
+        const size_t chunk = size_t(64) << 20;
+        char* bounce[2];
+        CK(hipHostMalloc((void**)&bounce[0], chunk, hipHostMallocDefault));
+        CK(hipHostMalloc((void**)&bounce[1], chunk, hipHostMallocDefault));
+        hipEvent_t done[2];
+        CK(hipEventCreateWithFlags(&done[0], hipEventDisableTiming));
+        CK(hipEventCreateWithFlags(&done[1], hipEventDisableTiming));
+        for (int rep = 0; rep < 3; ++rep) {
+            char* src = fresh(up, true);
+            prefault(src, up, 16);
+            std::memset(src, 5 + rep, up);
+            report("h2d pageable new+written 2.15 GB", up, copy_once(dev_up, src, up, hipMemcpyHostToDevice, a));
+            report("h2d pageable same again", up, copy_once(dev_up, src, up, hipMemcpyHostToDevice, a));
+            munmap(src, up);
+            for (int T : {4, 8, 16}) {
+                src = fresh(up, true);
+                prefault(src, up, 16);
+                std::memset(src, 9 + rep, up);
+                CK(hipDeviceSynchronize());
+                const double t0 = now();
+                size_t k = 0;
+                for (size_t o = 0; o < up; o += chunk, ++k) {
+                    const size_t len = std::min(chunk, up - o);
+                    char* bb = bounce[k & 1];
+                    if (k >= 2) CK(hipEventSynchronize(done[k & 1]));
+                    par_memcpy(bb, src + o, len, T);
+                    CK(hipMemcpyAsync((char*)dev_up + o, bb, len, hipMemcpyHostToDevice, a));
+                    CK(hipEventRecord(done[k & 1], a));
+                }
+                CK(hipStreamSynchronize(a));
+                char name[96];
+                std::snprintf(name, sizeof name, "h2d via 2 x 64 MiB pinned bounce, T=%d memcpy", T);
+                report(name, up, now() - t0);
+                munmap(src, up);
+            }
+        }
+        return 0;
+    }
     for (int rep = 0; rep < 2; ++rep) {
         for (bool huge : {false, true}) {
             for (size_t sz : {down, boxes}) {

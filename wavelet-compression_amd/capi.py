@@ -262,16 +262,27 @@ class Context:
                                     units, n, ctypes.c_void_p(d_rmse)))
 
     # ---- host-array API ---------------------------------------------------
-    def forward_host(self, cells: np.ndarray, units, n: int, keep: float):
-        """cells: flat host array (float32 or float64) -> (payload bytes, offsets, kept)."""
+    def forward_host(self, cells: np.ndarray, units, n: int, keep: float, out=None):
+        """cells: flat host array (float32 or float64) -> (payload bytes, offsets, kept).
+        out: optional (payload uint8[>= payload_bound], offsets uint64[n + 1],
+        kept uint32[>= n]) to fill instead of new arrays (a caller that streams
+        batches reuses its buffers: no page faults, no frees per call)."""
         c = np.ascontiguousarray(cells)
         dtype = WC_F64 if c.dtype == np.float64 else WC_F32
         if c.dtype not in (np.float32, np.float64):
             raise TypeError("cells must be float32 or float64")
         cap = payload_bound(units, n)
-        payload = np.empty(cap, np.uint8)
-        offsets = np.zeros(n + 1, np.uint64)
-        kept = np.zeros(max(n, 1), np.uint32)
+        if out is None:
+            payload = np.empty(cap, np.uint8)
+            offsets = np.zeros(n + 1, np.uint64)
+            kept = np.zeros(max(n, 1), np.uint32)
+        else:
+            payload, offsets, kept = out
+            if (payload.dtype != np.uint8 or payload.size < cap or not payload.flags.c_contiguous
+                    or offsets.dtype != np.uint64 or offsets.size < n + 1 or not offsets.flags.c_contiguous
+                    or kept.dtype != np.uint32 or kept.size < n or not kept.flags.c_contiguous):
+                raise ValueError("out: (uint8[>= payload_bound], uint64[n + 1], uint32[n]) contiguous arrays")
+            cap = payload.size
         self._check(self._L.wc_forward_host(self._h, c.ctypes.data, dtype, units, n, float(keep),
                                             payload.ctypes.data, cap, offsets.ctypes.data,
                                             kept.ctypes.data))
@@ -298,10 +309,14 @@ class Context:
         self._check(self._L.wc_rmse_host(self._h, o.ctypes.data, dtype, r.ctypes.data, units, n, out.ctypes.data))
         return out[:n]
 
-    def inverse_host(self, payload: np.ndarray, offsets: np.ndarray, units, n: int, extent: int):
+    def inverse_host(self, payload: np.ndarray, offsets: np.ndarray, units, n: int, extent: int, out=None):
+        """-> float32[extent] boxes (cells no unit owns stay 0, or as they were in `out`)."""
         p = np.ascontiguousarray(payload, dtype=np.uint8)
         o = np.ascontiguousarray(offsets, dtype=np.uint64)
-        out = np.zeros(max(extent, 1), np.float32)
+        if out is None:
+            out = np.zeros(max(extent, 1), np.float32)
+        elif out.dtype != np.float32 or out.size < extent or not out.flags.c_contiguous:
+            raise ValueError("out: contiguous float32[>= extent]")
         self._check(self._L.wc_inverse_host(self._h, p.ctypes.data, o.ctypes.data, units, n,
                                             out.ctypes.data))
         return out[:extent]

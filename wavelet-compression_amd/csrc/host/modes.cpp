@@ -19,6 +19,7 @@
 #include <filesystem>
 #include <fstream>
 #include <future>
+#include <memory>
 #include <mutex>
 #include <numeric>
 #include <thread>
@@ -198,7 +199,9 @@ void load_chunk(const RunIndex& r, Chunk& c, int threads) {
 }
 
 struct Packed {
-    std::vector<uint8_t> payload;
+    // worst-case sized (every coefficient kept) and only partly written: not
+    // zero-filled (a std::vector would memset the whole bound, 8 B per cell)
+    std::unique_ptr<uint8_t[]> payload;
     std::vector<uint64_t> offsets;
     std::vector<uint32_t> kept;
 };
@@ -206,12 +209,13 @@ struct Packed {
 Packed forward_chunk(const Chunk& c, double keep) {
     Packed p;
     const int n = (int)c.units.size();
-    p.payload.resize(wc_payload_bound(c.units.data(), n));
+    const uint64_t cap = wc_payload_bound(c.units.data(), n);
+    p.payload.reset(new uint8_t[cap]);
     p.offsets.resize(n + 1);
     p.kept.resize(n);
     wc_ctx* ctx = thread_ctx();
-    check(ctx, wc_forward_host(ctx, c.cells.data(), WC_F64, c.units.data(), n, keep, p.payload.data(),
-                               p.payload.size(), p.offsets.data(), p.kept.data()),
+    check(ctx, wc_forward_host(ctx, c.cells.data(), WC_F64, c.units.data(), n, keep, p.payload.get(), cap,
+                               p.offsets.data(), p.kept.data()),
           "GPU forward");
     return p;
 }
@@ -256,7 +260,7 @@ void compress_run(const RunIndex& r, double keep, const std::filesystem::path& d
             for (size_t k = 0; k < nc; ++k) {
                 const size_t u = i * nc + k;
                 const BoxRef& b = c.boxes[i];
-                jobs.push_back(XzJob{p.payload.data() + p.offsets[u], 20 + 8ull * p.kept[u],
+                jobs.push_back(XzJob{p.payload.get() + p.offsets[u], 20 + 8ull * p.kept[u],
                                      (dir / unit_name(b.t, b.lev, r.comp_idxs[k], b.box)).string()});
             }
         return jobs;

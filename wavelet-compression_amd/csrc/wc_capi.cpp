@@ -16,6 +16,7 @@
 #include "wc_hostmem.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -25,6 +26,8 @@
 #include <mutex>
 #include <string>
 #include <vector>
+#include <thread>
+#include <condition_variable>
 
 namespace wc {
 size_t transform_lds_bytes(int lbx, int lby, int lbz);
@@ -1525,6 +1528,20 @@ static std::vector<int> host_runs(const wc_ctx* c, const wc_unit* units, int n) 
     return rb;
 }
 
+// WCAMD_HOST_TRACE=1: the _host calls print their host-side timeline (ms
+// since the call began) to stderr.  Diagnostic.
+struct HostTrace {
+    const bool on = std::getenv("WCAMD_HOST_TRACE") != nullptr;
+    const std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    const char* call;
+    explicit HostTrace(const char* name) : call(name) {}
+    void operator()(const char* what, int r = -1) const {
+        if (!on) return;
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        std::fprintf(stderr, "[%s] %8.2f ms %s %d\n", call, ms, what, r);
+    }
+};
+
 // WC_OPT_HOST_THREADS unset: the job's CPU share (OMP_NUM_THREADS, 16 per GPU
 // on the MI355X boxes, where nproc shows the whole host) or the cores, <= 16.
 static int host_threads_default() {
@@ -1534,14 +1551,101 @@ static int host_threads_default() {
     return std::clamp(t, 1, 16);
 }
 
-// Fault in the pages of a host destination before a device-to-host copy lands
-// there (wc_hostmem.h: the copy's own thread faults at 12–20 GB/s).
-static void host_populate(wc_ctx* c, void* p, size_t bytes) {
+// Faulting in the pages of a host destination before a device-to-host copy
+// lands there (wc_hostmem.h: the copy's own thread faults at 12–20 GB/s).
+// Resolved on the call's thread before any helper thread starts; null = off.
+struct Populate {
+    wc::HostPool* pool = nullptr;
+    bool on = false, thp = true;
+    void operator()(void* p, size_t bytes) const {
+        if (on && bytes) wc::populate_for_write(pool, p, bytes, thp);
+    }
+};
+
+static Populate host_populate(wc_ctx* c) {
     if (c->opt_host_threads < 0) c->opt_host_threads = host_threads_default();
-    if (c->opt_host_threads == 0 || bytes == 0) return;
+    Populate P;
+    if (c->opt_host_threads == 0) return P;
     if (!c->hpool || c->hpool->threads() != c->opt_host_threads)
         c->hpool = std::make_unique<wc::HostPool>(c->opt_host_threads - 1);
-    wc::populate_for_write(c->hpool.get(), p, bytes, c->opt_host_thp);
+    P.pool = c->hpool.get();
+    P.on = true;
+    P.thp = c->opt_host_thp;
+    return P;
+}
+
+// Progress of a pipelined _host call's runs, published by one thread and
+// awaited by another: a copy from or to pageable host memory returns only
+// when it is done, so the uploads (the call's thread) and the downloads (a
+// helper thread) of different runs overlap only from different threads.
+class RunGate {
+public:
+    void publish(int runs) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            done_ = runs;
+        }
+        cv_.notify_all();
+    }
+    void cancel() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            cancelled_ = true;
+        }
+        cv_.notify_all();
+    }
+    bool wait(int r) {  // false: cancelled before run r was published
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return done_ > r || cancelled_; });
+        return done_ > r;
+    }
+
+private:
+    std::mutex mu_;
+    std::condition_variable cv_;
+    int done_ = 0;
+    bool cancelled_ = false;
+};
+
+// What a helper thread of a _host call ran into (applied to the context by
+// the call's thread once the helper has joined).
+struct HelperStatus {
+    int rc = WC_OK;
+    std::string msg;
+    void hip(hipError_t e, const char* what) {
+        if (rc == WC_OK) {
+            rc = WC_ERR_HIP;
+            msg = std::string(what) + ": " + hipGetErrorString(e);
+        }
+    }
+    void invalid(const char* what) {
+        if (rc == WC_OK) {
+            rc = WC_ERR_INVALID;
+            msg = what;
+        }
+    }
+};
+
+// Runs `body` on a helper thread (bound to the context's device) when the
+// call has more than one run, else on the call's thread after `main`.
+extern "C++" {
+template <class Main, class Body>
+static int with_helper(wc_ctx* c, int nr, RunGate& gate, HelperStatus& hs, Main main, Body body) {
+    std::thread helper;
+    if (nr > 1)
+        helper = std::thread([&] {
+            hipError_t e = hipSetDevice(c->device);
+            if (e != hipSuccess) return hs.hip(e, "hipSetDevice (helper)");
+            body();
+        });
+    const int rc = main();
+    if (rc != WC_OK) gate.cancel();
+    if (helper.joinable()) helper.join();
+    else if (rc == WC_OK) body();
+    if (rc != WC_OK) return rc;
+    if (hs.rc != WC_OK) return fail(c, hs.rc, hs.msg);
+    return WC_OK;
+}
 }
 
 // The copy streams (when there is more than one run) and 2 events per run.
@@ -1573,6 +1677,7 @@ static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_u
     if ((rc = set_device(c))) return rc;
     const size_t esz = dtype == WC_F64 ? 8 : 4;
     const uint64_t ext = cells_extent(units, n);
+    const HostTrace mark("forward_host");
 
     // Runs of contiguous units of about opt_host_chunk cells (at most 16),
     // pipelined: run r's cells upload on `up` while run r-1 computes on the
@@ -1602,61 +1707,86 @@ static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_u
     uint64_t* pin_poff = (uint64_t*)c->pinned;                   // [n + nr]
     uint32_t* pin_kept = (uint32_t*)(pin_poff + (n + nr));       // [n]
     uint8_t* d_cells = (uint8_t*)c->h_cells.p;
-    for (int r = 0; r < nr; ++r) {
-        const int a = rb[r], m = rb[r + 1] - rb[r];
-        uint64_t lo = UINT64_MAX, hi = 0;
-        for (int i = a; i < a + m; ++i) {
-            const uint64_t cnt = (uint64_t)units[i].nx * units[i].ny * units[i].nz;
-            if (!cnt) continue;
-            lo = std::min(lo, units[i].cell_offset);
-            hi = std::max(hi, units[i].cell_offset + cnt);
+    const Populate populate = host_populate(c);
+    RunGate gate;
+    HelperStatus hs;
+    uint64_t R = 4;  // run r's packed bytes [4, end) land at R (== 4 mod 8); the next run starts at R + end
+    // The call's thread: uploads, kernels, each run's sizes to pinned memory.
+    auto enqueue = [&]() -> int {
+        for (int r = 0; r < nr; ++r) {
+            const int a = rb[r], m = rb[r + 1] - rb[r];
+            uint64_t lo = UINT64_MAX, hi = 0;
+            for (int i = a; i < a + m; ++i) {
+                const uint64_t cnt = (uint64_t)units[i].nx * units[i].ny * units[i].nz;
+                if (!cnt) continue;
+                lo = std::min(lo, units[i].cell_offset);
+                hi = std::max(hi, units[i].cell_offset + cnt);
+            }
+            hipStream_t cs = nr > 1 ? c->up : c->stream;
+            hipError_t e;
+            if (hi > lo &&
+                (e = hipMemcpyAsync(d_cells + esz * lo, (const uint8_t*)cells + esz * lo, esz * (hi - lo),
+                                    hipMemcpyHostToDevice, cs)) != hipSuccess)
+                return hip_fail(c, e, "cells upload");
+            if (nr > 1 && ((e = hipEventRecord(c->hev[2 * r], c->up)) != hipSuccess ||
+                           (e = hipStreamWaitEvent(c->stream, c->hev[2 * r], 0)) != hipSuccess))
+                return hip_fail(c, e, "upload event");
+            uint8_t* pay = (uint8_t*)c->h_payload.p + pbase[r];
+            uint8_t* packed = (uint8_t*)c->h_packed.p + pbase[r];
+            uint64_t* doff = (uint64_t*)c->h_offsets.p + (a + r);
+            uint64_t* dpoff = (uint64_t*)c->h_poff.p + (a + r);
+            uint32_t* dkept = (uint32_t*)c->h_kept.p + a;
+            int rc2;
+            if ((rc2 = wc_forward(c, c->h_cells.p, dtype, units + a, m, keep, pay, pbase[r + 1] - pbase[r], doff,
+                                  dkept)))
+                return rc2;
+            // Pack the slots densely (offsets stay == 4 mod 8), sizes to pinned memory.
+            e = launch_pack(c->stream, (const UnitDev*)c->plan.d_units.p, m, dkept, pay, dpoff, packed);
+            if (e != hipSuccess) return hip_fail(c, e, "pack launch");
+            if ((e = hipMemcpyAsync(pin_poff + (a + r), dpoff, sizeof(uint64_t) * (m + 1), hipMemcpyDeviceToHost,
+                                    c->stream)) != hipSuccess ||
+                (e = hipMemcpyAsync(pin_kept + a, dkept, 4ull * m, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+                (e = hipEventRecord(c->hev[2 * r + 1], c->stream)) != hipSuccess)
+                return hip_fail(c, e, "sizes readback");
+            gate.publish(r + 1);
         }
-        hipStream_t cs = nr > 1 ? c->up : c->stream;
-        if (hi > lo &&
-            (e = hipMemcpyAsync(d_cells + esz * lo, (const uint8_t*)cells + esz * lo, esz * (hi - lo),
-                                hipMemcpyHostToDevice, cs)) != hipSuccess)
-            return hip_fail(c, e, "cells upload");
-        if (nr > 1 && ((e = hipEventRecord(c->hev[2 * r], c->up)) != hipSuccess ||
-                       (e = hipStreamWaitEvent(c->stream, c->hev[2 * r], 0)) != hipSuccess))
-            return hip_fail(c, e, "upload event");
-        uint8_t* pay = (uint8_t*)c->h_payload.p + pbase[r];
-        uint8_t* packed = (uint8_t*)c->h_packed.p + pbase[r];
-        uint64_t* doff = (uint64_t*)c->h_offsets.p + (a + r);
-        uint64_t* dpoff = (uint64_t*)c->h_poff.p + (a + r);
-        uint32_t* dkept = (uint32_t*)c->h_kept.p + a;
-        if ((rc = wc_forward(c, c->h_cells.p, dtype, units + a, m, keep, pay, pbase[r + 1] - pbase[r], doff, dkept)))
-            return rc;
-        // Pack the slots densely (offsets stay == 4 mod 8), sizes to pinned memory.
-        e = launch_pack(c->stream, (const UnitDev*)c->plan.d_units.p, m, dkept, pay, dpoff, packed);
-        if (e != hipSuccess) return hip_fail(c, e, "pack launch");
-        if ((e = hipMemcpyAsync(pin_poff + (a + r), dpoff, sizeof(uint64_t) * (m + 1), hipMemcpyDeviceToHost,
-                                c->stream)) != hipSuccess ||
-            (e = hipMemcpyAsync(pin_kept + a, dkept, 4ull * m, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
-            (e = hipEventRecord(c->hev[2 * r + 1], c->stream)) != hipSuccess)
-            return hip_fail(c, e, "sizes readback");
-    }
-    // Each run's packed bytes [4, end) land at R (== 4 mod 8); the next run starts at R + end.
-    uint64_t R = 4;
-    for (int r = 0; r < nr; ++r) {
-        const int a = rb[r], m = rb[r + 1] - rb[r];
-        if ((e = hipEventSynchronize(c->hev[2 * r + 1])) != hipSuccess) return hip_fail(c, e, "sizes sync");
-        const uint64_t* po = pin_poff + (a + r);
-        for (int i = 0; i < m; ++i) {
-            offsets[a + i] = R - 4 + po[i];
-            kept[a + i] = pin_kept[a + i];
-        }
-        const uint64_t span = po[m] - 4;
-        if (R - 4 + po[m] > cap) return fail(c, WC_ERR_INVALID, "payload_capacity");
+        mark("enqueued", nr);
+        return WC_OK;
+    };
+    // The helper (or, with one run, the call's thread afterwards): each run's
+    // sizes, offsets and kept counts, then its packed payloads to the caller.
+    auto download = [&] {
         hipStream_t ds = nr > 1 ? c->down : c->stream;
-        host_populate(c, payload + R, span);
-        if (span && (e = hipMemcpyAsync(payload + R, (const uint8_t*)c->h_packed.p + pbase[r] + 4, span,
-                                        hipMemcpyDeviceToHost, ds)) != hipSuccess)
-            return hip_fail(c, e, "payload readback");
-        R += po[m];
-    }
+        for (int r = 0; r < nr; ++r) {
+            if (!gate.wait(r)) return;
+            const int a = rb[r], m = rb[r + 1] - rb[r];
+            hipError_t e;
+            if ((e = hipEventSynchronize(c->hev[2 * r + 1])) != hipSuccess) return hs.hip(e, "sizes sync");
+            mark("sizes", r);
+            const uint64_t* po = pin_poff + (a + r);
+            for (int i = 0; i < m; ++i) {
+                offsets[a + i] = R - 4 + po[i];
+                kept[a + i] = pin_kept[a + i];
+            }
+            const uint64_t span = po[m] - 4;
+            if (R - 4 + po[m] > cap) return hs.invalid("payload_capacity");
+            populate(payload + R, span);
+            mark("populated", r);
+            if (span && (e = hipMemcpyAsync(payload + R, (const uint8_t*)c->h_packed.p + pbase[r] + 4, span,
+                                            hipMemcpyDeviceToHost, ds)) != hipSuccess)
+                return hs.hip(e, "payload readback");
+            mark("d2h issued", r);
+            R += po[m];
+        }
+        hipError_t e;
+        if (nr > 1 && (e = hipStreamSynchronize(c->down)) != hipSuccess) return hs.hip(e, "payload readback");
+        mark("down synced");
+    };
+    if ((rc = with_helper(c, nr, gate, hs, enqueue, download))) return rc;
     offsets[n] = R - 4;
-    if (nr > 1 && (e = hipStreamSynchronize(c->down)) != hipSuccess) return hip_fail(c, e, "payload readback");
-    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(c, e, "sync");
+    hipError_t e2;
+    if ((e2 = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(c, e2, "sync");
+    mark("done");
     return check_kernel_errors(c);
 }
 
@@ -1687,59 +1817,107 @@ static int inverse_host_once(wc_ctx* c, const uint8_t* payload, const uint64_t* 
     std::vector<int> rb = host_runs(c, units, n);
     const int nr = (int)rb.size() - 1;
     hipError_t e;
+    const HostTrace mark("inverse_host");
     if ((rc = host_streams(c, nr))) return rc;
     if ((e = hipMemcpyAsync(c->h_offsets.p, offsets, sizeof(uint64_t) * n, hipMemcpyHostToDevice, c->stream)) !=
         hipSuccess)
         return hip_fail(c, e, "offsets upload");
+    // Each run's boxes go back as one copy per span of back-to-back units:
+    // exactly the cells the units own (the caller's buffer may have gaps).
+    struct Span {
+        int run;
+        uint64_t lo, hi;  // cells
+    };
+    std::vector<Span> spans;
+    std::vector<int> first_span(nr + 1, 0);
     for (int r = 0; r < nr; ++r) {
-        const int a = rb[r], m = rb[r + 1] - rb[r];
-        uint64_t lo = UINT64_MAX, hi = 0;
-        for (int i = a; i < a + m; ++i) {
-            int32_t cnt;
-            std::memcpy(&cnt, payload + offsets[i] + 16, 4);
-            lo = std::min(lo, offsets[i]);
-            hi = std::max(hi, offsets[i] + 20 + 8 * (uint64_t)cnt);
-        }
-        hipStream_t us = nr > 1 ? c->up : c->stream;
-        if (hi > lo && (e = hipMemcpyAsync((uint8_t*)c->h_payload.p + lo, payload + lo, hi - lo,
-                                           hipMemcpyHostToDevice, us)) != hipSuccess)
-            return hip_fail(c, e, "payload upload");
-        if (nr > 1 && ((e = hipEventRecord(c->hev[2 * r], c->up)) != hipSuccess ||
-                       (e = hipStreamWaitEvent(c->stream, c->hev[2 * r], 0)) != hipSuccess))
-            return hip_fail(c, e, "upload event");
-        if ((rc = wc_inverse(c, (const uint8_t*)c->h_payload.p, (const uint64_t*)c->h_offsets.p + a, units + a, m,
-                             (float*)c->h_out.p)))
-            return rc;
-        if (nr > 1 && (e = hipEventRecord(c->hev[2 * r + 1], c->stream)) != hipSuccess)
-            return hip_fail(c, e, "decode event");
-    }
-    // Every upload and decode is queued; the boxes download run by run, each
-    // destination span faulted in just before its copy (host_populate).
-    for (int r = 0; r < nr; ++r) {
-        const int a = rb[r], m = rb[r + 1] - rb[r];
-        hipStream_t ds = nr > 1 ? c->down : c->stream;
-        if (nr > 1 && (e = hipStreamWaitEvent(c->down, c->hev[2 * r + 1], 0)) != hipSuccess)
-            return hip_fail(c, e, "decode event");
-        // Copy back exactly the cells the units own (the caller's buffer may
-        // have gaps), one copy per span of back-to-back units.
-        for (int i = a; i < a + m;) {
+        first_span[r] = (int)spans.size();
+        for (int i = rb[r]; i < rb[r + 1];) {
             const uint64_t o = units[i].cell_offset;
             uint64_t end = o + (uint64_t)units[i].nx * units[i].ny * units[i].nz;
             int j = i + 1;
-            for (; j < a + m; ++j) {
+            for (; j < rb[r + 1]; ++j) {
                 const uint64_t cj = (uint64_t)units[j].nx * units[j].ny * units[j].nz;
                 if (cj && units[j].cell_offset != end) break;
                 end += cj;
             }
-            if (end > o) host_populate(c, out + o, sizeof(float) * (end - o));
-            if (end > o && (e = hipMemcpyAsync(out + o, (float*)c->h_out.p + o, sizeof(float) * (end - o),
-                                               hipMemcpyDeviceToHost, ds)) != hipSuccess)
-                return hip_fail(c, e, "box readback");
+            if (end > o) spans.push_back({r, o, end});
             i = j;
         }
     }
-    if (nr > 1 && (e = hipStreamSynchronize(c->down)) != hipSuccess) return hip_fail(c, e, "box readback");
+    first_span[nr] = (int)spans.size();
+    const Populate populate = host_populate(c);
+    RunGate gate, resident;
+    HelperStatus hs;
+    // The destination spans do not depend on the device: with several runs a
+    // thread of its own faults them in ahead of the downloads.
+    std::thread ahead;
+    if (populate.on && nr > 1)
+        ahead = std::thread([&] {
+            for (int r = 0; r < nr; ++r) {
+                for (int k = first_span[r]; k < first_span[r + 1]; ++k)
+                    populate(out + spans[k].lo, sizeof(float) * (spans[k].hi - spans[k].lo));
+                resident.publish(r + 1);
+            }
+        });
+    // The call's thread: payload uploads and decodes, run by run.
+    auto enqueue = [&]() -> int {
+        for (int r = 0; r < nr; ++r) {
+            const int a = rb[r], m = rb[r + 1] - rb[r];
+            uint64_t lo = UINT64_MAX, hi = 0;
+            for (int i = a; i < a + m; ++i) {
+                int32_t cnt;
+                std::memcpy(&cnt, payload + offsets[i] + 16, 4);
+                lo = std::min(lo, offsets[i]);
+                hi = std::max(hi, offsets[i] + 20 + 8 * (uint64_t)cnt);
+            }
+            hipStream_t us = nr > 1 ? c->up : c->stream;
+            hipError_t e;
+            if (hi > lo && (e = hipMemcpyAsync((uint8_t*)c->h_payload.p + lo, payload + lo, hi - lo,
+                                               hipMemcpyHostToDevice, us)) != hipSuccess)
+                return hip_fail(c, e, "payload upload");
+            if (nr > 1 && ((e = hipEventRecord(c->hev[2 * r], c->up)) != hipSuccess ||
+                           (e = hipStreamWaitEvent(c->stream, c->hev[2 * r], 0)) != hipSuccess))
+                return hip_fail(c, e, "upload event");
+            int rc2;
+            if ((rc2 = wc_inverse(c, (const uint8_t*)c->h_payload.p, (const uint64_t*)c->h_offsets.p + a, units + a,
+                                  m, (float*)c->h_out.p)))
+                return rc2;
+            if (nr > 1 && (e = hipEventRecord(c->hev[2 * r + 1], c->stream)) != hipSuccess)
+                return hip_fail(c, e, "decode event");
+            gate.publish(r + 1);
+        }
+        mark("enqueued", nr);
+        return WC_OK;
+    };
+    // The helper (or, with one run, the call's thread afterwards): each run's
+    // boxes to the caller once it is decoded and its spans are resident.
+    auto download = [&] {
+        hipStream_t ds = nr > 1 ? c->down : c->stream;
+        for (int r = 0; r < nr; ++r) {
+            if (!gate.wait(r)) return;
+            hipError_t e;
+            if (nr > 1 && (e = hipStreamWaitEvent(c->down, c->hev[2 * r + 1], 0)) != hipSuccess)
+                return hs.hip(e, "decode event");
+            if (ahead.joinable()) resident.wait(r);
+            for (int k = first_span[r]; k < first_span[r + 1]; ++k) {
+                const uint64_t o = spans[k].lo, bytes = sizeof(float) * (spans[k].hi - o);
+                if (!ahead.joinable()) populate(out + o, bytes);
+                if ((e = hipMemcpyAsync(out + o, (float*)c->h_out.p + o, bytes, hipMemcpyDeviceToHost, ds)) !=
+                    hipSuccess)
+                    return hs.hip(e, "box readback");
+            }
+            mark("d2h issued", r);
+        }
+        hipError_t e;
+        if (nr > 1 && (e = hipStreamSynchronize(c->down)) != hipSuccess) return hs.hip(e, "box readback");
+        mark("down synced");
+    };
+    rc = with_helper(c, nr, gate, hs, enqueue, download);
+    if (ahead.joinable()) ahead.join();
+    if (rc) return rc;
     if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(c, e, "sync");
+    mark("done");
     return check_kernel_errors(c);
 }
 
