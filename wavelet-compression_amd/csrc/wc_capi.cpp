@@ -1566,8 +1566,14 @@ static Populate host_populate(wc_ctx* c) {
     if (c->opt_host_threads < 0) c->opt_host_threads = host_threads_default();
     Populate P;
     if (c->opt_host_threads == 0) return P;
-    if (!c->hpool || c->hpool->threads() != c->opt_host_threads)
-        c->hpool = std::make_unique<wc::HostPool>(c->opt_host_threads - 1);
+    if (!c->hpool || c->hpool->threads() != c->opt_host_threads) {
+        c->hpool.reset();
+        try {
+            c->hpool = std::make_unique<wc::HostPool>(c->opt_host_threads - 1);
+        } catch (...) {  // no threads: the faults stay with the copies
+            return P;
+        }
+    }
     P.pool = c->hpool.get();
     P.on = true;
     P.thp = c->opt_host_thp;
@@ -1632,16 +1638,26 @@ extern "C++" {
 template <class Main, class Body>
 static int with_helper(wc_ctx* c, int nr, RunGate& gate, HelperStatus& hs, Main main, Body body) {
     std::thread helper;
-    if (nr > 1)
-        helper = std::thread([&] {
-            hipError_t e = hipSetDevice(c->device);
-            if (e != hipSuccess) return hs.hip(e, "hipSetDevice (helper)");
-            body();
-        });
+    if (nr > 1) {
+        try {
+            helper = std::thread([&] {
+                hipError_t e = hipSetDevice(c->device);
+                if (e != hipSuccess) return hs.hip(e, "hipSetDevice (helper)");
+                body();
+            });
+        } catch (...) {  // no thread: the body runs after main on this one
+        }
+    }
     const int rc = main();
     if (rc != WC_OK) gate.cancel();
     if (helper.joinable()) helper.join();
     else if (rc == WC_OK) body();
+    if (rc != WC_OK || hs.rc != WC_OK) {
+        // Copies queued before the failure may still read or write the
+        // caller's buffers: none may outlive the call.
+        for (hipStream_t st : {c->up, c->down, c->stream})
+            if (st) (void)hipStreamSynchronize(st);
+    }
     if (rc != WC_OK) return rc;
     if (hs.rc != WC_OK) return fail(c, hs.rc, hs.msg);
     return WC_OK;
@@ -1852,14 +1868,18 @@ static int inverse_host_once(wc_ctx* c, const uint8_t* payload, const uint64_t* 
     // The destination spans do not depend on the device: with several runs a
     // thread of its own faults them in ahead of the downloads.
     std::thread ahead;
-    if (populate.on && nr > 1)
-        ahead = std::thread([&] {
-            for (int r = 0; r < nr; ++r) {
-                for (int k = first_span[r]; k < first_span[r + 1]; ++k)
-                    populate(out + spans[k].lo, sizeof(float) * (spans[k].hi - spans[k].lo));
-                resident.publish(r + 1);
-            }
-        });
+    if (populate.on && nr > 1) {
+        try {
+            ahead = std::thread([&] {
+                for (int r = 0; r < nr; ++r) {
+                    for (int k = first_span[r]; k < first_span[r + 1]; ++k)
+                        populate(out + spans[k].lo, sizeof(float) * (spans[k].hi - spans[k].lo));
+                    resident.publish(r + 1);
+                }
+            });
+        } catch (...) {  // no thread: the downloads fault their spans in themselves
+        }
+    }
     // The call's thread: payload uploads and decodes, run by run.
     auto enqueue = [&]() -> int {
         for (int r = 0; r < nr; ++r) {
