@@ -127,6 +127,9 @@ static void params_case() {
 static void format_files_case() {
     TempDir dir;
     for (const char* n : {"plt00075", "plt00074", "plt00080", "plt00070", "notes"}) fs::create_directories(dir.path() / n);
+    // digits past INT_MAX saturate (the reference's std::stoi would throw)
+    REQUIRE(clean_string("/t/run9999999999/plt00074") == 2147483647);
+    REQUIRE(clean_string("plt2147483647") == 2147483647 && clean_string("x0002147483646") == 2147483646);
     // digits of the whole path count: use a digit-free temp root
     const auto files = format_files(slash(dir.path()), "plt00074", "plt00079");
     if (clean_string(dir.path().string()) != -1) return;  // temp path has digits: reference quirk, skip

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cctype>
 #include <filesystem>
+#include <limits>
 #include <map>
 #include <sstream>
 
@@ -129,7 +130,13 @@ int clean_string(std::string filename) {
     if (digits.empty()) return -1;
     const size_t nz = digits.find_first_not_of('0');
     if (nz == std::string::npos) return 0;
-    return std::stoi(digits.substr(nz));
+    // The reference's std::stoi throws std::out_of_range (an uncaught
+    // terminate) once the digits pass INT_MAX, which the digits of a whole
+    // path easily do (a temp directory's random name): saturate instead, so
+    // such a path simply matches no time range.
+    const std::string d = digits.substr(nz);
+    if (d.size() > 10 || (d.size() == 10 && d > "2147483647")) return std::numeric_limits<int>::max();
+    return std::stoi(d);
 }
 
 std::vector<std::string> format_files(std::string data_dir, std::string min_time, std::string max_time) {
