@@ -5,8 +5,9 @@ src/compressor.cpp:192-248 per box, src/modes.cpp:100-103):
   * every unit: header (W, H, D, ncoeff, nrle), 0 <= kept <= ncoeff, and the
     worst-case slot offsets;
   * payload bytes equal the oracle's on 10 units (first, last, random ones);
-  * the staged two-kernel path and the cohort forward (WC_OPT_COHORT) write
-    identical bytes for ALL 512 units (zeroed payload buffers compared whole);
+  * the staged two-kernel path, the cohort forward (WC_OPT_COHORT) and the
+    look-backs' ticket form write identical bytes for ALL 512 units (zeroed
+    payload buffers compared whole; the stage timers show which path ran);
   * wc_inverse of the whole batch reproduces the oracle's decompress()
     (rle_decode + inverse_wavelet_decompose, src/decompressor.cpp:14-159) on 2
     sampled units bit for bit.
@@ -21,7 +22,10 @@ KEEP = float(np.float32(0.9999))
 
 
 @pytest.fixture(scope="module")
-def c5_run(wc):
+def c5_run(wc, ctx):
+    """The session context: the ONLY live context, so the launch-order form
+    (and with it the cohort forward) is the one that runs; a second live
+    context would switch both to the ticket form."""
     import torch
     import bench_workloads as bw
     units = bw.WORKLOADS["c5"]["units"]()
@@ -29,7 +33,6 @@ def c5_run(wc):
     dev = torch.device("cuda", 0)
     cells, offs, extent = bw.synth_cells(torch, dev, units, "f32")
     tab, n, _ = bw.units_array(wc.capi, units, offs)
-    ctx = wc.capi.Context(0)
     cap = wc.capi.payload_bound(tab, n)
     payload = torch.zeros(cap, dtype=torch.uint8, device=dev)
     offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
@@ -42,7 +45,6 @@ def c5_run(wc):
              offsets=offsets.cpu().numpy(), kept=kept.cpu().numpy(), tab=tab, n=n, ctx=ctx, dev=dev, cap=cap,
              extent=extent)
     yield r
-    ctx.close()
     del r, cells, payload
     torch.cuda.empty_cache()
 
@@ -87,24 +89,39 @@ def test_c5_payloads_match_oracle(c5_run, oracle):
         assert int(r["kept"][i]) == k
 
 
-@pytest.mark.parametrize("cohort,lag", [(0, 2), (2, 2), (4, 1)])
-def test_c5_paths_identical_all_units(c5_run, wc, cohort, lag):
+@pytest.mark.parametrize("cohort,lag,ordered,stage", [(0, 2, 1, "emit"), (2, 2, 1, "cohort"), (4, 1, 1, "cohort"),
+                                                     (4, 1, 0, "emit")])
+def test_c5_paths_identical_all_units(c5_run, wc, cohort, lag, ordered, stage):
     """The default path's bytes for all 512 units against the staged two-kernel
-    path (cohort 0) and the cohort forward: whole zeroed buffers compared."""
+    path (cohort 0), the cohort forward, and the look-backs' ticket form
+    (WC_OPT_ORDERED 0: the two-kernel path): whole zeroed buffers compared.
+    The stage timers show which path ran."""
     import torch
+    from wavelet_compression_amd.capi import WC_OPT_ORDERED
     r = c5_run
+    c = r["ctx"]
     other = torch.zeros_like(r["payload"])
     offs = torch.zeros_like(r["offsets_dev"])
     kept = torch.zeros(r["n"], dtype=torch.int32, device=r["dev"])
-    c = wc.capi.Context(0)
+    # torch filled these on its own stream; the context's stream does not wait
+    # for it (round 4: a fill still running zeroed the tail units' kept counts)
+    torch.cuda.synchronize()
     try:
         c.set_option(WC_OPT_COHORT, cohort)
         c.set_option(WC_OPT_COHORT_LAG, lag)
+        c.set_option(WC_OPT_ORDERED, ordered)
+        c.profile_enable(True)
+        c.profile_read()
         c.forward(r["cells"].data_ptr(), wc.capi.WC_F32, r["tab"], r["n"], KEEP, other.data_ptr(), r["cap"],
                   offs.data_ptr(), kept.data_ptr())
         c.synchronize()
+        stages = c.profile_read()
     finally:
-        c.close()
+        c.profile_enable(False)
+        c.set_option(WC_OPT_COHORT, 0)
+        c.set_option(WC_OPT_COHORT_LAG, 2)
+        c.set_option(WC_OPT_ORDERED, 1)
+    assert stage in stages and ("cohort" if stage == "emit" else "emit") not in stages, stages
     assert np.array_equal(kept.cpu().numpy(), r["kept"])
     assert np.array_equal(offs.cpu().numpy(), r["offsets"])
     assert torch.equal(other, r["payload"])
@@ -116,6 +133,7 @@ def test_c5_inverse_sampled_units_match_oracle(c5_run, oracle):
     import torch
     r = c5_run
     regen = torch.empty(r["extent"], dtype=torch.float32, device=r["dev"])
+    torch.cuda.synchronize()
     r["ctx"].inverse(r["payload"].data_ptr(), r["offsets_dev"].data_ptr(), r["tab"], r["n"], regen.data_ptr())
     r["ctx"].synchronize()
     for i in (1, r["n"] - 2):

@@ -124,11 +124,14 @@ def test_cohort_not_taken_in_ticket_form(wc, ctx, oracle, batch):
     assert got[3] == oracle.compress_payload(boxes[3].astype(np.float32), KEEPS[1])[0]
 
 
-def test_cohort_wait_timeout_reported_then_exact(wc, oracle):
+def test_cohort_wait_timeout_reported_then_exact(wc, ctx, oracle):
     """WC_OPT_SPIN_LIMIT 1: the first unanswered poll of a cohort wait fails;
     the call reports WC_ERR_HIP (no hang, no out-of-range access), and the
-    next call with the default bound is exact."""
+    next call with the default bound is exact.  On the session context (the
+    only live one: a second context would take the ticket form, not the
+    cohort); the timeout makes the ticket form sticky, reset afterwards."""
     import torch
+    from wavelet_compression_amd.capi import WC_OPT_TICKETS
     boxes = _boxes(oracle, 6, 29)
     units, n, host = _pack(wc, boxes, np.float32)
     dev = torch.device("cuda", 0)
@@ -137,11 +140,14 @@ def test_cohort_wait_timeout_reported_then_exact(wc, oracle):
     payload = torch.zeros(cap, dtype=torch.uint8, device=dev)
     offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     kept = torch.zeros(n, dtype=torch.int32, device=dev)
-    c = wc.capi.Context(0)
+    torch.cuda.synchronize()  # the fills above run on torch's stream, the context on its own
+    c = ctx
     try:
         c.set_option(WC_OPT_COHORT, 1)
         c.set_option(WC_OPT_COHORT_LAG, 1)
         c.set_option(WC_OPT_SPIN_LIMIT, 1)
+        c.profile_enable(True)
+        c.profile_read()
         seen = False
         for _ in range(4):
             c.forward(cells.data_ptr(), wc.capi.WC_F32, units, n, KEEPS[0], payload.data_ptr(), cap,
@@ -152,14 +158,21 @@ def test_cohort_wait_timeout_reported_then_exact(wc, oracle):
                 assert e.code == wc.capi.WC_ERR_HIP and "timed out" in str(e), e
                 seen = True
                 break
+        assert "cohort" in c.profile_read()
         c.set_option(WC_OPT_SPIN_LIMIT, 0)
+        c.set_option(WC_OPT_TICKETS, 0)
         c.forward(cells.data_ptr(), wc.capi.WC_F32, units, n, KEEPS[0], payload.data_ptr(), cap,
                   offsets.data_ptr(), kept.data_ptr())
         c.synchronize()
+        assert "cohort" in c.profile_read()
         p, o, k = payload.cpu().numpy(), offsets.cpu().numpy(), kept.cpu().numpy()
         for i in range(n):
             got = p[int(o[i]):int(o[i]) + 20 + 8 * int(k[i])].tobytes()
             assert got == oracle.compress_payload(boxes[i].astype(np.float32), KEEPS[0])[0], i
         assert seen, "no cohort wait timed out under WC_OPT_SPIN_LIMIT 1"
     finally:
-        c.close()
+        c.profile_enable(False)
+        c.set_option(WC_OPT_SPIN_LIMIT, 0)
+        c.set_option(WC_OPT_TICKETS, 0)
+        c.set_option(WC_OPT_COHORT, 0)
+        c.set_option(WC_OPT_COHORT_LAG, 2)

@@ -95,6 +95,7 @@ def test_emit_without_stage_is_rejected(wc, ctx, oracle):
     d_pay = torch.empty(cap, dtype=torch.uint8, device=dev)
     d_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     d_kept = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()  # the fills above run on torch's stream, the context on its own
     ctx.forward_host(cells, units, n, 0.999)  # any other call invalidates the staged scratch
     with pytest.raises(wc.WaveletError):
         ctx.forward_emit(units, n, 0.999, None, d_pay.data_ptr(), cap, d_off.data_ptr(), d_kept.data_ptr())
