@@ -95,7 +95,7 @@ void populate_range(char* lo, char* hi, size_t page) {
 
 void populate_force_touch(bool on) { g_force_touch.store(on); }
 
-void populate_for_write(HostPool* pool, void* p, size_t bytes, bool thp) {
+void populate_for_write(HostPool* pool, void* p, size_t bytes, bool thp) try {
     static const size_t page = (size_t)sysconf(_SC_PAGESIZE);
     constexpr size_t kHuge = size_t(2) << 20;
     const uintptr_t a = (uintptr_t)p, e = a + bytes;
@@ -125,6 +125,7 @@ void populate_for_write(HostPool* pool, void* p, size_t bytes, bool thp) {
         return;
     }
     pool->run((int)parts.size(), one);
+} catch (...) {  // an allocation failure: leave the faults to the copy
 }
 
 }  // namespace wc
