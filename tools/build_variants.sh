@@ -11,7 +11,8 @@ for spec in "$@"; do
     /opt/rocm/bin/hipcc $FLAGS $defs -c $CS/$f.hip -o $out/obj/$f.o &
   done
   /opt/rocm/bin/hipcc $FLAGS $defs -c $CS/wc_capi.cpp -o $out/obj/wc_capi.o &
+  g++ -O2 -std=c++17 -fPIC -c $CS/wc_hostmem.cpp -o $out/obj/wc_hostmem.o &
   wait
-  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out/libwavelet_amd.so $out/obj/*.o
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out/libwavelet_amd.so $out/obj/*.o -lpthread
   rm -rf $out/obj
 done
