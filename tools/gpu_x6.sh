@@ -3,6 +3,7 @@
 # -DWC_TILE_X=6: whole 512-B fp32 rows of a 128^3 unit, two adjacent rows = 1 KB
 # per z plane, 16-coefficient segments) vs 32 x 1 x 32 (default); check runs
 # against the conservative path, then C5 and 128^3 fp64, 2 reps.
+# (Round 3 record: WC_TILE_X was removed after the form measured slower; this script no longer builds it.)
 S=tools/bin/wc_bench
 steps=("chk_x6:90:LD_LIBRARY_PATH=tools/variants/x6 $S 64 128 f32 0.9999 3 1 1 1"
        "chk_x6_f64:90:LD_LIBRARY_PATH=tools/variants/x6 $S 32 128 f64 0.999 3 1 1 1")
