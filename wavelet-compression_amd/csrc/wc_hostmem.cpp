@@ -6,7 +6,6 @@
 
 #include <algorithm>
 #include <atomic>
-#include <cerrno>
 #include <cstdint>
 
 #ifndef MADV_POPULATE_WRITE
@@ -79,13 +78,31 @@ namespace {
 
 std::atomic<bool> g_force_touch{false};
 
+// Does this kernel know MADV_POPULATE_WRITE (Linux 5.14)?  Probed once on a
+// private anonymous page, so that EINVAL on a caller's range later means a
+// mapping it does not apply to (VM_IO / VM_PFNMAP: left alone), not an old
+// kernel.
+bool kernel_has_populate() {
+    static const bool has = [] {
+        const size_t page = (size_t)sysconf(_SC_PAGESIZE);
+        void* p = mmap(nullptr, page, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) return false;
+        const bool ok = madvise(p, page, MADV_POPULATE_WRITE) == 0;
+        munmap(p, page);
+        return ok;
+    }();
+    return has;
+}
+
 void populate_range(char* lo, char* hi, size_t page) {
     if (hi <= lo) return;
     if (!g_force_touch.load(std::memory_order_relaxed)) {
-        if (madvise(lo, (size_t)(hi - lo), MADV_POPULATE_WRITE) == 0) return;
-        if (errno != EINVAL) return;  // EFAULT, ENOMEM, EHWPOISON …: leave the faults to the copy
+        if (kernel_has_populate()) {
+            (void)madvise(lo, (size_t)(hi - lo), MADV_POPULATE_WRITE);  // any failure: the copy faults instead
+            return;
+        }
     }
-    for (char* q = lo; q < hi; q += page) {  // kernels before 5.14
+    for (char* q = lo; q < hi; q += page) {  // kernels before 5.14: a read and a write-back per page
         volatile char* v = q;
         *v = *v;
     }
