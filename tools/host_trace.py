@@ -23,6 +23,9 @@ pinned = torch.empty(cells_dev.numel(), dtype=cells_dev.dtype, pin_memory=True)
 pinned.copy_(cells_dev)
 torch.cuda.synchronize()
 arr = pinned.numpy()
+if os.environ.get("HOST_TRACE_PAGEABLE"):  # cells in ordinary (pageable) host memory, as a C++ caller's vector
+    arr = arr.copy()
+    print("pageable cells", file=sys.stderr, flush=True)
 keep = float(np.float32(0.999))
 ctx = wc.capi.Context(0)
 for it in range(3):
