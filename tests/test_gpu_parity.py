@@ -739,6 +739,41 @@ def test_host_destination_prefault(wc, ctx, oracle, threads, thp):
     assert np.all(out[~owned] == 7.0)
 
 
+@pytest.mark.parametrize("chunk", [0, 1 << 21])
+def test_host_uploads_from_pageable_memory(wc, ctx, oracle, chunk):
+    """Large pageable sources (the cells of wc_forward_host, the payloads of
+    wc_inverse_host: >= 64 MB here) go through the context's pinned bounce
+    slots, copied by a host pool while earlier slots' DMA runs, also across
+    pipelined unit runs (HOST_CHUNK 2^21: slots rotating across runs); the
+    bytes equal the direct path's (WC_OPT_HOST_THREADS 0) and the oracle's."""
+    from wavelet_compression_amd.capi import WC_OPT_HOST_CHUNK, WC_OPT_HOST_THREADS
+    keep = float(np.float32(0.99999))  # most coefficients kept: a payload of ~80 MB
+    boxes = synth(oracle, [(64, 64, 64)] * 40, seed0=71)
+    units, n, extent, cells = pack(wc, boxes)
+    assert cells.nbytes >= (64 << 20)
+    ctx.set_option(WC_OPT_HOST_CHUNK, chunk)
+    try:
+        ctx.set_option(WC_OPT_HOST_THREADS, 0)
+        p0, o0, k0 = ctx.forward_host(cells, units, n, keep)
+        r0 = ctx.inverse_host(p0, o0[:n], units, n, extent)
+        ctx.set_option(WC_OPT_HOST_THREADS, -1)
+        p1, o1, k1 = ctx.forward_host(cells, units, n, keep)
+        assert int(o1[n]) >= (64 << 20)
+        r1 = ctx.inverse_host(p1, o1[:n], units, n, extent)
+        r2 = ctx.inverse_host(p1.copy(), o1[:n], units, n, extent)  # a source the runtime has never seen
+    finally:
+        ctx.set_option(WC_OPT_HOST_THREADS, -1)
+        ctx.set_option(WC_OPT_HOST_CHUNK, 1 << 25)
+    end = int(o0[n])
+    assert np.array_equal(o0, o1) and np.array_equal(k0, k1) and np.array_equal(p0[:end + 4], p1[:end + 4])
+    assert np.array_equal(r0, r1) and np.array_equal(r0, r2)
+    for i in (0, n - 1):
+        want = oracle_payload(oracle, boxes[i], keep)
+        assert wc.capi.unit_payload(p1, o1, k1, i) == want, i
+        o = units[i].cell_offset
+        assert r1[o:o + boxes[i].size].tobytes() == oracle.decompress_payload(want).ravel().tobytes(), i
+
+
 def test_plan_cache_eviction(wc, ctx, oracle):
     """More distinct batches than the plan cache holds (16), each twice: plans
     are swapped back in, evicted, and rebuilt into an evicted plan's buffers;

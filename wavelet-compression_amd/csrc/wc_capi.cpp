@@ -173,6 +173,13 @@ struct wc_ctx {
     int opt_host_threads = -1;    // WC_OPT_HOST_THREADS (-1: not yet resolved from the environment)
     bool opt_host_thp = true;     // WC_OPT_HOST_THP
     std::unique_ptr<wc::HostPool> hpool;
+    // uploads from pageable host memory: copied by upool's threads into pinned
+    // bounce slots, each slot's copy to the device ordered by an event
+    std::unique_ptr<wc::HostPool> upool;
+    void* bounce = nullptr;
+    std::vector<hipEvent_t> bev;   // per slot: recorded after the slot's last queued copy
+    std::vector<bool> bev_live;    // per slot: bev recorded (wait on it before the slot is rewritten)
+    uint32_t bnext = 0;            // next slot (rotates across calls)
     // plans of earlier batches (most recent last), swapped in when a batch recurs
     std::vector<Plan> plan_cache;
     // persistent-grid sizes (resident workgroups for an LDS size) on this device
@@ -1062,6 +1069,8 @@ void wc_ctx_destroy(wc_ctx* c) {
     if (c->up) (void)hipStreamDestroy(c->up);
     if (c->down) (void)hipStreamDestroy(c->down);
     if (c->pinned) (void)hipHostFree(c->pinned);
+    if (c->bounce) (void)hipHostFree(c->bounce);
+    for (hipEvent_t e : c->bev) (void)hipEventDestroy(e);
     for (auto& m : c->marks) {
         c->ev_pool.push_back(m.a);
         c->ev_pool.push_back(m.b);
@@ -1580,6 +1589,74 @@ static Populate host_populate(wc_ctx* c) {
     return P;
 }
 
+// Is p pinned (or device) memory the DMA engines read directly?  A pageable
+// pointer makes the query fail; its error is cleared so that no later launch
+// check sees it.
+static bool dma_ready(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged ||
+           a.type == hipMemoryTypeUnified;
+}
+
+constexpr size_t kBounceSlot = size_t(32) << 20;  // bytes per pinned bounce slot
+constexpr int kBounceSlots = 4;
+
+// Host-to-device copy of `bytes` from `src` on stream `st`.  Pinned (or
+// device) sources and small copies go straight to the DMA engine.  A large
+// pageable source goes through the context's pinned bounce slots: this
+// thread's pool copies slot-sized pieces (8-16 threads: ~100 GB/s) while the
+// previous pieces' DMA runs (57 GB/s), instead of the runtime pinning pages
+// of a buffer it has not seen before (14-32 GB/s on the MI355X host,
+// profiles/r04/experiments/gpu_host_prefault.txt).  Returns the first error.
+static hipError_t host_upload(wc_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
+    if (bytes < 2 * kBounceSlot || c->opt_host_threads == 0 || dma_ready(src))
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+    hipError_t e;
+    if (!c->bounce) {
+        if ((e = hipHostMalloc(&c->bounce, kBounceSlot * kBounceSlots, hipHostMallocDefault)) != hipSuccess) {
+            c->bounce = nullptr;
+            return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+        }
+    }
+    while ((int)c->bev.size() < kBounceSlots) {
+        hipEvent_t ev;
+        if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+        c->bev.push_back(ev);
+        c->bev_live.push_back(false);
+    }
+    if (!c->upool || c->upool->threads() != c->opt_host_threads) {
+        c->upool.reset();
+        try {
+            c->upool = std::make_unique<wc::HostPool>(c->opt_host_threads - 1);
+        } catch (...) {
+            return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+        }
+    }
+    wc::HostPool& pool = *c->upool;
+    for (size_t off = 0; off < bytes; off += kBounceSlot) {
+        const int k = (int)(c->bnext++ % kBounceSlots);
+        const size_t len = std::min(kBounceSlot, bytes - off);
+        uint8_t* slot = (uint8_t*)c->bounce + kBounceSlot * k;
+        // the slot's previous copy (this call's or an earlier one's) has been read
+        if (c->bev_live[k] && (e = hipEventSynchronize(c->bev[k])) != hipSuccess) return e;
+        const int T = pool.threads();
+        const size_t per = (len / T + 4095) & ~size_t(4095);
+        pool.run(T, [&](int i) {
+            const size_t lo = std::min(len, per * i), hi = std::min(len, per * (i + 1));
+            if (hi > lo) std::memcpy(slot + lo, (const uint8_t*)src + off + lo, hi - lo);
+        });
+        if ((e = hipMemcpyAsync((uint8_t*)dst + off, slot, len, hipMemcpyHostToDevice, st)) != hipSuccess ||
+            (e = hipEventRecord(c->bev[k], st)) != hipSuccess)
+            return e;
+        c->bev_live[k] = true;
+    }
+    return hipSuccess;
+}
+
 // Progress of a pipelined _host call's runs, published by one thread and
 // awaited by another: a copy from or to pageable host memory returns only
 // when it is done, so the uploads (the call's thread) and the downloads (a
@@ -1741,8 +1818,8 @@ static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_u
             hipStream_t cs = nr > 1 ? c->up : c->stream;
             hipError_t e;
             if (hi > lo &&
-                (e = hipMemcpyAsync(d_cells + esz * lo, (const uint8_t*)cells + esz * lo, esz * (hi - lo),
-                                    hipMemcpyHostToDevice, cs)) != hipSuccess)
+                (e = host_upload(c, d_cells + esz * lo, (const uint8_t*)cells + esz * lo, esz * (hi - lo), cs)) !=
+                    hipSuccess)
                 return hip_fail(c, e, "cells upload");
             if (nr > 1 && ((e = hipEventRecord(c->hev[2 * r], c->up)) != hipSuccess ||
                            (e = hipStreamWaitEvent(c->stream, c->hev[2 * r], 0)) != hipSuccess))
@@ -1893,8 +1970,7 @@ static int inverse_host_once(wc_ctx* c, const uint8_t* payload, const uint64_t* 
             }
             hipStream_t us = nr > 1 ? c->up : c->stream;
             hipError_t e;
-            if (hi > lo && (e = hipMemcpyAsync((uint8_t*)c->h_payload.p + lo, payload + lo, hi - lo,
-                                               hipMemcpyHostToDevice, us)) != hipSuccess)
+            if (hi > lo && (e = host_upload(c, (uint8_t*)c->h_payload.p + lo, payload + lo, hi - lo, us)) != hipSuccess)
                 return hip_fail(c, e, "payload upload");
             if (nr > 1 && ((e = hipEventRecord(c->hev[2 * r], c->up)) != hipSuccess ||
                            (e = hipStreamWaitEvent(c->stream, c->hev[2 * r], 0)) != hipSuccess))
