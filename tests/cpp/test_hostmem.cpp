@@ -3,6 +3,7 @@
 // plain and under ASan+UBSan / TSan (tests/test_sanitizers.py).
 //   * HostPool::run calls every task index exactly once, for pools of 0..15
 //     workers and jobs of 0..5000 tasks, many jobs back to back;
+//   * RunGate hands runs over in order, never early, and a cancel wakes a waiter;
 //   * populate_for_write never changes a byte (data written before it, never
 //     touched zeros, unaligned edges, both the MADV_POPULATE_WRITE path and the
 //     per-page touch path) and leaves the whole pages of the range resident.
@@ -10,6 +11,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -98,8 +100,41 @@ static void populate_edges() {
     CHECK(same);
 }
 
+// RunGate: a publisher thread queues runs one at a time with uneven delays;
+// the waiter sees every run exactly in order, never before it is published
+// (checked through a value the publisher writes first), and a cancel wakes a
+// waiter blocked on a run that never comes.
+static void run_gate() {
+    for (int rep = 0; rep < 20; ++rep) {
+        wc::RunGate gate;
+        constexpr int kRuns = 16;
+        std::vector<int> payload(kRuns, 0);
+        std::thread pub([&] {
+            for (int r = 0; r < kRuns; ++r) {
+                payload[r] = r + 1;  // written before the run is published
+                if ((r + rep) % 3 == 0) std::this_thread::sleep_for(std::chrono::microseconds(50 * (r % 4)));
+                gate.publish(r + 1);
+            }
+        });
+        bool ok = true;
+        for (int r = 0; r < kRuns; ++r) ok &= gate.wait(r) && payload[r] == r + 1;
+        pub.join();
+        CHECK(ok);
+        wc::RunGate stuck;
+        stuck.publish(2);
+        std::thread canceller([&] {
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+            stuck.cancel();
+        });
+        CHECK(stuck.wait(1));
+        CHECK(!stuck.wait(5));  // returns once cancelled
+        canceller.join();
+    }
+}
+
 int main() {
     pool_tasks();
+    run_gate();
     {
         wc::HostPool pool(7);
         for (bool touch : {false, true})

@@ -1657,39 +1657,6 @@ static hipError_t host_upload(wc_ctx* c, void* dst, const void* src, size_t byte
     return hipSuccess;
 }
 
-// Progress of a pipelined _host call's runs, published by one thread and
-// awaited by another: a copy from or to pageable host memory returns only
-// when it is done, so the uploads (the call's thread) and the downloads (a
-// helper thread) of different runs overlap only from different threads.
-class RunGate {
-public:
-    void publish(int runs) {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            done_ = runs;
-        }
-        cv_.notify_all();
-    }
-    void cancel() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            cancelled_ = true;
-        }
-        cv_.notify_all();
-    }
-    bool wait(int r) {  // false: cancelled before run r was published
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return done_ > r || cancelled_; });
-        return done_ > r;
-    }
-
-private:
-    std::mutex mu_;
-    std::condition_variable cv_;
-    int done_ = 0;
-    bool cancelled_ = false;
-};
-
 // What a helper thread of a _host call ran into (applied to the context by
 // the call's thread once the helper has joined).
 struct HelperStatus {
@@ -1713,7 +1680,7 @@ struct HelperStatus {
 // call has more than one run, else on the call's thread after `main`.
 extern "C++" {
 template <class Main, class Body>
-static int with_helper(wc_ctx* c, int nr, RunGate& gate, HelperStatus& hs, Main main, Body body) {
+static int with_helper(wc_ctx* c, int nr, wc::RunGate& gate, HelperStatus& hs, Main main, Body body) {
     std::thread helper;
     if (nr > 1) {
         try {
@@ -1801,7 +1768,7 @@ static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_u
     uint32_t* pin_kept = (uint32_t*)(pin_poff + (n + nr));       // [n]
     uint8_t* d_cells = (uint8_t*)c->h_cells.p;
     const Populate populate = host_populate(c);
-    RunGate gate;
+    wc::RunGate gate;
     HelperStatus hs;
     uint64_t R = 4;  // run r's packed bytes [4, end) land at R (== 4 mod 8); the next run starts at R + end
     // The call's thread: uploads, kernels, each run's sizes to pinned memory.
@@ -1940,7 +1907,7 @@ static int inverse_host_once(wc_ctx* c, const uint8_t* payload, const uint64_t* 
     }
     first_span[nr] = (int)spans.size();
     const Populate populate = host_populate(c);
-    RunGate gate, resident;
+    wc::RunGate gate, resident;
     HelperStatus hs;
     // The destination spans do not depend on the device: with several runs a
     // thread of its own faults them in ahead of the downloads.

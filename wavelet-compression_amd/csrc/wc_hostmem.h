@@ -45,6 +45,39 @@ private:
     bool stop_ = false;
 };
 
+// Progress of a pipelined _host call's runs, published by one thread and
+// awaited by another: a copy from or to pageable host memory returns only
+// when it is done, so the uploads (the call's thread) and the downloads (a
+// helper thread) of different runs overlap only from different threads.
+class RunGate {
+public:
+    void publish(int runs) {  // runs [0, runs) are queued
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            done_ = runs;
+        }
+        cv_.notify_all();
+    }
+    void cancel() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            cancelled_ = true;
+        }
+        cv_.notify_all();
+    }
+    bool wait(int r) {  // false: cancelled before run r was published
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return done_ > r || cancelled_; });
+        return done_ > r;
+    }
+
+private:
+    std::mutex mu_;
+    std::condition_variable cv_;
+    int done_ = 0;
+    bool cancelled_ = false;
+};
+
 // Make every whole page of [p, p + bytes) resident and writable without
 // changing a byte (MADV_POPULATE_WRITE; on kernels without it, a read and a
 // write-back of one byte per page, so the range must not be written
