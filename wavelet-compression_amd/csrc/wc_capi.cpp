@@ -1602,8 +1602,9 @@ static bool dma_ready(const void* p) {
            a.type == hipMemoryTypeUnified;
 }
 
-constexpr size_t kBounceSlot = size_t(32) << 20;  // bytes per pinned bounce slot
-constexpr int kBounceSlots = 4;
+constexpr size_t kBounceSlot = size_t(16) << 20;  // bytes per pinned bounce slot
+constexpr int kBounceSlots = 8;
+constexpr int kBounceThreads = 8;                  // enough to outrun the link (~110 GB/s into pinned memory)
 
 // Host-to-device copy of `bytes` from `src` on stream `st`.  Pinned (or
 // device) sources and small copies go straight to the DMA engine.  A large
@@ -1613,7 +1614,7 @@ constexpr int kBounceSlots = 4;
 // of a buffer it has not seen before (14-32 GB/s on the MI355X host,
 // profiles/r04/experiments/gpu_host_prefault.txt).  Returns the first error.
 static hipError_t host_upload(wc_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
-    if (bytes < 2 * kBounceSlot || c->opt_host_threads == 0 || dma_ready(src))
+    if (bytes < (size_t(64) << 20) || c->opt_host_threads == 0 || dma_ready(src))
         return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
     hipError_t e;
     if (!c->bounce) {
@@ -1628,10 +1629,11 @@ static hipError_t host_upload(wc_ctx* c, void* dst, const void* src, size_t byte
         c->bev.push_back(ev);
         c->bev_live.push_back(false);
     }
-    if (!c->upool || c->upool->threads() != c->opt_host_threads) {
+    const int ut = std::min(c->opt_host_threads, kBounceThreads);
+    if (!c->upool || c->upool->threads() != ut) {
         c->upool.reset();
         try {
-            c->upool = std::make_unique<wc::HostPool>(c->opt_host_threads - 1);
+            c->upool = std::make_unique<wc::HostPool>(ut - 1);
         } catch (...) {
             return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
         }
