@@ -572,6 +572,13 @@ def global_hist_leg(args, d: Dist, ctx, b: Batch):
             "allreduce": f"{b.capi.HIST_BINS} x u64 over {d.world} rank(s)" + (f" ({d.backend()})" if d.world > 1 else " (none)")}
 
 
+def link_ms(up: int, down: int) -> float:
+    """The PCIe floor of a call moving `up` and `down` bytes: each direction
+    at most 57 GB/s, both together at most 74.5 GB/s (measured on the MI355X
+    boxes, profiles/r04/experiments/gpu_pcie.txt)."""
+    return max(max(up, down) / 57e9, (up + down) / 74.5e9) * 1e3
+
+
 def host_leg(args, d: Dist, ctx, b: Batch):
     """C2 through wc_forward_host: the cells start in pinned host memory, the
     packed payloads end in pageable host memory; includes both PCIe copies.
@@ -614,9 +621,10 @@ def host_leg(args, d: Dist, ctx, b: Batch):
             "inverse": {"value": b.ncells / (ims * 1e-3), "unit": "cells/s", "ms_per_step": ims,
                         "h2d_bytes": d2h, "d2h_bytes": 4 * b.ncells,
                         "host_GBps": (d2h + 4 * b.ncells) / (ims * 1e-3) / 1e9, "fresh_ms_per_step": fims},
-            "link_bound_ms": {"forward": h2d / 57e9 * 1e3, "inverse": 4 * b.ncells / 57e9 * 1e3,
-                              "note": "bytes of the larger direction / 57 GB/s (the box's measured PCIe rate "
-                                      "per direction, profiles/r04/experiments/gpu_pcie.txt)"},
+            "link_bound_ms": {"forward": link_ms(h2d, d2h), "inverse": link_ms(d2h, 4 * b.ncells),
+                              "note": "max(bytes of the larger direction / 57 GB/s, bytes of both / 74.5 GB/s): "
+                                      "the box's measured PCIe rates, one direction and both at once "
+                                      "(profiles/r04/experiments/gpu_pcie.txt)"},
             "note": "PCIe-inclusive (pinned host cells in, packed payloads out to reused pageable host buffers), "
                     "one rank; fresh_ms_per_step allocates new result arrays per call; "
                     "`value` above is the HBM-resident rate"}
