@@ -108,7 +108,7 @@ def kernel_sources_sha() -> str:
     """Hash of the kernel + C-ABI sources: a PMC summary applies only to them."""
     h = hashlib.sha256()
     cs = ROOT / "wavelet-compression_amd" / "csrc"
-    for p in sorted(list(cs.glob("*.hip")) + list(cs.glob("*.h")) + [cs / "wc_capi.cpp"]):
+    for p in sorted(list(cs.glob("*.hip")) + list(cs.glob("*.h")) + list(cs.glob("wc_*.cpp"))):
         h.update(p.name.encode())
         h.update(p.read_bytes())
     return h.hexdigest()[:16]
@@ -222,6 +222,9 @@ class Batch:
         self.kept = torch.zeros(max(self.n, 1), dtype=torch.int32, device=d.dev)
         self.regen = torch.empty(max(self.extent, 1), dtype=torch.float32, device=d.dev) if inverse else None
         self.rmse = torch.zeros(max(self.n, 1), dtype=torch.float64, device=d.dev) if inverse else None
+        # the payloads' row index (wc_forward_rows / wc_inverse_rows: in-process round trips)
+        self.rows_bytes = self.capi.rowindex_bytes(self.tab, self.n) if (inverse and self.n) else 0
+        self.rows = torch.empty(max(self.rows_bytes // 8, 1), dtype=torch.int64, device=d.dev) if inverse else None
         torch.cuda.synchronize()
 
     def forward(self, ctx):
@@ -242,6 +245,23 @@ class Batch:
         if self.n:
             ctx.inverse_rmse(self.payload.data_ptr(), self.offsets.data_ptr(), self.tab, self.n,
                              self.cells_dev.data_ptr(), self.code, self.regen.data_ptr(), self.rmse.data_ptr())
+
+    def forward_rows(self, ctx):
+        if self.n:
+            ctx.forward_rows(self.cells_dev.data_ptr(), self.code, self.tab, self.n, self.keep,
+                             self.payload.data_ptr(), self.cap, self.offsets.data_ptr(), self.kept.data_ptr(),
+                             self.rows.data_ptr(), self.rows_bytes)
+
+    def inverse_rows(self, ctx):
+        if self.n:
+            ctx.inverse_rows(self.payload.data_ptr(), self.offsets.data_ptr(), self.tab, self.n,
+                             self.rows.data_ptr(), self.regen.data_ptr())
+
+    def inverse_rows_rmse(self, ctx):
+        if self.n:
+            ctx.inverse_rows(self.payload.data_ptr(), self.offsets.data_ptr(), self.tab, self.n,
+                             self.rows.data_ptr(), self.regen.data_ptr(), self.cells_dev.data_ptr(), self.code,
+                             self.rmse.data_ptr())
 
     def kept_total(self):
         return int(self.kept[:self.n].to(self.kept.device).sum().item()) if self.n else 0
@@ -293,8 +313,8 @@ def stage_times(ctx, step, steps):
     return {k: (ms / cnt, cnt / steps) for k, (ms, cnt) in ctx.profile_read().items()}
 
 
-FWD_STAGES = ("transform", "fallback", "emit", "cohort")
-INV_STAGES = ("rowindex", "decode", "inverse", "rmse")
+FWD_STAGES = ("transform", "fallback", "emit")
+INV_STAGES = ("rowindex", "decode", "inverse", "rmse", "pairs")
 
 
 def pmc_summary(path, workload, dtype):
@@ -352,8 +372,7 @@ def headline(args, d: Dist, ctx):
                   "payload_bytes": 8 * kept + 20 * b.n})
     elapsed = m["seconds"]
     # roofline of the dominant kernel: its algorithmic bytes per launch / its launch time
-    own = {"transform": b.s_in * b.ncells, "emit": 8 * kept + 20 * b.n,
-           "cohort": alg_bytes_forward(b.s_in, b.ncells, kept, b.n)}  # the cohort launch is the whole forward
+    own = {"transform": b.s_in * b.ncells, "emit": 8 * kept + 20 * b.n}
     dominant = max(stages, key=lambda k: stages[k][0])
     dom_ms = stages[dominant][0]
     achieved = own.get(dominant, 0) / (dom_ms * 1e-3) / 1e9
@@ -414,8 +433,23 @@ def inverse_leg(args, d: Dist, ctx, b: Batch):
                   "rmse_sum": float(r.sum().item()), "max_rmse": float(r.max().item())})
     ms = m["seconds"] / args.steps * 1e3
     alg = alg_bytes_inverse(b.ncells, kept, b.n)
+    # the in-process round trip's inverse: the same payloads with the row index
+    # wc_forward_rows wrote beside them (wc_inverse_rows: no row index kernel)
+    b.forward_rows(ctx)
+    ctx.synchronize()
+    rsecs = timed(d, ctx, lambda: b.inverse_rows(ctx), args.steps, 2)
+    rst = stage_times(ctx, lambda: b.inverse_rows(ctx), args.steps)
+    rms = d.reduce({"seconds": rsecs})["seconds"] / args.steps * 1e3
     torch.cuda.synchronize()
     return {"value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
+            "with_forward_row_index": {
+                "ms_per_step": rms, "value": m["cells"] / (rms * 1e-3), "unit": "cells/s",
+                "stage_ms_per_launch": {k: round(v[0], 4) for k, v in rst.items()},
+                "roofline_path": {"achieved": alg / (rms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                                  "frac": alg / (rms * 1e-3) / 1e9 / PEAK_HBM_GBPS},
+                "note": "wc_inverse_rows of the same payloads with the row index wc_forward_rows wrote "
+                        "(the -estimate / round-trip form; `ms_per_step` above: wc_inverse from the payloads "
+                        "alone, the -d form)"},
             "stage_ms_per_launch": {k: round(v[0], 4) for k, v in st.items()},
             "roofline_path": {"achieved": alg / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                               "frac": alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, "bytes_per_step": alg,
@@ -441,11 +475,16 @@ def round_trip_leg(args, d: Dist, name):
         b.inverse(ctx)
         b.rmse_step(ctx)
 
-    def step():  # wc_inverse_rmse: the RMSE pass fused into the row-indexed inverse
+    def fused():  # wc_inverse_rmse: the RMSE fused into the row-indexed inverse, the row index from the payloads
         b.forward(ctx)
         b.inverse_rmse(ctx)
 
+    def step():  # the forward writes the row index, the inverse reads it (no row index kernel)
+        b.forward_rows(ctx)
+        b.inverse_rows_rmse(ctx)
+
     sep_ms = timed(d, ctx, separate, args.leg_steps, 2) / args.leg_steps * 1e3
+    fused_ms = timed(d, ctx, fused, args.leg_steps, 2) / args.leg_steps * 1e3
     secs = timed(d, ctx, step, args.leg_steps, 2)
     st = stage_times(ctx, step, args.leg_steps)
     kept = b.kept_total()
@@ -460,6 +499,8 @@ def round_trip_leg(args, d: Dist, name):
     out = {"workload": spec["desc"], "units": b.n, "cells": b.ncells, "dtype": spec["dtype"],
            "kept_fraction": kept / b.ncells, "ms_per_step": ms,
            "round_trip_cells_per_s": b.ncells / (ms * 1e-3),
+           "path": "wc_forward_rows + wc_inverse_rows (fused RMSE, the forward's row index)",
+           "fused_from_payload_ms_per_step": fused_ms,
            "separate_calls_ms_per_step": sep_ms,
            "stage_ms_per_step": {k: round(v[0] * v[1], 4) for k, v in st.items()},
            "roofline_path": {"bytes_per_step": fwd + inv + rm, "achieved": (fwd + inv + rm) / (ms * 1e-3) / 1e9,

@@ -25,6 +25,11 @@
  *   - Functions without a _host suffix take DEVICE pointers (HBM-resident data)
  *     and are asynchronous on the context's stream.  _host variants take host
  *     pointers, copy through pinned staging, and return when results are ready.
+ *   - Device buffers of cells, payloads, coefficients and reconstructions must
+ *     be 16-byte aligned (hipMalloc and torch allocations are); offsets,
+ *     kept counts, row indexes and RMSE outputs need their element alignment;
+ *     original cells of the RMSE calls any element alignment.  Otherwise
+ *     WC_ERR_INVALID.
  *   - One context per device per host thread.  The context owns its stream and
  *     its scratch memory; the caller owns every buffer it passes.
  *
@@ -135,14 +140,6 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  *   and offsets out; 0 = one run.  wc_inverse_host runs the same way (run
  *   r+1's payload bytes upload while run r decodes and run r-1's boxes
  *   download).
- * WC_OPT_COHORT (default 0 = off), WC_OPT_COHORT_LAG (default 2): the cohort
- *   forward for batches whose every unit is large (>= 2^21 cells) and of the
- *   32 x 1 x 32-block transform shape (hx, hz multiples of 32, even cell
- *   offset): transform and pack in ONE persistent launch, units in cohorts of
- *   WC_OPT_COHORT, the pack of cohort p - lag beside the transform of cohort
- *   p, staged coefficients in a ring of (lag + 2) * cohort units that stays in
- *   the Infinity Cache.  Same bytes out; no dispatch-order assumption (items
- *   are dequeued in list order).
  * WC_OPT_HOST_THREADS (default: OMP_NUM_THREADS, else the cores, at most 16):
  *   wc_forward_host / wc_inverse_host make the pages of each destination span
  *   of the caller's host buffer resident (MADV_POPULATE_WRITE, no byte
@@ -150,8 +147,10 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  *   it: a copy into never-touched pageable memory otherwise takes the page
  *   faults on its own thread (C2 payloads: 12-20 GB/s instead of the link's
  *   57).  0 = leave the faults to the copy.  Whole pages inside a span only.
- * WC_OPT_HOST_THP (default 1): advise transparent huge pages
- *   (MADV_HUGEPAGE) on the 2-MiB-aligned interior of those spans first.
+ * WC_OPT_HOST_THP (default 0): 1 = also advise transparent huge pages
+ *   (MADV_HUGEPAGE) on the 2-MiB-aligned interior of those spans first.  Off
+ *   by default: the advice splits the caller's mappings and changes their
+ *   huge-page policy for the life of the mapping (the caller owns its memory).
  */
 #define WC_OPT_SPARSE 12
 #define WC_OPT_ORDERED 13
@@ -164,8 +163,8 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
 #define WC_OPT_TICKETS 20
 #define WC_OPT_RIX_XCD 22
 #define WC_OPT_INV_GROUPS 23
-#define WC_OPT_COHORT 24
-#define WC_OPT_COHORT_LAG 25
+/* 24, 25: retired (the round-4 cohort forward, removed: slower than the
+ * two-kernel forward in every measured shape) */
 #define WC_OPT_HOST_THREADS 27
 #define WC_OPT_HOST_THP 28
 int wc_set_option(wc_ctx* ctx, int option, int64_t value);
@@ -254,6 +253,40 @@ int wc_inverse_rmse(wc_ctx* ctx, const uint8_t* d_payload, const uint64_t* d_off
                     const wc_unit* units, int n, const void* d_orig, int dtype, float* d_out,
                     double* d_rmse);
 
+/* Round trips in one process (the reference's -estimate: compress, then
+ * decompress the same boxes and calc_rmse_per_box, src/modes.cpp:236-291).
+ * The forward knows, as it packs the pairs, where every flat row of a unit
+ * starts in the payload; wc_forward_rows writes that ROW INDEX beside the
+ * payloads, and wc_inverse_rows reads it instead of re-deriving it from the
+ * payloads (the row index kernel of wc_inverse, a third of its time).
+ *
+ *   Row index layout (caller-owned device buffer, wc_rowindex_bytes): unit u
+ *   owns W*H + 1 entries of 8 bytes, after the entries of units 0..u-1.  Entry
+ *   r < W*H of flat row r = I*H + J (the D coefficients r*D .. r*D + D - 1 of
+ *   the reference's flat order, src/compressor.cpp:178-181) is {uint32 k,
+ *   uint32 p_k - r*D}: k the first pair whose flat position p_k is >= r*D;
+ *   entry W*H and the rows after the last pair hold {nrle, ncoeff - r*D}.
+ *   Written for the units of the row-indexed shape (W and H even, D % 8 ==
+ *   0, cells > 0); the entries of other units are not written (their inverse
+ *   decodes from the payload).
+ *
+ *   wc_forward_rows: wc_forward (same payloads, offsets, kept counts) that
+ *     also writes the row index (rowinfo_capacity >= wc_rowindex_bytes).
+ *   wc_inverse_rows: wc_inverse (d_orig = d_rmse = NULL) or wc_inverse_rmse
+ *     (both set) of payloads whose row index d_rowinfo came from
+ *     wc_forward_rows of the same payloads and units (NULL: derived from the
+ *     payloads, = wc_inverse / wc_inverse_rmse).  Pair indices read from the
+ *     row index are clamped to each payload's pair count, so a row index that
+ *     belongs to other payloads gives wrong cells but never an access outside
+ *     the payloads; headers are checked against the units (WC_ERR_FORMAT at
+ *     the next wc_synchronize). */
+uint64_t wc_rowindex_bytes(const wc_unit* units, int n);
+int wc_forward_rows(wc_ctx* ctx, const void* d_cells, int dtype, const wc_unit* units, int n, double keep,
+                    uint8_t* d_payload, uint64_t payload_capacity, uint64_t* d_offsets, uint32_t* d_kept,
+                    void* d_rowinfo, uint64_t rowinfo_capacity);
+int wc_inverse_rows(wc_ctx* ctx, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
+                    const void* d_rowinfo, const void* d_orig, int dtype, float* d_out, double* d_rmse);
+
 /* Transform only, host pointers (the reference's static wavelet_decompose). */
 int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* units, int n,
                       float* flat);
@@ -268,7 +301,7 @@ int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* 
 #define WC_STAGE_INVERSE 3    /* K6  inverse transform */
 #define WC_STAGE_RMSE 4       /* K7  */
 #define WC_STAGE_HIST 5       /* coefficient-magnitude histogram (wc_forward_stage with d_hist) */
-#define WC_STAGE_COHORT 6     /* cohort forward: K1 + K2 in one persistent launch (WC_OPT_COHORT) */
+#define WC_STAGE_PAIRS 6      /* header check + pair counts of wc_inverse_rows with a caller row index */
 #define WC_NUM_STAGES 7
 int wc_profile_enable(wc_ctx* ctx, int on);
 int wc_profile_read(wc_ctx* ctx, double* total_ms, uint32_t* launches, int nstages);

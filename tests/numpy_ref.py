@@ -73,3 +73,18 @@ def compress_payload(box: np.ndarray, keep: float) -> bytes:
     pairs["r"] = runs
     pairs["v"] = flat[pos]
     return hdr + pairs.tobytes()
+
+
+def row_index(payload: bytes, W: int, H: int, D: int) -> np.ndarray:
+    """The row index of one payload (include/wavelet_amd.h wc_rowindex_bytes):
+    (W*H + 1, 2) uint32, entry r = (k, p_k - r*D), k the first pair whose flat
+    position p_k (rle_decode's idx, src/decompressor.cpp:14-30) is >= r*D, or
+    (nrle, ncoeff - r*D) past the last pair."""
+    hdr = np.frombuffer(payload[:20], "<i4")
+    n, nrle = int(hdr[3]), int(hdr[4])
+    pairs = np.frombuffer(payload[20:20 + 8 * nrle], dtype=[("r", "<i4"), ("v", "<f4")])
+    pos = np.cumsum(pairs["r"].astype(np.int64) + 1) - 1
+    starts = np.arange(W * H + 1, dtype=np.int64) * D
+    k = np.searchsorted(pos, starts, side="left")
+    p = np.where(k < nrle, pos[np.minimum(k, max(nrle - 1, 0))] if nrle else n, n)
+    return np.stack([k, p - starts], axis=1).astype(np.uint32)

@@ -5,16 +5,14 @@ src/compressor.cpp:192-248 per box, src/modes.cpp:100-103):
   * every unit: header (W, H, D, ncoeff, nrle), 0 <= kept <= ncoeff, and the
     worst-case slot offsets;
   * payload bytes equal the oracle's on 10 units (first, last, random ones);
-  * the staged two-kernel path, the cohort forward (WC_OPT_COHORT) and the
-    look-backs' ticket form write identical bytes for ALL 512 units (zeroed
-    payload buffers compared whole; the stage timers show which path ran);
+  * the launch-order and the ticket form of the look-backs write identical
+    bytes for ALL 512 units (zeroed payload buffers compared whole);
   * wc_inverse of the whole batch reproduces the oracle's decompress()
     (rle_decode + inverse_wavelet_decompose, src/decompressor.cpp:14-159) on 2
     sampled units bit for bit.
 """
 import numpy as np
 import pytest
-from wavelet_compression_amd.capi import WC_OPT_COHORT, WC_OPT_COHORT_LAG
 
 pytestmark = pytest.mark.gpu
 
@@ -24,8 +22,7 @@ KEEP = float(np.float32(0.9999))
 @pytest.fixture(scope="module")
 def c5_run(wc, ctx):
     """The session context: the ONLY live context, so the launch-order form
-    (and with it the cohort forward) is the one that runs; a second live
-    context would switch both to the ticket form."""
+    is the one that runs (a second live context would switch to the tickets)."""
     import torch
     import bench_workloads as bw
     units = bw.WORKLOADS["c5"]["units"]()
@@ -89,13 +86,11 @@ def test_c5_payloads_match_oracle(c5_run, oracle):
         assert int(r["kept"][i]) == k
 
 
-@pytest.mark.parametrize("cohort,lag,ordered,stage", [(0, 2, 1, "emit"), (2, 2, 1, "cohort"), (4, 1, 1, "cohort"),
-                                                     (4, 1, 0, "emit")])
-def test_c5_paths_identical_all_units(c5_run, wc, cohort, lag, ordered, stage):
-    """The default path's bytes for all 512 units against the staged two-kernel
-    path (cohort 0), the cohort forward, and the look-backs' ticket form
-    (WC_OPT_ORDERED 0: the two-kernel path): whole zeroed buffers compared.
-    The stage timers show which path ran."""
+@pytest.mark.parametrize("ordered", [1, 0])
+def test_c5_paths_identical_all_units(c5_run, wc, ordered):
+    """The default path's bytes for all 512 units against a second run in the
+    launch-order form and in the look-backs' ticket form (WC_OPT_ORDERED 0):
+    whole zeroed buffers compared; the option readback shows which form ran."""
     import torch
     from wavelet_compression_amd.capi import WC_OPT_ORDERED
     r = c5_run
@@ -107,21 +102,13 @@ def test_c5_paths_identical_all_units(c5_run, wc, cohort, lag, ordered, stage):
     # for it (round 4: a fill still running zeroed the tail units' kept counts)
     torch.cuda.synchronize()
     try:
-        c.set_option(WC_OPT_COHORT, cohort)
-        c.set_option(WC_OPT_COHORT_LAG, lag)
         c.set_option(WC_OPT_ORDERED, ordered)
-        c.profile_enable(True)
-        c.profile_read()
+        assert c.get_option(WC_OPT_ORDERED) == ordered
         c.forward(r["cells"].data_ptr(), wc.capi.WC_F32, r["tab"], r["n"], KEEP, other.data_ptr(), r["cap"],
                   offs.data_ptr(), kept.data_ptr())
         c.synchronize()
-        stages = c.profile_read()
     finally:
-        c.profile_enable(False)
-        c.set_option(WC_OPT_COHORT, 0)
-        c.set_option(WC_OPT_COHORT_LAG, 2)
         c.set_option(WC_OPT_ORDERED, 1)
-    assert stage in stages and ("cohort" if stage == "emit" else "emit") not in stages, stages
     assert np.array_equal(kept.cpu().numpy(), r["kept"])
     assert np.array_equal(offs.cpu().numpy(), r["offsets"])
     assert torch.equal(other, r["payload"])

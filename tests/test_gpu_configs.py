@@ -9,11 +9,13 @@ C1 (configs[0]): the reference's own fixtures tests/plt00074 -> plt00075
     then -c and -d over both fixtures, both levels and components: the
     regenerated plotfiles are the fixture files byte for byte.
 C3 (configs[2]): the 4-level AMR layout x 4 components (bench_workloads.py,
-    SURVEY.md §8(d)), wc_forward -> wc_inverse -> wc_rmse on one GPU through
-    the C-ABI; payload bytes and reconstructions bit-exact against the oracle
-    on a per-level, per-component sample, per-box RMSE within 1e-6 relative of
-    calc_rmse_per_box (src/calc-loss.cpp:12-43); size-independent checks on
-    every unit (headers, kept counts, RMSE of the exact reconstruction).
+    SURVEY.md §8(d)), 2304 units on one GPU through the C-ABI, in the three
+    round-trip forms: wc_forward_rows + wc_inverse_rows (what bench.py's c3
+    leg times), wc_forward + wc_inverse_rmse, wc_forward + wc_inverse +
+    wc_rmse.  EVERY unit's payload bytes, kept count and reconstruction
+    bit-exact against the oracle, its RMSE within 1e-12 of calc_rmse_per_box
+    (src/calc-loss.cpp:12-43); every unit's row index against the numpy
+    restatement; the three forms identical.
 """
 import os
 import re
@@ -103,8 +105,16 @@ def test_c1_estimate_on_reference_fixtures(digit_free_dir):
         assert n == 5  # Header, Level_{0,1}/Cell_H and Level_{0,1}/Cell_D_00000
 
 
+def _threads():
+    return max(1, min(16, os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+
+
 @pytest.fixture(scope="module")
 def c3_run(wc):
+    """The C3 batch through the two paths bench.py's c3 leg times and the
+    -estimate round trip: wc_forward_rows + wc_inverse_rows (the forward's row
+    index, fused RMSE) and wc_forward + wc_inverse_rmse (the row index from the
+    payloads); plus wc_inverse + wc_rmse, the separate calls."""
     import torch
     import bench_workloads as bw
     units = bw.WORKLOADS["c3"]["units"]()
@@ -114,72 +124,116 @@ def c3_run(wc):
     tab, n, _ = bw.units_array(wc.capi, units, offs)
     ctx = wc.capi.Context(0)
     cap = wc.capi.payload_bound(tab, n)
-    payload = torch.empty(cap, dtype=torch.uint8, device=dev)
-    offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    kept = torch.zeros(n, dtype=torch.int32, device=dev)
-    regen = torch.full((extent,), float("nan"), dtype=torch.float32, device=dev)
-    rmse = torch.zeros(n, dtype=torch.float64, device=dev)
-    torch.cuda.synchronize()
-    ctx.forward(cells.data_ptr(), wc.capi.WC_F64, tab, n, keep, payload.data_ptr(), cap, offsets.data_ptr(),
-                kept.data_ptr())
-    ctx.inverse(payload.data_ptr(), offsets.data_ptr(), tab, n, regen.data_ptr())
-    ctx.rmse(cells.data_ptr(), wc.capi.WC_F64, regen.data_ptr(), tab, n, rmse.data_ptr())
-    ctx.synchronize()
-    yield dict(units=units, offs=offs, cells=cells, payload=payload, offsets=offsets.cpu().numpy(),
-               kept=kept.cpu().numpy(), regen=regen, rmse=rmse.cpu().numpy(), keep=keep)
+    rb = wc.capi.rowindex_bytes(tab, n)
+    F64 = wc.capi.WC_F64
+    out = {}
+    for path in ("rows", "fused", "separate"):
+        payload = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        kept = torch.zeros(n, dtype=torch.int32, device=dev)
+        regen = torch.full((extent,), float("nan"), dtype=torch.float32, device=dev)
+        rmse = torch.zeros(n, dtype=torch.float64, device=dev)
+        rowinfo = torch.zeros(rb // 4, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        if path == "rows":
+            ctx.forward_rows(cells.data_ptr(), F64, tab, n, keep, payload.data_ptr(), cap, offsets.data_ptr(),
+                             kept.data_ptr(), rowinfo.data_ptr(), rb)
+            ctx.inverse_rows(payload.data_ptr(), offsets.data_ptr(), tab, n, rowinfo.data_ptr(), regen.data_ptr(),
+                             cells.data_ptr(), F64, rmse.data_ptr())
+        else:
+            ctx.forward(cells.data_ptr(), F64, tab, n, keep, payload.data_ptr(), cap, offsets.data_ptr(),
+                        kept.data_ptr())
+            if path == "fused":
+                ctx.inverse_rmse(payload.data_ptr(), offsets.data_ptr(), tab, n, cells.data_ptr(), F64,
+                                 regen.data_ptr(), rmse.data_ptr())
+            else:
+                ctx.inverse(payload.data_ptr(), offsets.data_ptr(), tab, n, regen.data_ptr())
+                ctx.rmse(cells.data_ptr(), F64, regen.data_ptr(), tab, n, rmse.data_ptr())
+        ctx.synchronize()
+        out[path] = dict(payload=payload.cpu().numpy(), offsets=offsets.cpu().numpy(), kept=kept.cpu().numpy(),
+                         regen=regen.cpu().numpy(), rmse=rmse.cpu().numpy(),
+                         rowinfo=rowinfo.cpu().numpy().view(np.uint32).reshape(-1, 2))
+        del payload, regen, rowinfo
+    r = dict(units=units, offs=offs, cells=cells.cpu().numpy(), keep=keep, **out)
     ctx.close()
+    del cells
+    torch.cuda.empty_cache()
+    yield r
 
 
-def _sample(units, per_group=2, seed=3):
-    rng = np.random.default_rng(seed)
-    groups = {}
-    for i, u in enumerate(units):
-        groups.setdefault((u.lev, u.comp, (u.W, u.H, u.D)), []).append(i)
-    out = []
-    for key in sorted(groups):
-        idx = groups[key]
-        out += [idx[0]] + list(rng.choice(idx[1:], size=min(per_group - 1, len(idx) - 1), replace=False))
-    return sorted(out)
+def _box(r, i):
+    u = r["units"][i]
+    o = r["offs"][i]
+    return r["cells"][o:o + u.cells].reshape(u.D, u.H, u.W)
 
 
-def test_c3_payloads_and_reconstruction_match_oracle(c3_run, oracle):
+def _payload(p, i):
+    po = int(p["offsets"][i])
+    return p["payload"][po:po + 20 + 8 * int(p["kept"][i])].tobytes()
+
+
+def test_c3_every_unit_matches_oracle(c3_run, oracle):
+    """All 2304 C3 units through wc_forward_rows + wc_inverse_rows (the c3
+    leg of bench.py and -estimate): every payload and kept count equal the
+    oracle's compress() minus xz, every reconstruction its decompress() bit for
+    bit, every RMSE within 1e-12 of calc_rmse_per_box (src/calc-loss.cpp:12-43)."""
+    from concurrent.futures import ThreadPoolExecutor
     r = c3_run
+    p = r["rows"]
     units = r["units"]
-    sample = _sample(units)
-    assert {units[i].lev for i in sample} == {0, 1, 2, 3}
-    for i in sample:
+    assert {u.lev for u in units} == {0, 1, 2, 3} and len(units) == 2304
+
+    def check(i):
         u = units[i]
-        o = r["offs"][i]
-        box = oracle.narrow(r["cells"][o:o + u.cells].cpu().numpy().reshape(u.D, u.H, u.W))
+        box = oracle.narrow(_box(r, i))
         want, wk = oracle.compress_payload(box, r["keep"])
-        po = int(r["offsets"][i])
-        got = r["payload"][po:po + 20 + 8 * int(r["kept"][i])].cpu().numpy().tobytes()
-        assert got == want, (i, u)
-        assert int(r["kept"][i]) == wk
+        if _payload(p, i) != want or int(p["kept"][i]) != wk:
+            return i, "payload"
         back = oracle.decompress_payload(want)
-        assert r["regen"][o:o + u.cells].cpu().numpy().tobytes() == back.ravel().tobytes(), (i, u)
-        ref = oracle.rmse(box, back)
-        assert r["rmse"][i] == pytest.approx(ref, rel=1e-6, abs=1e-300), (i, u)
-
-
-def test_c3_every_unit_size_independent(c3_run, oracle):
-    """All 2304 units: headers, kept bounds, and RMSE of an exact reconstruction
-    equal to the RMSE the oracle computes from the GPU's own reconstruction."""
-    r = c3_run
-    units = r["units"]
-    pay = r["payload"].cpu().numpy()
-    for i, u in enumerate(units):
-        po = int(r["offsets"][i])
-        hdr = np.frombuffer(pay[po:po + 20].tobytes(), "<i4")
-        assert hdr.tolist() == [u.W, u.H, u.D, u.cells, int(r["kept"][i])], (i, u)
-        assert 0 <= r["kept"][i] <= u.cells
-    assert np.all(np.isfinite(r["rmse"])) and np.all(r["rmse"] >= 0)
-    frac = r["kept"].sum() / sum(u.cells for u in units)
-    assert 0.05 < frac < 0.95
-    # RMSE of every 97th unit recomputed by the oracle from the GPU reconstruction
-    for i in range(0, len(units), 97):
-        u = units[i]
         o = r["offs"][i]
-        box = oracle.narrow(r["cells"][o:o + u.cells].cpu().numpy().reshape(u.D, u.H, u.W))
-        rg = r["regen"][o:o + u.cells].cpu().numpy().reshape(u.D, u.H, u.W)
-        assert r["rmse"][i] == pytest.approx(oracle.rmse(box, rg), rel=1e-12, abs=1e-300), (i, u)
+        if p["regen"][o:o + u.cells].tobytes() != back.ravel().tobytes():
+            return i, "regen"
+        ref = oracle.rmse(box, back)
+        if abs(float(p["rmse"][i]) - ref) > 1e-12 * abs(ref):
+            return i, ("rmse", float(p["rmse"][i]), ref)
+        return None
+
+    with ThreadPoolExecutor(_threads()) as ex:
+        bad = [x for x in ex.map(check, range(len(units))) if x is not None]
+    assert not bad, bad[:16]
+    frac = p["kept"].astype(np.int64).sum() / sum(u.cells for u in units)
+    assert 0.05 < frac < 0.95
+
+
+def test_c3_row_index_of_every_unit(c3_run):
+    """The forward's row index, entry for entry, as the restatement derives it
+    from each payload (tests/numpy_ref.py row_index); every C3 shape is
+    row-indexable (even W, H and D % 8 == 0)."""
+    import numpy_ref as R
+    r = c3_run
+    p = r["rows"]
+    ent = 0
+    for i, u in enumerate(r["units"]):
+        assert u.W % 2 == 0 and u.H % 2 == 0 and u.D % 8 == 0
+        want = R.row_index(_payload(p, i), u.W, u.H, u.D)
+        assert np.array_equal(p["rowinfo"][ent:ent + u.W * u.H + 1], want), (i, u)
+        ent += u.W * u.H + 1
+    assert ent * 8 == p["rowinfo"].nbytes
+
+
+def test_c3_paths_identical(c3_run):
+    """The three round-trip forms give the same payloads, offsets, kept counts
+    and cells; the two fused forms the same RMSE bits, the separate calls an
+    RMSE within 1e-12 (another summation order)."""
+    r = c3_run
+    a, b, c = r["rows"], r["fused"], r["separate"]
+    for x in (b, c):
+        assert np.array_equal(a["offsets"], x["offsets"]) and np.array_equal(a["kept"], x["kept"])
+        assert a["regen"].tobytes() == x["regen"].tobytes()
+    for i in range(len(r["units"])):
+        assert _payload(a, i) == _payload(b, i) == _payload(c, i), i
+    assert np.array_equal(a["rmse"], b["rmse"])
+    assert np.allclose(a["rmse"], c["rmse"], rtol=1e-12, atol=0)
+    hdr_ok = all(np.frombuffer(_payload(a, i)[:20], "<i4").tolist() == [u.W, u.H, u.D, u.cells, int(a["kept"][i])]
+                 for i, u in enumerate(r["units"]))
+    assert hdr_ok

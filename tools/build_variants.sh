@@ -7,7 +7,7 @@ FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-gpu-flu
 for spec in "$@"; do
   name="${spec%%:*}"; defs="${spec#*:}"
   out=tools/variants/$name; mkdir -p $out/obj
-  for f in wc_cohort wc_transform wc_hist wc_compact wc_inverse wc_emit; do
+  for f in wc_transform wc_hist wc_compact wc_inverse wc_emit; do
     /opt/rocm/bin/hipcc $FLAGS $defs -c $CS/$f.hip -o $out/obj/$f.o &
   done
   /opt/rocm/bin/hipcc $FLAGS $defs -c $CS/wc_capi.cpp -o $out/obj/wc_capi.o &

@@ -100,7 +100,9 @@ int main(int argc, char** argv) {
     const double keep = (double)(float)(argc > 4 ? std::atof(argv[4]) : 0.999);
     const int steps = argc > 5 ? std::atoi(argv[5]) : 10;
     const int warmup = argc > 6 ? std::atoi(argv[6]) : 2;
-    const int inv_mode = argc > 7 ? std::atoi(argv[7]) : 0;  // 1 wc_inverse, 2 wc_inverse_rmse (fused calc_rmse_per_box)
+    // 1 wc_inverse, 2 wc_inverse_rmse (fused calc_rmse_per_box), 3 the round trip with the forward's row
+    // index (wc_forward_rows + wc_inverse_rows with the RMSE)
+    const int inv_mode = argc > 7 ? std::atoi(argv[7]) : 0;
     const bool inverse = inv_mode != 0;
     const bool check = argc > 8 ? std::atoi(argv[8]) != 0 : false;
     const int ordered = argc > 9 ? std::atoi(argv[9]) : 1;
@@ -152,7 +154,10 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&kept, 4 * boxes));
     double* rmse = nullptr;
     if (inverse) CK(hipMalloc(&regen, 4 * extent));
-    if (inv_mode == 2) CK(hipMalloc(&rmse, 8 * boxes));
+    if (inv_mode >= 2) CK(hipMalloc(&rmse, 8 * boxes));
+    void* rowinfo = nullptr;
+    const uint64_t rowinfo_bytes = wc_rowindex_bytes(units.data(), boxes);
+    if (inv_mode == 3) CK(hipMalloc(&rowinfo, rowinfo_bytes));
 
     wc_ctx* ctx = nullptr;
     if (wc_ctx_create(0, &ctx) != WC_OK) {
@@ -164,13 +169,6 @@ int main(int argc, char** argv) {
     wc_set_option(ctx, WC_OPT_INVERSE_ROWS, rows);
     if (wc_set_option(ctx, WC_OPT_RIX_LDS, rix_lds) != WC_OK || wc_set_option(ctx, WC_OPT_RIX_TX, rix_tx) != WC_OK ||
         wc_set_option(ctx, WC_OPT_RIX_BLOCKED, rix_blocked) != WC_OK || wc_set_option(ctx, WC_OPT_RIX_XCD, rix_xcd) != WC_OK) {
-        std::fprintf(stderr, "options: %s\n", wc_last_error(ctx));
-        return 2;
-    }
-    // WCB_COHORT=S, WCB_COHORT_LAG=L: the cohort forward (WC_OPT_COHORT / _LAG)
-    const int cohort = std::getenv("WCB_COHORT") ? std::atoi(std::getenv("WCB_COHORT")) : 0;
-    const int cohort_lag = std::getenv("WCB_COHORT_LAG") ? std::atoi(std::getenv("WCB_COHORT_LAG")) : 2;
-    if (wc_set_option(ctx, WC_OPT_COHORT, cohort) != WC_OK || wc_set_option(ctx, WC_OPT_COHORT_LAG, cohort_lag) != WC_OK) {
         std::fprintf(stderr, "options: %s\n", wc_last_error(ctx));
         return 2;
     }
@@ -188,7 +186,10 @@ int main(int argc, char** argv) {
                 rc = wc_forward(ctx, (uint8_t*)cells + esz * per * chunk * g, f64 ? WC_F64 : WC_F32, units.data(),
                                 chunk, keep, payload + ccap * g, ccap, offsets + (chunk + 1) * g, kept + chunk * g);
         } else {
-            rc = wc_forward(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, keep, payload, cap, offsets, kept);
+            rc = rowinfo ? wc_forward_rows(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, keep, payload, cap,
+                                           offsets, kept, rowinfo, rowinfo_bytes)
+                         : wc_forward(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, keep, payload, cap,
+                                      offsets, kept);
         }
         if (rc != WC_OK) {
             std::fprintf(stderr, "wc_forward: %s\n", wc_last_error(ctx));
@@ -196,9 +197,11 @@ int main(int argc, char** argv) {
         }
     };
     auto inv = [&]() {
-        int rc = inv_mode == 2 ? wc_inverse_rmse(ctx, payload, offsets, units.data(), boxes, cells,
-                                                 f64 ? WC_F64 : WC_F32, regen, rmse)
-                               : wc_inverse(ctx, payload, offsets, units.data(), boxes, regen);
+        int rc = inv_mode == 3   ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, rowinfo, cells,
+                                                   f64 ? WC_F64 : WC_F32, regen, rmse)
+                 : inv_mode == 2 ? wc_inverse_rmse(ctx, payload, offsets, units.data(), boxes, cells,
+                                                   f64 ? WC_F64 : WC_F32, regen, rmse)
+                                 : wc_inverse(ctx, payload, offsets, units.data(), boxes, regen);
         if (rc != WC_OK) {
             std::fprintf(stderr, "wc_inverse: %s\n", wc_last_error(ctx));
             std::exit(2);
@@ -261,13 +264,11 @@ int main(int argc, char** argv) {
         run(off_a, k_a, pa, ra);
         wc_set_option(ctx, WC_OPT_ORDERED, 0);
         wc_set_option(ctx, WC_OPT_SPARSE, 0);
-        wc_set_option(ctx, WC_OPT_COHORT, 0);
         wc_set_option(ctx, WC_OPT_INVERSE_ROWS, 0);
         run(off_b, k_b, pb, rb);
         wc_set_option(ctx, WC_OPT_ORDERED, ordered);
         wc_set_option(ctx, WC_OPT_SPARSE, sparse);
         wc_set_option(ctx, WC_OPT_INVERSE_ROWS, rows);
-        wc_set_option(ctx, WC_OPT_COHORT, cohort);
         identical = 1;
         for (int i = 0; i < boxes && identical; ++i) {
             if (k_a[i] != k_b[i] || off_a[i] != off_b[i]) identical = 0;
@@ -281,12 +282,12 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(hk.data(), kept, 4 * boxes, hipMemcpyDeviceToHost));
     double ksum = 0;
     for (uint32_t k : hk) ksum += k;
-    const char* names[WC_NUM_STAGES] = {"transform", "emit", "decode", "inverse", "rmse", "hist", "cohort"};
+    const char* names[WC_NUM_STAGES] = {"transform", "emit", "decode", "inverse", "rmse", "hist", "pairs"};
     std::printf("{\"boxes\": %d, \"dim\": %d, \"dtype\": \"%s\", \"keep\": %.17g, \"steps\": %d, "
                 "\"ms_per_step\": %.4f, \"cells_per_s\": %.6e, \"kept_fraction\": %.6f, \"payload_bytes\": %llu, "
-                "\"ordered\": %d, \"sparse\": %d, \"cohort\": [%d, %d], \"rows\": %d, \"rix\": [%d, %d, %d], \"paths_identical\": %d, \"stage_ms\": {",
+                "\"ordered\": %d, \"sparse\": %d, \"rows\": %d, \"rix\": [%d, %d, %d], \"paths_identical\": %d, \"stage_ms\": {",
                 boxes, dim, f64 ? "f64" : "f32", keep, steps, step_ms, ncells / (step_ms * 1e-3),
-                ksum / (double)ncells, (unsigned long long)total, ordered, sparse, cohort, cohort_lag, rows, rix_lds, rix_tx, rix_blocked, identical);
+                ksum / (double)ncells, (unsigned long long)total, ordered, sparse, rows, rix_lds, rix_tx, rix_blocked, identical);
     bool first = true;
     for (int s = 0; s < WC_NUM_STAGES; ++s)
         if (cnt[s]) {
@@ -311,5 +312,6 @@ int main(int argc, char** argv) {
     (void)hipFree(kept);
     if (regen) (void)hipFree(regen);
     if (rmse) (void)hipFree(rmse);
+    if (rowinfo) (void)hipFree(rowinfo);
     return 0;
 }

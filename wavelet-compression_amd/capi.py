@@ -28,7 +28,8 @@ EXPORTED = (
     "wc_inverse", "wc_inverse_host", "wc_inverse_flat", "wc_rmse", "wc_version",
     "wc_profile_enable", "wc_profile_read", "wc_set_option", "wc_inverse_flat_host", "wc_rmse_host",
     "wc_decompose_host", "wc_device_count", "wc_forward_stage", "wc_hist_threshold",
-    "wc_forward_emit", "wc_inverse_rmse", "wc_get_option",
+    "wc_forward_emit", "wc_inverse_rmse", "wc_get_option", "wc_rowindex_bytes", "wc_forward_rows",
+    "wc_inverse_rows",
 )
 WC_OPT_SPARSE = 12   # sparse coefficient staging in the forward (default 1)
 WC_OPT_ORDERED = 13  # look-back tile index from the launch order (1, default) or per-unit tickets (0)
@@ -41,13 +42,11 @@ WC_OPT_SPIN_LIMIT = 19  # polls before a look-back wait is declared timed out (0
 WC_OPT_TICKETS = 20  # 1: ticket form whatever WC_OPT_ORDERED says (set by a look-back timeout: sticky)
 WC_OPT_RIX_XCD = 22  # row-indexed inverse tiles dealt to XCDs in contiguous runs (default 0)
 WC_OPT_INV_GROUPS = 23  # row-indexed inverse in N unit groups, row index of g+1 beside K6r of g (default 1)
-WC_OPT_COHORT = 24  # cohort forward: units per cohort (0 = off); large S32-shape units only
-WC_OPT_COHORT_LAG = 25  # cohort forward: pack of cohort p - lag beside the transform of cohort p (default 2)
 WC_OPT_HOST_THREADS = 27  # _host calls: threads that fault in a copy's host destination first (0 = off)
-WC_OPT_HOST_THP = 28  # _host calls: advise huge pages on those destinations (default 1)
+WC_OPT_HOST_THP = 28  # _host calls: advise huge pages on those destinations (default 0)
 
 # Stage ids of wc_profile_read (include/wavelet_amd.h WC_STAGE_*).
-STAGES = ("transform", "emit", "decode", "inverse", "rmse", "hist", "cohort")
+STAGES = ("transform", "emit", "decode", "inverse", "rmse", "hist", "pairs")
 
 
 class WcUnit(ctypes.Structure):
@@ -108,6 +107,9 @@ def load_library() -> ctypes.CDLL:
                                     ctypes.POINTER(ctypes.c_uint64)]),
         "wc_forward_emit": (i32, [vp, up, i32, ctypes.c_double, ctypes.POINTER(ctypes.c_float), vp, u64,
                                   vp, vp]),
+        "wc_rowindex_bytes": (u64, [up, i32]),
+        "wc_forward_rows": (i32, [vp, vp, i32, up, i32, ctypes.c_double, vp, u64, vp, vp, vp, u64]),
+        "wc_inverse_rows": (i32, [vp, vp, vp, up, i32, vp, vp, i32, vp, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -141,6 +143,11 @@ def make_units(dims: Sequence[Sequence[int]], offsets: Iterable[int] | None = No
 
 def payload_bound(units, n) -> int:
     return int(load_library().wc_payload_bound(units, n))
+
+
+def rowindex_bytes(units, n) -> int:
+    """Bytes of a batch's row index (wc_rowindex_bytes: W*H + 1 entries of 8 B per unit)."""
+    return int(load_library().wc_rowindex_bytes(units, n))
 
 
 def _share_torch_runtime():
@@ -223,6 +230,21 @@ class Context:
         self._check(self._L.wc_forward(self._h, ctypes.c_void_p(d_cells), dtype, units, n,
                                        float(keep), ctypes.c_void_p(d_payload), capacity,
                                        ctypes.c_void_p(d_offsets), ctypes.c_void_p(d_kept)))
+
+    def forward_rows(self, d_cells: int, dtype: int, units, n: int, keep: float, d_payload: int,
+                     capacity: int, d_offsets: int, d_kept: int, d_rowinfo: int, rowinfo_capacity: int):
+        """wc_forward that also writes the payloads' row index (include/wavelet_amd.h)."""
+        self._check(self._L.wc_forward_rows(self._h, ctypes.c_void_p(d_cells), dtype, units, n, float(keep),
+                                            ctypes.c_void_p(d_payload), capacity, ctypes.c_void_p(d_offsets),
+                                            ctypes.c_void_p(d_kept), ctypes.c_void_p(d_rowinfo), rowinfo_capacity))
+
+    def inverse_rows(self, d_payload: int, d_offsets: int, units, n: int, d_rowinfo: int | None, d_out: int,
+                     d_orig: int | None = None, dtype: int = WC_F32, d_rmse: int | None = None):
+        """wc_inverse (d_orig None) or wc_inverse_rmse with the row index of
+        wc_forward_rows (d_rowinfo None: derived from the payloads)."""
+        self._check(self._L.wc_inverse_rows(self._h, ctypes.c_void_p(d_payload), ctypes.c_void_p(d_offsets),
+                                            units, n, ctypes.c_void_p(d_rowinfo or 0), ctypes.c_void_p(d_orig or 0),
+                                            dtype, ctypes.c_void_p(d_out), ctypes.c_void_p(d_rmse or 0)))
 
     def forward_stage(self, d_cells: int, dtype: int, units, n: int, d_hist: int | None = None):
         """Global-threshold mode, step 1 (include/wavelet_amd.h): transform into

@@ -43,10 +43,11 @@ hipError_t launch_transform_fallback(hipStream_t, const void*, int, const UnitDe
 hipError_t launch_pack(hipStream_t, const UnitDev*, int, const uint32_t*, const uint8_t*, uint64_t*, uint8_t*);
 hipError_t launch_decode(hipStream_t, const UnitDev*, const FTile*, uint32_t, const FTile*, uint32_t,
                          unsigned long long*, uint32_t, const uint8_t*, const uint64_t*, uint32_t*,
-                         unsigned long long*, float*, uint2*, uint32_t*, int);
+                         unsigned long long*, float*, uint2*, uint32_t*, int, uint32_t*);
+hipError_t launch_pair_counts(hipStream_t, const UnitDev*, int, const uint8_t*, const uint64_t*, uint32_t*, uint32_t*);
 hipError_t launch_inverse_rows(hipStream_t, const RTile*, uint32_t, size_t, uint32_t, const uint8_t*,
                                const uint64_t*, const uint2*, float*, int, const void*, int, const UnitDev*, int,
-                               double*, double*, bool);
+                               double*, double*, bool, const uint32_t*);
 hipError_t launch_inverse(hipStream_t, const float*, int, const UnitDev*, const XTile*, uint32_t, size_t, uint32_t,
                           size_t, float*);
 hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDev*, int, const FTile*,
@@ -54,7 +55,6 @@ hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDe
 hipError_t launch_emit(hipStream_t, const EmitParams&, const float*, uint32_t, uint32_t);
 hipError_t launch_hist(hipStream_t, const UnitDev*, const FTile*, uint32_t, const float*, uint32_t,
                        unsigned long long*);
-hipError_t launch_cohort(hipStream_t, const CohortParams&, const void*, int);
 }  // namespace wc
 
 using namespace wc;
@@ -88,17 +88,6 @@ struct Plan {
     // [ig_rd[g], ig_rd[g+1]) and its K6r tiles rtiles [ig_rt[g], ig_rt[g+1])
     std::vector<uint32_t> ig_rd, ig_rt;
     std::vector<EmitDesc> edesc;  // [units of kEmitTile tiles | units of kEmitTileBig tiles]
-    // cohort forward (wc_cohort.hip, build_cohort): every unit large and of the
-    // S32 shape; work list, emit descriptors (kEmitTile tiles, coef_off = ring
-    // slot offsets), ring of coh_ring units of coh_slot floats
-    int coh_size = 0, coh_lag = 0;    // WC_OPT_COHORT / WC_OPT_COHORT_LAG the plan was built with
-    bool coh = false;
-    std::vector<uint32_t> citems;
-    std::vector<EmitDesc> cedesc;
-    uint32_t coh_ring = 0;
-    uint64_t coh_slot = 0;
-    uint64_t coh_net = 0;              // cohort emit tiles (look-back granules)
-    size_t coh_state_bytes = 0;        // 16 (spare) | key[n] | kdone[n] | edone[n] | status[coh_net]
     uint32_t nedesc_small = 0;
     uint32_t ngen = 0, nfast = 0, netiles = 0;
     uint32_t ign = 0, ifast = 0;  // ixtiles split
@@ -110,7 +99,7 @@ struct Plan {
     uint64_t flag_bytes = 0;   // bytes of sparse-staging segment flags (UnitDev::flag_off ranges + slack)
     size_t lds_gen = 0, lds_fast = 0, lds_inverse = 0;
     size_t state_bytes = 0;    // forward per-call state: 16 | key[n] | tickets[n] | status[netiles]
-    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_edesc, d_ixtiles, d_rtiles, d_rdtiles, d_citems, d_cedesc;
+    DevBuf d_units, d_xtiles, d_ftiles, d_dtiles, d_edesc, d_ixtiles, d_rtiles, d_rdtiles;
 };
 
 int ceil_log2(int64_t v) {
@@ -140,8 +129,6 @@ struct wc_ctx {
     bool opt_rix_blocked = false; // WC_OPT_RIX_BLOCKED
     bool opt_rix_xcd = false;     // WC_OPT_RIX_XCD
     int opt_inv_groups = 1;       // WC_OPT_INV_GROUPS
-    int opt_cohort = 0;           // WC_OPT_COHORT (units per cohort; 0 = off)
-    int opt_cohort_lag = 2;       // WC_OPT_COHORT_LAG
     hipStream_t aux = nullptr;    // second stream of the pipelined inverse
     std::vector<hipEvent_t> iev;  // its events
     // A kernel that may raise error bits ran since the last check.  Kernels
@@ -155,7 +142,7 @@ struct wc_ctx {
     bool sparse_staged = false;  // the last stage_transform used sparse staging
     uint64_t plan_gen = 0;  // bumped whenever get_plan rebuilds the plan
     // scratch (grow-only)
-    DevBuf coef, part, errflag, state, flags, rowinfo, ring;
+    DevBuf coef, part, errflag, state, flags, rowinfo, npairs;
     // row index (wc_inverse): epoch-tagged look-back granules, zeroed when
     // allocated and never again (a granule of an earlier call reads as
     // unpublished); epoch: the call counter they are tagged with
@@ -171,7 +158,7 @@ struct wc_ctx {
     size_t pinned_bytes = 0;
     // host pages of a copy's destination faulted in ahead of it (wc_hostmem.h)
     int opt_host_threads = -1;    // WC_OPT_HOST_THREADS (-1: not yet resolved from the environment)
-    bool opt_host_thp = true;     // WC_OPT_HOST_THP
+    bool opt_host_thp = false;    // WC_OPT_HOST_THP (opt-in: the advice changes the caller's mappings)
     std::unique_ptr<wc::HostPool> hpool;
     // uploads from pageable host memory: copied by upool's threads into pinned
     // bounce slots, each slot's copy to the device ordered by an event
@@ -235,6 +222,13 @@ int validate_units(wc_ctx* c, const wc_unit* units, int n) {
             return fail(c, WC_ERR_INVALID, "unit " + std::to_string(i) + ": more than 2^31-1 cells");
     }
     return WC_OK;
+}
+
+// Device buffers: 16-B aligned (the kernels pick their vector widths from
+// element offsets; hipMalloc and torch allocations are 256-B aligned).
+int check_aligned(wc_ctx* c, const void* p, const char* what, uintptr_t align = 16) {
+    if (((uintptr_t)p & (align - 1)) == 0) return WC_OK;
+    return fail(c, WC_ERR_INVALID, std::string(what) + ": device buffer not " + std::to_string(align) + "-byte aligned");
 }
 
 hipEvent_t take_event(wc_ctx* c) {
@@ -382,102 +376,6 @@ void build_etiles(Plan& P, int n) {
     }
 }
 
-// The cohort forward's plan (wc_cohort.hip).  Eligible: every unit has the
-// S32 transform shape (32 x 1 x 32-block tiles, hx and hz multiples of 32,
-// even cell offset) and at least kEmitBigCells (< 2^30) cells.  Units form
-// cohorts of S in batch order; phase p lists cohort p's K1 tiles (unit-major)
-// merged evenly with cohort p - lag's emit tiles (interleaved by tile index
-// across the cohort's units: a unit's consecutive tiles are S apart, so a
-// look-back usually finds its predecessors published).  Ring slot of unit u:
-// u mod R, R = (lag + 2) S — a slot is rewritten two phases after its unit's
-// emit tiles were listed.
-#ifndef WC_COH_RUN
-#define WC_COH_RUN 1  // items of one kind per run of the cohort work list (8 measured slower: gpu_cohort_runs.txt)
-#endif
-void build_cohort(Plan& P, int n, int S, int lag) {
-    P.coh = false;
-    P.coh_size = S;
-    P.coh_lag = lag;
-    P.citems.clear();
-    P.cedesc.clear();
-    if (S <= 0 || n <= 0) return;
-    uint64_t maxc = 0;
-    for (int i = 0; i < n; ++i) {
-        const UnitDev& d = P.units[i];
-        const bool s32 = d.fast && d.lbx == 5 && d.lby == 0 && d.lbz == 5 && d.hx % 32 == 0 && d.hz % 32 == 0 &&
-                         (d.cell_off & 1) == 0;
-        if (!s32 || d.ncells < kEmitBigCells || d.ncells >= (uint64_t(1) << 30)) return;
-        maxc = std::max(maxc, d.ncells);
-    }
-    const uint32_t R = (uint32_t)std::min<int64_t>((int64_t)(lag + 2) * S, n);
-    const uint64_t slot = round_up(maxc, 32);
-    if ((uint64_t)R * slot * 4 >= (uint64_t(1) << 31)) return;  // buffer-resource range: 31 bits
-    std::vector<uint32_t> cet(n + 1, 0);
-    for (int i = 0; i < n; ++i) cet[i + 1] = cet[i] + (uint32_t)((P.units[i].ncells + kEmitTile - 1) / kEmitTile);
-    P.coh_net = cet[n];
-    for (int i = 0; i < n; ++i) {
-        const UnitDev& d = P.units[i];
-        for (uint32_t t = 0; t < cet[i + 1] - cet[i]; ++t) {
-            EmitDesc e{};
-            e.coef_off = (uint64_t)(i % R) * slot;
-            e.pay_off = d.pay_off;
-            e.ncells = d.ncells;
-            e.unit = (uint32_t)i;
-            e.index = t;
-            e.et_begin = cet[i];
-            e.net = cet[i + 1] - cet[i];
-            e.nx = d.nx;
-            e.ny = d.ny;
-            e.nz = d.nz;
-            e.sparse = 0;
-            e.lbz = d.lbz;
-            P.cedesc.push_back(e);
-        }
-    }
-    const int C = (n + S - 1) / S;
-    std::vector<uint32_t> k1, em;
-    for (int p = 0; p < C + lag; ++p) {
-        k1.clear();
-        em.clear();
-#ifndef WC_COH_XP_ELIST
-        if (p < C)
-#else
-        if (false)  // diagnostic (timing only): emit items only
-#endif
-            for (int i = p * S; i < std::min(n, (p + 1) * S); ++i)
-                for (uint32_t t = 0; t < P.units[i].ntx; ++t) k1.push_back(P.units[i].xt_begin + t);
-        const int q = p - lag;
-#ifdef WC_COH_XP_K1LIST
-        if (false) {  // diagnostic (timing only): K1 items only
-#else
-        if (q >= 0 && q < C) {
-#endif
-            const int a = q * S, b = std::min(n, (q + 1) * S);
-            uint32_t tmax = 0;
-            for (int i = a; i < b; ++i) tmax = std::max(tmax, cet[i + 1] - cet[i]);
-            for (uint32_t t = 0; t < tmax; ++t)
-                for (int i = a; i < b; ++i)
-                    if (t < cet[i + 1] - cet[i]) em.push_back(0x80000000u | (cet[i] + t));
-        }
-        // merge evenly in runs of WC_COH_RUN items of one kind: blocks are dealt
-        // round-robin to the 8 XCDs, so a run of 8 spreads each kind over all
-        // of them (alternating single items put every K1 tile on 4 XCDs and
-        // every emit tile on the other 4: profiles/r04/experiments/gpu_cohort_xp.txt)
-        const uint64_t A = (k1.size() + WC_COH_RUN - 1) / WC_COH_RUN, B = (em.size() + WC_COH_RUN - 1) / WC_COH_RUN;
-        uint64_t x = 0, y = 0;
-        while (x < A || y < B) {
-            const bool k = y >= B || (x < A && x * B <= y * A);
-            const std::vector<uint32_t>& v = k ? k1 : em;
-            const size_t a = (size_t)(k ? x++ : y++) * WC_COH_RUN;
-            P.citems.insert(P.citems.end(), v.begin() + a, v.begin() + std::min(v.size(), a + WC_COH_RUN));
-        }
-    }
-    P.coh_ring = R;
-    P.coh_slot = slot;
-    P.coh_state_bytes = round_up(16 + 16ull * n, 8) + 8ull * P.coh_net;
-    P.coh = true;
-}
-
 // K6r tiling (wc_inverse.hip k_inverse_rows): TX x TY blocks in (x, y), all of
 // z; the tile's LDS is 4 TX ranges of TY*D + 4 floats, at most kRixLds.  TX
 // up to 16 blocks (32-cell = 128-B output rows), then TY as large as fits
@@ -503,14 +401,13 @@ bool set_rix_tiling(UnitDev& d, int budget, int max_lx) {
 
 bool plan_matches(const wc_ctx* c, const Plan& P, const wc_unit* units, int n) {
     return P.inv_rows == c->opt_inv_rows && P.rix_lds == c->opt_rix_lds && P.rix_lx == c->opt_rix_lx &&
-           P.rix_xcd == c->opt_rix_xcd && P.inv_groups == c->opt_inv_groups && P.coh_size == c->opt_cohort &&
-           P.coh_lag == c->opt_cohort_lag &&
+           P.rix_xcd == c->opt_rix_xcd && P.inv_groups == c->opt_inv_groups &&
            (int)P.key.size() == n && (n == 0 || std::memcmp(P.key.data(), units, sizeof(wc_unit) * n) == 0);
 }
 
 void free_plan(Plan& P) {
-    DevBuf* bufs[] = {&P.d_units,   &P.d_xtiles, &P.d_ftiles, &P.d_dtiles, &P.d_edesc,
-                      &P.d_ixtiles, &P.d_rtiles, &P.d_rdtiles, &P.d_citems, &P.d_cedesc};
+    DevBuf* bufs[] = {&P.d_units,   &P.d_xtiles, &P.d_ftiles, &P.d_dtiles,
+                      &P.d_edesc,   &P.d_ixtiles, &P.d_rtiles, &P.d_rdtiles};
     for (DevBuf* b : bufs) {
         if (b->p) (void)hipFree(b->p);
         *b = DevBuf{};
@@ -584,6 +481,9 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         d.ntz = (d.nbz + (1 << d.lbz) - 1) >> d.lbz;
         d.pay_off = pay_cursor;  // slot of 20 + 8*ncells bytes + 4 pad: next slot stays == 4 (mod 8)
         pay_cursor += 24 + 8 * d.ncells;
+        // row index entries (include/wavelet_amd.h wc_rowindex_bytes): W*H + 1 per unit, every unit
+        d.row_off = P.rowinfo_entries;
+        P.rowinfo_entries += (uint64_t)u.nx * u.ny + 1;
         d.coef_off = (coef_cursor + 31) & ~uint64_t(31);  // 128 B: sparse-staging segments align
         coef_cursor = d.coef_off + d.ncells;
         if (d.ncells == 0) continue;
@@ -610,14 +510,13 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         else
             P.lds_gen = std::max(P.lds_gen, transform_lds_bytes(d.lbx, d.lby, d.lbz));
         P.lds_inverse = std::max(P.lds_inverse, transform_lds_bytes(d.lbx, d.lby, d.lbz));
+        if (d.fast) {  // the row-indexable shape: the forward can emit its row index (wc_forward_rows)
+            // floor(p / D) = (p * m) >> (31 + l), p < 2^31 (wc_device.h div_rows)
+            const int lg = ceil_log2(d.nz);
+            const uint64_t m = (uint64_t(1) << (31 + lg)) / (uint64_t)d.nz + 1;
+            d.dmagic = m | ((uint64_t)(31 + lg) << 32);
+        }
         if (P.inv_rows && set_rix_tiling(d, P.rix_lds, P.rix_lx)) {
-            d.row_off = P.rowinfo_entries;
-            P.rowinfo_entries += (uint64_t)d.nx * d.ny + 1;
-            {  // floor(p / D) = (p * m) >> (31 + l), p < 2^31 (wc_inverse.hip div_rows)
-                const int lg = ceil_log2(d.nz);
-                const uint64_t m = (uint64_t(1) << (31 + lg)) / (uint64_t)d.nz + 1;
-                d.dmagic = m | ((uint64_t)(31 + lg) << 32);
-            }
             d.rt_begin = (uint32_t)P.rtiles.size();
             for (int by = 0; by < d.hy; by += 1 << d.ilby)
                 for (int bx = 0; bx < d.hx; bx += 1 << d.ilbx) {
@@ -692,9 +591,6 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         uint64_t rix_cells = 0;
         for (UnitDev& d : P.units) {
             d.ndt = d.rix ? (uint32_t)(d.ncells / kRixTile) + 1 : d.nftiles;
-#ifdef WC_XP_RIX_CAP  // diagnostic (timing only): row-index tiles for a kept fraction of at most this
-            if (d.rix) d.ndt = std::min(d.ndt, (uint32_t)((double)d.ncells * WC_XP_RIX_CAP / kRixTile) + 2);
-#endif
             d.dt_begin = total;
             total += d.ndt;
             maxt = std::max(maxt, d.ndt);
@@ -739,7 +635,6 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
     P.coef_extent = coef_cursor ? coef_cursor + kFlatTile : 0;  // slack: flat tiles read whole float4 groups
     P.flag_bytes = flag_cursor + kEmitTileBig;                  // slack: a partial last tile's flag loads
     build_etiles(P, n);
-    build_cohort(P, n, c->opt_cohort, c->opt_cohort_lag);
     int rc;
     if ((rc = upload(c, P.d_units, P.units.data(), sizeof(UnitDev) * P.units.size(), "upload units")) ||
         (rc = upload(c, P.d_xtiles, P.xtiles.data(), sizeof(XTile) * P.xtiles.size(), "upload xtiles")) ||
@@ -748,9 +643,7 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         (rc = upload(c, P.d_dtiles, P.dtiles.data(), sizeof(FTile) * P.dtiles.size(), "upload dtiles")) ||
         (rc = upload(c, P.d_edesc, P.edesc.data(), sizeof(EmitDesc) * P.edesc.size(), "upload edesc")) ||
         (rc = upload(c, P.d_rtiles, P.rtiles.data(), sizeof(RTile) * P.rtiles.size(), "upload rtiles")) ||
-        (rc = upload(c, P.d_rdtiles, P.rdtiles.data(), sizeof(FTile) * P.rdtiles.size(), "upload rdtiles")) ||
-        (rc = upload(c, P.d_citems, P.citems.data(), sizeof(uint32_t) * P.citems.size(), "upload citems")) ||
-        (rc = upload(c, P.d_cedesc, P.cedesc.data(), sizeof(EmitDesc) * P.cedesc.size(), "upload cedesc")))
+        (rc = upload(c, P.d_rdtiles, P.rdtiles.data(), sizeof(FTile) * P.rdtiles.size(), "upload rdtiles")))
         return rc;
     // The host vectors back the async copies: finish them before returning.
     hipError_t e = hipStreamSynchronize(c->stream);
@@ -790,9 +683,9 @@ int ensure_scratch(wc_ctx* c) {
         (rc = ensure(c, c->flags, P.flag_bytes)) ||
         (rc = ensure(c, c->part, sizeof(double) * std::max<size_t>(nft, 4 * P.rtiles.size()))) ||
         (rc = ensure(c, c->rowinfo, sizeof(uint32_t) * 2 * std::max<uint64_t>(P.rowinfo_entries, 1))) ||
+        (rc = ensure(c, c->npairs, sizeof(uint32_t) * P.units.size())) ||
         (rc = ensure_zeroed(c, c->istate, istate_bytes(P))) ||
-        (rc = ensure(c, c->state, std::max({P.state_bytes, decode_state_bytes(P), P.coh_state_bytes}))) ||
-        (P.coh && (rc = ensure(c, c->ring, (size_t)P.coh_ring * P.coh_slot * sizeof(float)))))
+        (rc = ensure(c, c->state, std::max(P.state_bytes, decode_state_bytes(P)))))
         return rc;
     return WC_OK;
 }
@@ -915,7 +808,7 @@ int stage_transform(wc_ctx* c, const void* d_cells, int dtype, double keep, bool
 // (gthresh: the global-threshold mode's fp32 threshold, or null).  Uses the
 // unit keys and the zeroed tickets / look-back granules of the per-call state.
 int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_payload, uint64_t* d_offsets,
-               uint32_t* d_kept) {
+               uint32_t* d_kept, uint2* d_rows = nullptr) {
     Plan& P = c->plan;
     uint8_t* st = (uint8_t*)c->state.p;
     EmitParams p{};
@@ -936,6 +829,7 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
         p.gthresh = *gthresh;
     }
     p.flags = (c->sparse_staged && !gthresh) ? (const uint8_t*)c->flags.p : nullptr;
+    p.rowinfo = d_rows;
     StageTimer t(c, WC_STAGE_EMIT);
     hipError_t e = launch_emit(c->stream, p, (const float*)c->coef.p, P.nedesc_small,
                                (uint32_t)P.edesc.size() - P.nedesc_small);
@@ -944,54 +838,10 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
     return WC_OK;
 }
 
-// The cohort forward (wc_cohort.hip): K1 + emit of every unit in one
-// persistent launch, staging through the Infinity-Cache-resident ring.
-int forward_cohort(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
-                   uint64_t* d_offsets, uint32_t* d_kept) {
-    Plan& P = c->plan;
-    uint8_t* st = (uint8_t*)c->state.p;
-    hipError_t e = hipMemsetAsync(st, 0, P.coh_state_bytes, c->stream);
-    if (e != hipSuccess) return hip_fail(c, e, "memset cohort state");
-    CohortParams p{};
-    unsigned long long* key = (unsigned long long*)(st + 16);
-    p.E.units = (const UnitDev*)P.d_units.p;
-    p.E.edesc = (const EmitDesc*)P.d_cedesc.p;
-    p.E.n = n;
-    p.E.ordered = 1;
-    p.E.key = key;
-    p.E.status = (unsigned long long*)(st + round_up(16 + 16ull * n, 8));
-    p.E.payload = d_payload;
-    p.E.offsets = d_offsets;
-    p.E.kept = d_kept;
-    p.E.err = (uint32_t*)c->errflag.p;
-    p.E.keep = keep;
-    p.units = (const UnitDev*)P.d_units.p;
-    p.xtiles = (const XTile*)P.d_xtiles.p;
-    p.items = (const uint32_t*)P.d_citems.p;
-    p.nitems = (uint32_t)P.citems.size();
-    p.ring_units = P.coh_ring;
-    p.key = key;
-    p.kdone = (uint32_t*)(st + 16 + 8ull * n);
-    p.edone = (uint32_t*)(st + 16 + 12ull * n);
-    p.ring = (float*)c->ring.p;
-    p.ring_bytes = (uint32_t)(P.coh_ring * P.coh_slot * sizeof(float));
-    {
-        StageTimer t(c, WC_STAGE_COHORT);
-        e = launch_cohort(c->stream, p, d_cells, dtype);
-    }
-    if (e != hipSuccess) return hip_fail(c, e, "cohort launch");
-    c->sparse_staged = false;
-    c->err_check_pending = true;  // a wait that timed out surfaces at wc_synchronize
-    return WC_OK;
-}
-
 int forward_staged(wc_ctx* c, const void* d_cells, int dtype, int n, double keep, uint8_t* d_payload,
-                   uint64_t* d_offsets, uint32_t* d_kept) {
-    // the cohort launch relies on in-order dispatch (one block per item): the
-    // ticket form runs the two-kernel path
-    if (c->plan.coh && use_ordered(c)) return forward_cohort(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
+                   uint64_t* d_offsets, uint32_t* d_kept, uint2* d_rows = nullptr) {
     int rc = stage_transform(c, d_cells, dtype, keep, c->opt_sparse);
-    return rc ? rc : stage_emit(c, n, keep, nullptr, d_payload, d_offsets, d_kept);
+    return rc ? rc : stage_emit(c, n, keep, nullptr, d_payload, d_offsets, d_kept, d_rows);
 }
 
 uint64_t cells_extent(const wc_unit* units, int n) {
@@ -1058,8 +908,7 @@ void wc_ctx_destroy(wc_ctx* c) {
                       &c->h_offsets,     &c->h_poff,         &c->h_kept,         &c->h_out,
                       &c->plan.d_units,  &c->plan.d_xtiles,  &c->plan.d_ftiles,  &c->plan.d_dtiles,
                       &c->plan.d_edesc, &c->plan.d_ixtiles, &c->plan.d_rtiles,
-                      &c->plan.d_rdtiles, &c->plan.d_citems, &c->plan.d_cedesc, &c->rowinfo, &c->istate,
-                      &c->ring};
+                      &c->plan.d_rdtiles, &c->rowinfo,    &c->istate,        &c->npairs};
     for (DevBuf* b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (Plan& P : c->plan_cache) free_plan(P);
@@ -1145,14 +994,6 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
         case WC_OPT_TICKETS:
             c->force_tickets = value != 0;
             return WC_OK;
-        case WC_OPT_COHORT:
-            if (value < 0 || value > 64) return fail(c, WC_ERR_INVALID, "WC_OPT_COHORT: 0..64 units");
-            c->opt_cohort = (int)value;
-            return WC_OK;
-        case WC_OPT_COHORT_LAG:
-            if (value < 1 || value > 8) return fail(c, WC_ERR_INVALID, "WC_OPT_COHORT_LAG: 1..8 cohorts");
-            c->opt_cohort_lag = (int)value;
-            return WC_OK;
         case WC_OPT_HOST_THREADS:
             if (value < -1 || value > 256) return fail(c, WC_ERR_INVALID, "WC_OPT_HOST_THREADS: -1..256");
             c->opt_host_threads = (int)value;
@@ -1179,8 +1020,6 @@ int wc_get_option(const wc_ctx* c, int option, int64_t* value) {
         case WC_OPT_HOST_CHUNK: *value = c->opt_host_chunk; return WC_OK;
         case WC_OPT_SPIN_LIMIT: *value = c->opt_spin_limit; return WC_OK;
         case WC_OPT_TICKETS: *value = c->force_tickets ? 1 : 0; return WC_OK;
-        case WC_OPT_COHORT: *value = c->opt_cohort; return WC_OK;
-        case WC_OPT_COHORT_LAG: *value = c->opt_cohort_lag; return WC_OK;
         case WC_OPT_HOST_THREADS:
             *value = c->opt_host_threads < 0 ? host_threads_default() : c->opt_host_threads;
             return WC_OK;
@@ -1220,9 +1059,39 @@ int wc_forward(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, 
     if (n == 0) return WC_OK;
     if (!d_cells || !d_payload || !d_offsets || !d_kept) return fail(c, WC_ERR_INVALID, "null buffer");
     if (cap < wc_payload_bound(units, n)) return fail(c, WC_ERR_INVALID, "payload_capacity < wc_payload_bound");
+    if ((rc = check_aligned(c, d_cells, "cells")) || (rc = check_aligned(c, d_payload, "payload")) ||
+        (rc = check_aligned(c, d_offsets, "offsets", 8)) || (rc = check_aligned(c, d_kept, "kept", 4)))
+        return rc;
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
     if ((rc = ensure_scratch(c))) return rc;
     return forward_staged(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept);
+}
+
+uint64_t wc_rowindex_bytes(const wc_unit* units, int n) {
+    uint64_t e = 0;
+    for (int i = 0; i < n; ++i) e += (uint64_t)units[i].nx * units[i].ny + 1;
+    return 8 * e;
+}
+
+int wc_forward_rows(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, int n, double keep,
+                    uint8_t* d_payload, uint64_t cap, uint64_t* d_offsets, uint32_t* d_kept, void* d_rowinfo,
+                    uint64_t rowinfo_capacity) {
+    if (!c) return WC_ERR_INVALID;
+    int rc;
+    if ((rc = validate_units(c, units, n))) return rc;
+    if (dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
+    if (n == 0) return WC_OK;
+    if (!d_cells || !d_payload || !d_offsets || !d_kept || !d_rowinfo) return fail(c, WC_ERR_INVALID, "null buffer");
+    if (cap < wc_payload_bound(units, n)) return fail(c, WC_ERR_INVALID, "payload_capacity < wc_payload_bound");
+    if (rowinfo_capacity < wc_rowindex_bytes(units, n))
+        return fail(c, WC_ERR_INVALID, "rowinfo_capacity < wc_rowindex_bytes");
+    if ((rc = check_aligned(c, d_cells, "cells")) || (rc = check_aligned(c, d_payload, "payload")) ||
+        (rc = check_aligned(c, d_offsets, "offsets", 8)) || (rc = check_aligned(c, d_kept, "kept", 4)) ||
+        (rc = check_aligned(c, d_rowinfo, "rowinfo", 8)))
+        return rc;
+    if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
+    if ((rc = ensure_scratch(c))) return rc;
+    return forward_staged(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept, (uint2*)d_rowinfo);
 }
 
 int wc_forward_stage(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, int n, uint64_t* d_hist) {
@@ -1232,6 +1101,7 @@ int wc_forward_stage(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* u
     if (dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
     if (n == 0) return WC_OK;
     if (!d_cells) return fail(c, WC_ERR_INVALID, "null buffer");
+    if ((rc = check_aligned(c, d_cells, "cells"))) return rc;
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
     // dense staging: the histogram and any later threshold need every coefficient
     if ((rc = ensure_scratch(c)) || (rc = stage_transform(c, d_cells, dtype, 0.0, false))) return rc;
@@ -1287,6 +1157,9 @@ int wc_forward_emit(wc_ctx* c, const wc_unit* units, int n, double keep, const f
     if (n == 0) return WC_OK;
     if (!d_payload || !d_offsets || !d_kept) return fail(c, WC_ERR_INVALID, "null buffer");
     if (cap < wc_payload_bound(units, n)) return fail(c, WC_ERR_INVALID, "payload_capacity < wc_payload_bound");
+    if ((rc = check_aligned(c, d_payload, "payload")) || (rc = check_aligned(c, d_offsets, "offsets", 8)) ||
+        (rc = check_aligned(c, d_kept, "kept", 4)))
+        return rc;
     const bool staged = c->staged;
     const uint64_t gen = c->plan_gen;
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
@@ -1311,6 +1184,7 @@ int wc_decompose(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units
     if (dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
     if (n == 0) return WC_OK;
     if (!d_cells || !d_flat) return fail(c, WC_ERR_INVALID, "null buffer");
+    if ((rc = check_aligned(c, d_cells, "cells")) || (rc = check_aligned(c, d_flat, "flat"))) return rc;
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
     Plan& P = c->plan;
     const UnitDev* du = (const UnitDev*)P.d_units.p;
@@ -1329,8 +1203,11 @@ namespace {
 
 // wc_inverse, and with orig != null also calc_rmse_per_box fused into the
 // row-indexed inverse (every unit row-indexed; the caller checks).
+// user_rows (wc_inverse_rows): the caller's row index of these payloads, as
+// wc_forward_rows wrote it: K6r reads it and the row index kernel does not
+// run; units that are not row-indexed still decode densely.
 int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, int n, float* d_out,
-                 const void* d_orig, int dtype, double* d_rmse) {
+                 const void* d_orig, int dtype, double* d_rmse, const uint2* user_rows = nullptr) {
     Plan& P = c->plan;
     int rc = WC_OK;
     hipError_t e = hipSuccess;
@@ -1350,14 +1227,15 @@ int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets,
         c->epoch = 1;
     }
     const int ng = (int)P.ig_rd.size() - 1;  // row-indexed groups (0: none)
-    const bool piped = ng > 1 && !c->prof;   // profiling times each kernel alone
+    const bool piped = ng > 1 && !c->prof && !user_rows;  // profiling times each kernel alone
+    const uint2* rows_in = user_rows ? user_rows : (const uint2*)c->rowinfo.p;
     if (piped && (rc = inverse_stream(c, 2 * ng + 2))) return rc;
     auto rows = [&](int g, hipStream_t s) {  // K6r over group g's tiles
         const uint32_t t0 = P.ig_rt[g], nt = P.ig_rt[g + 1] - P.ig_rt[g];
         return launch_inverse_rows(s, (const RTile*)P.d_rtiles.p + t0, nt, P.lds_rows,
-                                   nt ? persistent_grid(c, 1, P.lds_rows) : 1u, d_payload, d_offsets,
-                                   (const uint2*)c->rowinfo.p, d_out, c->opt_rix_blocked ? 1 : 0, d_orig, dtype,
-                                   (const UnitDev*)P.d_units.p, n, (double*)c->part.p, d_rmse, g == ng - 1);
+                                   nt ? persistent_grid(c, 1, P.lds_rows) : 1u, d_payload, d_offsets, rows_in, d_out,
+                                   c->opt_rix_blocked ? 1 : 0, d_orig, dtype, (const UnitDev*)P.d_units.p, n,
+                                   (double*)c->part.p, d_rmse, g == ng - 1, (const uint32_t*)c->npairs.p);
     };
     auto index = [&](int g, hipStream_t s) {  // K5 over group g's tiles (g = ng: the dense decode)
         const bool dense = g == ng;
@@ -1365,7 +1243,8 @@ int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets,
                              dense ? (uint32_t)P.dtiles.size() : 0u, (const FTile*)P.d_rdtiles.p + (dense ? 0 : P.ig_rd[g]),
                              dense ? 0u : P.ig_rd[g + 1] - P.ig_rd[g], (unsigned long long*)c->istate.p, c->epoch,
                              d_payload, d_offsets, (uint32_t*)st, (unsigned long long*)(st + round_up(4ull * n, 8)),
-                             (float*)c->coef.p, (uint2*)c->rowinfo.p, (uint32_t*)c->errflag.p, ord ? 1 : 0);
+                             (float*)c->coef.p, (uint2*)c->rowinfo.p, (uint32_t*)c->errflag.p, ord ? 1 : 0,
+                             (uint32_t*)c->npairs.p);
     };
     if (piped) {
         // K5 of group g + 1 on the context stream beside K6r of group g on the
@@ -1395,19 +1274,25 @@ int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets,
         c->err_check_pending = true;
         return rc;
     }
-    {
+    if (ng > 0 && user_rows) {  // the row index is the caller's: check the headers, count the pairs
+        StageTimer t(c, WC_STAGE_PAIRS);
+        e = launch_pair_counts(c->stream, (const UnitDev*)P.d_units.p, n, d_payload, d_offsets,
+                               (uint32_t*)c->npairs.p, (uint32_t*)c->errflag.p);
+        if (e != hipSuccess) return hip_fail(c, e, "pair count launch");
+    }
+    if ((ng > 0 && !user_rows) || !P.dtiles.empty()) {  // a decode stage only when something launches
         StageTimer t(c, WC_STAGE_DECODE);
         for (int g = 0; g <= ng && e == hipSuccess; ++g)
-            if (g < ng || !P.dtiles.empty()) e = index(g, c->stream);
+            if ((g < ng && !user_rows) || (g == ng && !P.dtiles.empty())) e = index(g, c->stream);
     }
     if (e != hipSuccess) return hip_fail(c, e, "decode launch");
     {
         StageTimer t(c, WC_STAGE_INVERSE);
         for (int g = 0; g < ng && e == hipSuccess; ++g) e = rows(g, c->stream);
         if (e == hipSuccess && ng == 0 && d_orig)  // every unit empty: the per-unit RMSE (0) only
-            e = launch_inverse_rows(c->stream, nullptr, 0, 0, 1u, d_payload, d_offsets, (const uint2*)c->rowinfo.p,
-                                    d_out, 0, d_orig, dtype, (const UnitDev*)P.d_units.p, n, (double*)c->part.p,
-                                    d_rmse, true);
+            e = launch_inverse_rows(c->stream, nullptr, 0, 0, 1u, d_payload, d_offsets, rows_in, d_out, 0, d_orig,
+                                    dtype, (const UnitDev*)P.d_units.p, n, (double*)c->part.p, d_rmse, true,
+                                    (const uint32_t*)c->npairs.p);
         if (e == hipSuccess)
             e = launch_inverse(c->stream, (const float*)c->coef.p, 0, (const UnitDev*)P.d_units.p,
                                (const XTile*)P.d_ixtiles.p, P.ign, P.lds_inverse, P.ifast, P.lds_fast, d_out);
@@ -1424,32 +1309,42 @@ extern "C" {
 
 int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
                float* d_out) {
-    if (!c) return WC_ERR_INVALID;
-    int rc;
-    if ((rc = validate_units(c, units, n))) return rc;
-    if (n == 0) return WC_OK;
-    if (!d_payload || !d_offsets || !d_out) return fail(c, WC_ERR_INVALID, "null buffer");
-    if ((rc = set_device(c)) || (rc = get_plan(c, units, n)) || (rc = ensure_scratch(c))) return rc;
-    return inverse_impl(c, d_payload, d_offsets, n, d_out, nullptr, 0, nullptr);
+    return wc_inverse_rows(c, d_payload, d_offsets, units, n, nullptr, nullptr, WC_F32, d_out, nullptr);
 }
 
 int wc_inverse_rmse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
                     const void* d_orig, int dtype, float* d_out, double* d_rmse) {
     if (!c) return WC_ERR_INVALID;
+    if (n > 0 && (!d_orig || !d_rmse)) return fail(c, WC_ERR_INVALID, "null buffer");
+    return wc_inverse_rows(c, d_payload, d_offsets, units, n, nullptr, d_orig, dtype, d_out, d_rmse);
+}
+
+// wc_inverse / wc_inverse_rmse, and with d_rowinfo the caller's row index in
+// place of the row index kernel (wc_forward_rows wrote it for these payloads).
+int wc_inverse_rows(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
+                    const void* d_rowinfo, const void* d_orig, int dtype, float* d_out, double* d_rmse) {
+    if (!c) return WC_ERR_INVALID;
     int rc;
     if ((rc = validate_units(c, units, n))) return rc;
-    if (dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
+    if (d_orig && dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
     if (n == 0) return WC_OK;
-    if (!d_payload || !d_offsets || !d_out || !d_orig || !d_rmse) return fail(c, WC_ERR_INVALID, "null buffer");
+    if (!d_payload || !d_offsets || !d_out || (!d_orig != !d_rmse)) return fail(c, WC_ERR_INVALID, "null buffer");
+    if ((rc = check_aligned(c, d_payload, "payload")) || (rc = check_aligned(c, d_offsets, "offsets", 8)) ||
+        (rc = check_aligned(c, d_out, "out")) || (rc = check_aligned(c, d_rowinfo, "rowinfo", 8)) ||
+        (rc = check_aligned(c, d_rmse, "rmse", 8)) ||
+        (rc = check_aligned(c, d_orig, "orig", dtype == WC_F64 ? 8 : 4)))
+        return rc;
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n)) || (rc = ensure_scratch(c))) return rc;
+    const uint2* rows = (const uint2*)d_rowinfo;
+    if (!d_orig) return inverse_impl(c, d_payload, d_offsets, n, d_out, nullptr, 0, nullptr, rows);
     const Plan& P = c->plan;
     bool all_rix = true;
     for (const UnitDev& d : P.units) all_rix &= d.rix != 0 || d.ncells == 0;
     if (!all_rix) {  // some units decode densely: the two calls, same results
-        if ((rc = inverse_impl(c, d_payload, d_offsets, n, d_out, nullptr, 0, nullptr))) return rc;
+        if ((rc = inverse_impl(c, d_payload, d_offsets, n, d_out, nullptr, 0, nullptr, rows))) return rc;
         return wc_rmse(c, d_orig, dtype, d_out, units, n, d_rmse);
     }
-    return inverse_impl(c, d_payload, d_offsets, n, d_out, d_orig, dtype == WC_F64 ? 1 : 0, d_rmse);
+    return inverse_impl(c, d_payload, d_offsets, n, d_out, d_orig, dtype == WC_F64 ? 1 : 0, d_rmse, rows);
 }
 
 int wc_inverse_flat(wc_ctx* c, const float* d_flat, const wc_unit* units, int n, float* d_out) {
@@ -1458,6 +1353,7 @@ int wc_inverse_flat(wc_ctx* c, const float* d_flat, const wc_unit* units, int n,
     if ((rc = validate_units(c, units, n))) return rc;
     if (n == 0) return WC_OK;
     if (!d_flat || !d_out) return fail(c, WC_ERR_INVALID, "null buffer");
+    if ((rc = check_aligned(c, d_flat, "flat")) || (rc = check_aligned(c, d_out, "out"))) return rc;
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
     Plan& P = c->plan;
     StageTimer t(c, WC_STAGE_INVERSE);
@@ -1565,7 +1461,7 @@ static int host_threads_default() {
 // Resolved on the call's thread before any helper thread starts; null = off.
 struct Populate {
     wc::HostPool* pool = nullptr;
-    bool on = false, thp = true;
+    bool on = false, thp = false;
     void operator()(void* p, size_t bytes) const {
         if (on && bytes) wc::populate_for_write(pool, p, bytes, thp);
     }

@@ -344,6 +344,60 @@ __device__ __forceinline__ uint64_t wave_incl_sum(uint64_t v) {
     return v;
 }
 
+// Wave-wide inclusive sum of 32-bit values on DPP lane moves (wave_incl_sum's
+// pattern); lanes whose source is out of range read 0.
+__device__ __forceinline__ uint32_t wave_incl_sum32(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// The row index of a payload (include/wavelet_amd.h wc_rowindex_bytes): for
+// every flat row r = I*H + J of a unit (D consecutive flat coefficients, x
+// slowest / z fastest, src/compressor.cpp:178-181) the entry (k, p_k - r*D),
+// k the first pair whose flat position p_k is >= r*D (nrle and ncoeff when
+// there is none), plus the sentinel row W*H.  Written by the row index kernel
+// from a payload (wc_inverse.hip k_rowindex) or by the emit as it packs the
+// pairs (wc_emit.h, wc_forward_rows); read by K6r.
+
+// floor(p / D) for p < 2^31 (Granlund-Montgomery, N = 31): dmagic = m |
+// (31 + l) << 32, l = ceil(log2 D), m = floor(2^(31+l) / D) + 1 < 2^32.
+__device__ __forceinline__ uint32_t div_rows(uint32_t p, uint64_t dmagic) {
+    return (uint32_t)(((uint64_t)p * (uint32_t)dmagic) >> (uint32_t)(dmagic >> 32));
+}
+
+// Rows [r_lo, r_lo + cnt) of this lane get (k, p - r * D).  Most lanes write 0
+// or 1 row; a long run of zeros (empty rows) is spread over the whole wave.
+// Every lane of the wave calls it (uniform control flow).
+__device__ __forceinline__ void write_rows(uint2* __restrict__ ri, uint32_t r_lo, uint32_t cnt, uint32_t k,
+                                           uint32_t p, uint32_t D, int l) {
+    if (!__ballot(cnt > 1)) {
+        if (cnt) ri[r_lo] = make_uint2(k, p - r_lo * D);
+        return;
+    }
+    const uint32_t incl = wave_incl_sum32(cnt);
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+    const uint32_t excl = incl - cnt;
+    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
+        const uint32_t job = j0 + (uint32_t)l;
+        int o = 0;  // first lane whose inclusive count exceeds job
+#pragma unroll
+        for (int s = 32; s >= 1; s >>= 1)
+            if ((uint32_t)__shfl(incl, o + s - 1) <= job) o += s;
+        o = o > 63 ? 63 : o;
+        const uint32_t orl = __shfl(r_lo, o), oex = __shfl(excl, o), ok = __shfl(k, o), op = __shfl(p, o);
+        if (job < total) {
+            const uint32_t r = orl + (job - oex);
+            ri[r] = make_uint2(ok, op - r * D);
+        }
+    }
+}
+
 // Uniform reads of launch-constant tables (plan descriptors, tile lists) through
 // the constant address space: scalar loads even after the kernel has stored to
 // global memory (a vector load's vmcnt wait would also wait for loads in flight).

@@ -1,6 +1,6 @@
 // wc_emit.h — the emit tile body (K2: keep threshold + ordered pack of staged
-// coefficients), shared by k_emit (wc_emit.hip) and the cohort forward
-// (wc_cohort.hip).  See wc_emit.hip for the algorithm and its reference lines.
+// coefficients) of k_emit (wc_emit.hip).  See wc_emit.hip for the algorithm
+// and its reference lines.
 #pragma once
 
 #include "wc_xform.h"
@@ -33,6 +33,14 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Row-index output of one unit (wc_forward_rows; dmagic == 0: none): its
+// entries, the Granlund-Montgomery constant of D, and D.
+struct RowOut {
+    uint2* __restrict__ ri;
+    uint64_t dmagic;
+    uint32_t D;
+};
+
 // Emit the kept coefficients of one kEmitTile chunk held in q (thread (w, l)
 // owns elements w*2048 + it*256 + 4l + j; kb bit it*4 + j = kept) as (run,
 // value) pairs: ranks from per-column ballots, run = f - prev - 1 (taken at
@@ -46,8 +54,15 @@ __device__ __forceinline__ uint32_t mbcnt64(unsigned long long m) {
 // four sparse, partial-line scatters; two blocks per copy-out fill the last
 // row of a copy better).  A wave's LDS operations execute in order, so the
 // stage needs no barrier.
+//
+// kRows (wc_forward_rows): pair k = rank + i at flat index f, the previous
+// pair's index pf, also writes the row entries of the rows whose first flat
+// position lies in (pf, f] (write_rows, wc_device.h): (k, f - r*D).
+template <bool kRows>
 __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, uint32_t start, int w, int l,
-                                           uint32_t rank, uint32_t prev, uint2* __restrict__ pairs, uint2* stage) {
+                                           uint32_t rank, uint32_t prev, uint2* __restrict__ pairs, uint2* stage,
+                                           const RowOut& ro) {
+    static_assert(!kRows || WC_EMIT_RUNLATE, "the row-index output needs the late-run copy-out");
     uint32_t soff = 0;  // pairs staged since the last copy-out
 #if !WC_EMIT_RUNLATE
     const unsigned long long lt = (1ull << l) - 1ull;
@@ -100,9 +115,6 @@ __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, ui
         // copy-out every WC_EMIT_SB blocks of 256 elements (the stage holds their pairs)
         if (it % WC_EMIT_SB == WC_EMIT_SB - 1 && soff) {
             __builtin_amdgcn_wave_barrier();
-#ifdef WC_XP_E_NOSTORE
-            if (soff == 0x7fffffffu)
-#endif
 #if WC_EMIT_RUNLATE
             {
                 // run = f - (previous pair's f) - 1: the previous pair is lane
@@ -116,6 +128,14 @@ __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, ui
                     const uint32_t left = dpp_u32<0x138, 0xf>(e.x);  // wave_shr:1
                     const uint32_t pf = l == 0 ? carry : left;
                     if (k < soff) pairs[rank + k] = make_uint2(e.x - pf - 1u, e.y);
+                    if constexpr (kRows) {
+                        if (ro.dmagic) {  // uniform: rows (floor(pf / D), floor(f / D)] start in (pf, f]
+                            const int32_t rhi = k < soff ? (int32_t)div_rows(e.x, ro.dmagic) : -1;
+                            const int32_t rlo = pf == 0xffffffffu ? 0 : (int32_t)div_rows(pf, ro.dmagic) + 1;
+                            write_rows(ro.ri, (uint32_t)rlo, rhi >= rlo ? (uint32_t)(rhi - rlo + 1) : 0u, rank + k,
+                                       e.x, ro.D, l);
+                        }
+                    }
                     carry = __builtin_amdgcn_readlane(e.x, 63);
                 }
                 prev = __builtin_amdgcn_readlane(e.x, (soff - 1u) & 63u);  // the last pair's index
@@ -183,11 +203,8 @@ __device__ __forceinline__ void finish_unit(const EmitParams& P, const EmitDesc&
 
 constexpr unsigned long long kMask31 = 0x7fffffffull;
 
-// Staged-coefficient sources of emit_tile:
-//   PlainSrc  (k_emit) coefficients and unit keys written by EARLIER launches:
-//             plain (and scalar) loads
-//   the cohort forward's source (wc_cohort.hip) reads coefficients staged in
-//   the SAME launch, write-through (sc1) on both sides.
+// Staged-coefficient source of emit_tile: coefficients and unit keys written
+// by EARLIER launches (K1), read with plain (and scalar) loads.
 struct PlainTile {
     const float4* __restrict__ p;
     __device__ __forceinline__ float4 operator[](int i) const { return p[i]; }
@@ -204,7 +221,9 @@ struct PlainSrc {
 
 // Threshold + ordered pack of tile `index` of unit `u`.  Thread t = (wave w,
 // lane l) owns elements w*2048 + it*256 + 4l + j, it 0..7.  sm: 16 LDS words.
-template <int EW, class Src>
+// kRows: also the unit's row index (P.rowinfo; the pairs' rows in
+// emit_pairs, the rows after the unit's last pair by its last tile).
+template <int EW, bool kRows, class Src>
 __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, const EmitDesc& U, uint32_t index,
                                           uint32_t* sm, uint2* stage, int tid) {
     constexpr uint32_t kTile = EW * 2048;
@@ -221,6 +240,12 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
     // segments its flags skipped once the threshold is known (rare).
     unsigned long long ukey = 0;
     if constexpr (kKeyPar) ukey = src.key(P, u);
+    RowOut ro{nullptr, 0ull, 0u};
+    if constexpr (kRows) {  // uniform scalar loads, first needed at the pair copy-out
+        ro.dmagic = cst(P.units)[u].dmagic;
+        ro.ri = P.rowinfo + cst(P.units)[u].row_off;
+        ro.D = (uint32_t)U.nz;
+    }
     uint32_t segf = 0xffu;  // bit it: group it may hold kept coefficients
     if (sparse) {
         // one flag byte per segment of TZ = 2^lbz coefficients (16 or 32)
@@ -310,9 +335,6 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
             // inclusive one are summed once every one of them has published;
             // a run of published aggregates before the first unpublished tile
             // is summed and the window slides past it.
-#ifdef WC_XP_E_NOLB
-            if (pos == -7)
-#endif
             for (uint32_t spins = 0;;) {
                 const int64_t idx = pos - l;
                 const unsigned long long v = idx >= first ? ld_rlx(P.status + idx) : kFlagIncl;
@@ -339,7 +361,11 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
         if (l == 0) {
             sm[0] = ecnt;
             sm[1] = elast;
-            if (index + 1 == U.net) finish_unit(P, U, ecnt + C);  // last tile
+            if (index + 1 == U.net) {  // last tile
+                finish_unit(P, U, ecnt + C);
+                sm[2] = ecnt + C;           // the unit's pair count
+                sm[3] = L1 ? L1 : elast;    // its last kept flat index + 1 (0: none)
+            }
         }
     }
     __syncthreads();
@@ -354,7 +380,19 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
         if (sm[4 + EW + i]) prev = start + sm[4 + EW + i] - 1u;
     }
     uint2* __restrict__ pairs = reinterpret_cast<uint2*>(P.payload + U.pay_off + 20);
-    emit_pairs(q, kb, start, w, l, rank, prev, pairs, stage);
+    emit_pairs<kRows>(q, kb, start, w, l, rank, prev, pairs, stage, ro);
+    if constexpr (kRows) {
+        // the rows after the unit's last pair and the sentinel row W*H: (nrle,
+        // ncoeff - r*D), as the virtual pair k = nrle at position ncoeff
+        if (ro.dmagic && index + 1 == U.net) {  // uniform
+            const uint32_t total = sm[2], last1 = sm[3];
+            const uint32_t rows = (uint32_t)U.nx * (uint32_t)U.ny;
+            const uint32_t nc = (uint32_t)U.ncells;
+            for (uint32_t r = (last1 ? div_rows(last1 - 1u, ro.dmagic) + 1u : 0u) + (uint32_t)tid; r <= rows;
+                 r += EW * kWave)
+                ro.ri[r] = make_uint2(total, nc - r * ro.D);
+        }
+    }
 }
 
 

@@ -28,6 +28,9 @@ namespace wc {
 #ifndef WC_EMIT_MINB
 #define WC_EMIT_MINB 8  // 4-wave launch: workgroups per CU the register budget is sized for (64 VGPRs)
 #endif
+#ifndef WC_EMIT_MINB_ROWS
+#define WC_EMIT_MINB_ROWS 6  // the same with the row-index output (wc_forward_rows): 80 VGPRs (72 spill)
+#endif
 #ifndef WC_EMIT_MINB8
 #define WC_EMIT_MINB8 2  // 8-wave launch (units of >= 2^21 cells)
 #endif
@@ -36,8 +39,9 @@ namespace wc {
 // in the ticket form.  The plan lists blocks interleaved by tile index across
 // the units of a group, groups in reverse transform order (wc_capi.cpp
 // build_etiles); units of kEmitBigCells or more cells form the 8-wave launch.
-template <int EW>
-__global__ __launch_bounds__(EW * kWave, EW == 8 ? WC_EMIT_MINB8 : WC_EMIT_MINB) void k_emit(EmitParams P,
+// ROWS (wc_forward_rows): the emit also writes the payloads' row index.
+template <int EW, bool ROWS>
+__global__ __launch_bounds__(EW * kWave, EW == 8 ? WC_EMIT_MINB8 : (ROWS ? WC_EMIT_MINB_ROWS : WC_EMIT_MINB)) void k_emit(EmitParams P,
                                                                            const float* __restrict__ coef) {
     __shared__ __attribute__((aligned(16))) uint32_t sm[32];
     __shared__ uint2 stage_all[EW][256 * WC_EMIT_SB];  // per-wave pair stage (emit_pairs)
@@ -45,22 +49,25 @@ __global__ __launch_bounds__(EW * kWave, EW == 8 ? WC_EMIT_MINB8 : WC_EMIT_MINB)
     uint2* stage = stage_all[tid >> 6];
     const EmitDesc E = P.edesc[blockIdx.x];
     if (P.ordered) {
-        emit_tile<EW>(P, PlainSrc{coef}, E, E.index, sm, stage, tid);
+        emit_tile<EW, ROWS>(P, PlainSrc{coef}, E, E.index, sm, stage, tid);
         return;
     }
     if (tid == 0) sm[31] = atomicAdd(P.tickets + E.unit, 1u);
     __syncthreads();
     const uint32_t index = __builtin_amdgcn_readfirstlane(sm[31]);
-    emit_tile<EW>(P, PlainSrc{coef}, E, index, sm, stage, tid);
+    emit_tile<EW, ROWS>(P, PlainSrc{coef}, E, index, sm, stage, tid);
 }
 
 hipError_t launch_emit(hipStream_t st, const EmitParams& p, const float* coef, uint32_t nsmall, uint32_t nbig) {
     static_assert(kEmitTile == WC_EMIT_EW * 2048 && kEmitTileBig == 8 * 2048, "emit tile sizes");
-    if (nsmall) k_emit<WC_EMIT_EW><<<nsmall, WC_EMIT_EW * kWave, 0, st>>>(p, coef);
-    if (nbig) {
-        EmitParams q = p;
-        q.edesc = p.edesc + nsmall;
-        k_emit<8><<<nbig, 8 * kWave, 0, st>>>(q, coef);
+    EmitParams q = p;
+    q.edesc = p.edesc + nsmall;
+    if (p.rowinfo) {
+        if (nsmall) k_emit<WC_EMIT_EW, true><<<nsmall, WC_EMIT_EW * kWave, 0, st>>>(p, coef);
+        if (nbig) k_emit<8, true><<<nbig, 8 * kWave, 0, st>>>(q, coef);
+    } else {
+        if (nsmall) k_emit<WC_EMIT_EW, false><<<nsmall, WC_EMIT_EW * kWave, 0, st>>>(p, coef);
+        if (nbig) k_emit<8, false><<<nbig, 8 * kWave, 0, st>>>(q, coef);
     }
     return hipGetLastError();
 }

@@ -136,23 +136,8 @@ struct EmitParams {
     uint32_t use_gthresh;          // 1: every unit uses gthresh (global histogram mode), 0: reference rule
     float gthresh;                 // fp32 threshold: keep |c| > gthresh
     const uint8_t* flags;          // sparse-staging segment flags (null: every unit dense)
-};
-
-// Parameter block of k_cohort (wc_cohort.hip), filled by wc_capi.cpp
-// forward_cohort: the cohort forward's work list (one block per item), its
-// per-unit counters and the staging ring.
-struct CohortParams {
-    EmitParams E;                  // emit fields: edesc = cohort emit descriptors (8192-coefficient tiles)
-    const UnitDev* units;
-    const XTile* xtiles;           // K1 tiles (the plan's list)
-    const uint32_t* items;         // work list: bit 31 set = emit (cohort edesc index), else xtile index
-    uint32_t nitems;
-    uint32_t ring_units;           // R: unit u stages into slot u mod R
-    unsigned long long* key;       // unit max keys (= E.key) } zeroed per call
-    uint32_t* kdone;               // K1 tiles finished      }
-    uint32_t* edone;               // emit tiles that have read their staging }
-    float* ring;                   // staging ring (E.edesc coef_off are slot offsets into it)
-    uint32_t ring_bytes;
+    uint2* rowinfo;                // wc_forward_rows: the payloads' row index out (null: not written);
+                                   // unit u's entries at units[u].row_off, units with dmagic != 0
 };
 
 constexpr int kSegShift = 4;    // sparse staging: flag index space of 16 coefficients per byte (min segment)

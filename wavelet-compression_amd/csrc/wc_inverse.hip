@@ -50,16 +50,6 @@ __device__ __forceinline__ bool read_header(const UnitDev& U, const uint8_t* __r
     return h[0] == U.nx && h[1] == U.ny && h[2] == U.nz && h[3] == (int32_t)U.ncells && nrle >= 0;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_sum32(uint32_t v) {
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return v;
-}
-
 // The same with saturating adds (v_add_u32 clamp): positions at or past
 // ncoeff (< 2^31) are all "dropped", so sums clamped at 2^32 - 1 decide the
 // same rows as exact ones.
@@ -73,38 +63,6 @@ __device__ __forceinline__ uint32_t wave_incl_sum32_sat(uint32_t v) {
     v = sat_add(v, __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));
     v = sat_add(v, __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));
     return v;
-}
-
-// floor(p / D) for p < 2^31 (Granlund-Montgomery, N = 31): dmagic = m |
-// (31 + l) << 32, l = ceil(log2 D), m = floor(2^(31+l) / D) + 1 < 2^32.
-__device__ __forceinline__ uint32_t div_rows(uint32_t p, uint64_t dmagic) {
-    return (uint32_t)(((uint64_t)p * (uint32_t)dmagic) >> (uint32_t)(dmagic >> 32));
-}
-
-// Rows [r_lo, r_lo + cnt) of this lane get (k, p - r * D).  Most lanes write 0
-// or 1 row; a long run of zeros (empty rows) is spread over the whole wave.
-__device__ __forceinline__ void write_rows(uint2* __restrict__ ri, uint32_t r_lo, uint32_t cnt, uint32_t k,
-                                           uint32_t p, uint32_t D, int l) {
-    if (!__ballot(cnt > 1)) {
-        if (cnt) ri[r_lo] = make_uint2(k, p - r_lo * D);
-        return;
-    }
-    const uint32_t incl = wave_incl_sum32(cnt);
-    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-    const uint32_t excl = incl - cnt;
-    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
-        const uint32_t job = j0 + (uint32_t)l;
-        int o = 0;  // first lane whose inclusive count exceeds job
-#pragma unroll
-        for (int s = 32; s >= 1; s >>= 1)
-            if ((uint32_t)__shfl(incl, o + s - 1) <= job) o += s;
-        o = o > 63 ? 63 : o;
-        const uint32_t orl = __shfl(r_lo, o), oex = __shfl(excl, o), ok = __shfl(k, o), op = __shfl(p, o);
-        if (job < total) {
-            const uint32_t r = orl + (job - oex);
-            ri[r] = make_uint2(ok, op - r * D);
-        }
-    }
 }
 
 // Row index of the row-indexed units.  Only the runs are needed (the values
@@ -130,7 +88,7 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDe
                                                      const uint64_t* __restrict__ offsets,
                                                      unsigned long long* __restrict__ status,
                                                      uint2* __restrict__ rowinfo, uint32_t* __restrict__ err,
-                                                     int ordered, uint32_t epoch) {
+                                                     int ordered, uint32_t epoch, uint32_t* __restrict__ npairs) {
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_x[2];
 #if WC_RIX_LDSV
@@ -147,6 +105,7 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDe
     int32_t nrle;
     const bool hok = read_header(U, ph, nrle);
     const uint32_t n = hok ? (uint32_t)nrle : 0u;
+    if (ft.index == 0 && tid == 0) npairs[u] = n;  // K6r bounds its pair indices by it
     // tiles up to the one holding the virtual pair k = n (the plan launches
     // floor(ncoeff / kRixTile) + 1, enough for the first dropped pair)
     if (ft.index > n / (uint32_t)kRixTile) return;  // uniform
@@ -205,9 +164,7 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDe
             if (l == 0) st_rlx(st, granule_e(kFlagIncl, epoch, tot));
         } else {
             if (l == 0) st_rlx(st + t, granule_e(kFlagAgg, epoch, tot));
-#ifndef WC_XP_NOLB
             excl = lookback_sum32e(st, (int64_t)t, l, err, epoch, timed_out);
-#endif
             if (l == 0) st_rlx(st + t, granule_e(kFlagIncl, epoch, sat_add(excl, tot)));
         }
         if (l == 0) {
@@ -258,9 +215,6 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDe
 #endif
         const int32_t rlo = (l == 0 ? carry : from) + 1;
         const uint32_t cnt = (k <= n && rhi >= rlo) ? (uint32_t)(rhi - rlo + 1) : 0u;
-#ifdef WC_XP_NOROWS
-        if (cnt == 12345u)
-#endif
         write_rows(ri, (uint32_t)rlo, cnt, k, phk, D, l);
         carry = __builtin_amdgcn_readlane(rhi, 63);
         if (carry < 0) break;  // uniform: lane 63 is past the virtual pair, so is every later round
@@ -651,7 +605,10 @@ struct RixRange {
     uint32_t ks, c0, e;  // rowinfo[r0] = (ks, c0), rowinfo[r0 + tyv].x = e
 };
 
-__device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* __restrict__ rowinfo, int w, int l) {
+// Pair indices are clamped to the payload's pair count npairs: an entry past
+// it (a row index that does not belong to this payload) reads no pair.
+__device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* __restrict__ rowinfo, uint32_t npairs,
+                                                   int w, int l) {
     RixRange R{0u, 0u, 0u};
     const int TX = 1 << T.lbx;
     if (l < TX) {
@@ -660,12 +617,22 @@ __device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* 
         if (bx < hx) {
             const uint64_t r0 = (uint64_t)(bx + ssx * hx) * T.H + T.by0 + ssy * hy;
             const uint2 a = rowinfo[T.row_off + r0];
-            R.ks = a.x;
+            R.ks = min(a.x, npairs);
             R.c0 = a.y;
-            R.e = rowinfo[T.row_off + r0 + T.tyv].x;
+            R.e = min(rowinfo[T.row_off + r0 + T.tyv].x, npairs);
         }
     }
     return R;
+}
+
+// Tile T's pairs in the payload; npairs[unit]: their count, checked against
+// the unit (k_rowindex or k_pair_counts: 0 for a header that disagrees).
+__device__ __forceinline__ const uint2* rix_payload(const uint8_t* __restrict__ payload,
+                                                    const uint64_t* __restrict__ offsets,
+                                                    const uint32_t* __restrict__ npairs, const RTile& T,
+                                                    uint32_t& np) {
+    np = cst(npairs)[T.unit];
+    return reinterpret_cast<const uint2*>(payload + offsets[T.unit] + 20);
 }
 
 // Per-lane range plan of a wave: pair count of range l (lanes < TX).
@@ -714,9 +681,6 @@ __device__ __forceinline__ void rix_scatter_range(float* __restrict__ reg, int R
         const uint32_t x = (i < cnt && i > 0) ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
         const uint32_t pos = carry + wave_incl_sum32(x);
         carry = __builtin_amdgcn_readlane(pos, 63);
-#ifdef WC_XP_NOSCATTER
-        if (q.y == 0x12345u)
-#endif
         if (i < cnt && pos < rlen) rg[pos] = __uint_as_float(q.y);
     }
 }
@@ -798,7 +762,9 @@ __device__ __forceinline__ void rix_load_orig(const void* __restrict__ orig, int
 // consecutive tiles share the payload lines at their range boundaries and the
 // unit's row entries) or strided (b, b + G, ...).
 // OT (fused calc_rmse_per_box, wc_inverse_rmse): 0 none, 1 fp64 original
-// cells, 2 fp32 original cells.  After the tile's synthesis (barrier), each
+// cells (16-B aligned: summed inside the x-quad synthesis), 2 fp32 original
+// cells, 3 fp64 original cells at a base that is not 16-B aligned (the
+// separate pass below, scalar loads).  After the tile's synthesis (barrier), each
 // wave re-reads part of the tile's output (L2-resident, just written) beside
 // the original cells and adds ((float)orig - regen)^2 in double; the wave's
 // sum goes to part[4 * tile + wave] and k_rmse_rows_final sums a unit's in
@@ -812,7 +778,8 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
                                                          const uint64_t* __restrict__ offsets,
                                                          const uint2* __restrict__ rowinfo, float* __restrict__ out,
                                                          int blocked, const void* __restrict__ orig,
-                                                         double* __restrict__ part) {
+                                                         double* __restrict__ part,
+                                                         const uint32_t* __restrict__ npairs) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     uint32_t G = gridDim.x, t = blockIdx.x, tend = ntiles;
@@ -826,8 +793,9 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
 
     // prologue: tile t's ranges and pairs in flight, tile t + G's row entries
     RTile T = tiles[t];
-    const uint2* pr = reinterpret_cast<const uint2*>(payload + offsets[T.unit] + 20);
-    RixRange R = rix_load_range(T, rowinfo, w, l);
+    uint32_t np;
+    const uint2* pr = rix_payload(payload, offsets, npairs, T, np);
+    RixRange R = rix_load_range(T, rowinfo, np, w, l);
     RixPlan PL = rix_plan(T, R, l);
     // prefetch slots, one per range (a wave owns at most 16 ranges at the
     // default WC_OPT_RIX_TX); the RMSE sums need registers
@@ -840,8 +808,9 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
     const uint2* pr1 = pr;
     if (t1 < tend) {
         T1 = tiles[t1];
-        pr1 = reinterpret_cast<const uint2*>(payload + offsets[T1.unit] + 20);
-        R1 = rix_load_range(T1, rowinfo, w, l);
+        uint32_t np1;
+        pr1 = rix_payload(payload, offsets, npairs, T1, np1);
+        R1 = rix_load_range(T1, rowinfo, np1, w, l);
     }
 
     for (;;) {
@@ -854,14 +823,10 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
             float4* r4 = reinterpret_cast<float4*>(reg);
             const uint32_t n4 = (uint32_t)(TX * RS) >> 2;
             for (uint32_t i = l; i < n4; i += 64) r4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-#ifndef WC_XP_NOSCANS
 #pragma unroll
             for (int j = 0; j < NR; ++j)
                 if (j < TX) rix_scatter_range(reg, RS, rlen, q[j], true, pr, R, PL, l, j);
             for (int j = NR; j < TX; ++j) rix_scatter_range(reg, RS, rlen, q[0], false, pr, R, PL, l, j);
-#else
-            if (q[0].x == 77u && q[5].y == 3u) reg[0] = 1.0f;
-#endif
         }
         __syncthreads();
 
@@ -876,8 +841,9 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
             rix_prefetch<NR>(q, pr1, R1, PL1, T1, l);
             if (t2 < tend) {
                 T2 = tiles[t2];
-                pr2 = reinterpret_cast<const uint2*>(payload + offsets[T2.unit] + 20);
-                R2 = rix_load_range(T2, rowinfo, w, l);
+                uint32_t np2;
+                pr2 = rix_payload(payload, offsets, npairs, T2, np2);
+                R2 = rix_load_range(T2, rowinfo, np2, w, l);
             }
         }
 
@@ -890,10 +856,7 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
             float* __restrict__ dst = out + T.cell_off;
             const int64_t sy = W, sz = (int64_t)W * H;
             const int64_t lo = (int64_t)(T.bx0 * 2);
-#ifdef WC_XP_NOPHASEC
-            if (tid < 0)
-#endif
-            f4 = WC_RIX_F4 && TX >= 2 && ((T.cell_off & 3) == 0) && ((W & 3) == 0);  // uniform
+            f4 = WC_RIX_F4 && TX >= 2 && ((T.cell_off & 3) == 0) && ((W & 3) == 0);  // uniform (out: 16-B aligned)
             if (f4) {
                 // two x-blocks x two z-blocks per thread: 16-B x-quad stores
                 const int nq = (TX >> 1) * TYv * (hz >> 1);
@@ -941,9 +904,6 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
 #pragma unroll
                             for (int dy = 0; dy < 2; ++dy) {
                                 float* p = dst + lo + 2 * bxl + sy * (2 * by + dy) + sz * (2 * (bzb + qb) + dz);
-#ifdef WC_XP_NOSTORE
-                                if (V[0][dz][dy][0] == 1.2345f)
-#endif
                                 *reinterpret_cast<float4*>(p) =
                                     make_float4(V[0][dz][dy][0], V[0][dz][dy][1], V[1][dz][dy][0], V[1][dz][dy][1]);
                             }
@@ -1034,7 +994,7 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
                 const uint32_t row = ci >> T.lbx;
                 const int64_t i = lo + 2 * x + sy * (int64_t)(row % (uint32_t)ny2) + sz * (int64_t)(row / (uint32_t)ny2);
                 float o0, o1;
-                if constexpr (OT == 1) {
+                if constexpr (OT == 1 || OT == 3) {
                     o0 = (float)((const double*)orig)[i];
                     o1 = (float)((const double*)orig)[i + 1];
                 } else {
@@ -1115,16 +1075,41 @@ static uint32_t resident_grid(const void* fn, size_t lds) {
     return (uint32_t)per_cu * (uint32_t)ncu;
 }
 
+// The pair count of every unit's payload, checked against the unit (the row
+// index of wc_inverse_rows comes from the caller, so k_rowindex, which checks
+// the headers otherwise, does not run): npairs[u] = nrle, or 0 and kErrHeader
+// for a header that disagrees (read_header).
+__global__ __launch_bounds__(kThreads) void k_pair_counts(const UnitDev* __restrict__ units, int n,
+                                                        const uint8_t* __restrict__ payload,
+                                                        const uint64_t* __restrict__ offsets,
+                                                        uint32_t* __restrict__ npairs, uint32_t* __restrict__ err) {
+    const int u = blockIdx.x * kThreads + threadIdx.x;
+    if (u >= n) return;
+    const UnitDev& U = units[u];
+    if (!U.rix) return;
+    int32_t nrle;
+    const bool ok = read_header(U, payload + offsets[u], nrle);
+    npairs[u] = ok ? (uint32_t)nrle : 0u;
+    if (!ok) atomicOr(err, kErrHeader);
+}
+
+hipError_t launch_pair_counts(hipStream_t st, const UnitDev* units, int n, const uint8_t* payload,
+                              const uint64_t* offsets, uint32_t* npairs, uint32_t* err) {
+    k_pair_counts<<<(n + kThreads - 1) / kThreads, kThreads, 0, st>>>(units, n, payload, offsets, npairs, err);
+    return hipGetLastError();
+}
+
 // K5.  Row-indexed units: the row index (epoch-tagged granules istate at
 // dt_begin, never zeroed per call).  Other units: the dense decode (zeroed
 // ticket / status).
 hipError_t launch_decode(hipStream_t st, const UnitDev* units, const FTile* ftiles, uint32_t nft,
                          const FTile* rtiles, uint32_t nrt, unsigned long long* istate, uint32_t epoch,
                          const uint8_t* payload, const uint64_t* offsets, uint32_t* ticket,
-                         unsigned long long* status, float* flat, uint2* rowinfo, uint32_t* err, int ordered) {
+                         unsigned long long* status, float* flat, uint2* rowinfo, uint32_t* err, int ordered,
+                         uint32_t* npairs) {
     if (nrt)
         k_rowindex<<<nrt, kThreads, 0, st>>>(units, rtiles, ticket, payload, offsets, istate, rowinfo, err, ordered,
-                                             epoch);
+                                             epoch, npairs);
     if (nft) k_decode<<<nft, kThreads, 0, st>>>(units, ftiles, payload, offsets, ticket, status, flat, err, ordered);
     return hipGetLastError();
 }
@@ -1162,7 +1147,7 @@ __global__ __launch_bounds__(64) void k_rmse_rows_final(const UnitDev* __restric
 hipError_t launch_inverse_rows(hipStream_t st, const RTile* tiles, uint32_t ntiles, size_t lds, uint32_t max_grid,
                                const uint8_t* payload, const uint64_t* offsets, const uint2* rowinfo, float* out,
                                int blocked, const void* orig, int dtype, const UnitDev* units, int n, double* part,
-                               double* rmse, bool rmse_final) {
+                               double* rmse, bool rmse_final, const uint32_t* npairs) {
     if (!ntiles) {
         if (orig && rmse_final) k_rmse_rows_final<<<n, 64, 0, st>>>(units, part, rmse);
         return hipGetLastError();
@@ -1170,13 +1155,16 @@ hipError_t launch_inverse_rows(hipStream_t st, const RTile* tiles, uint32_t ntil
     const uint32_t grid = std::min(ntiles, std::max(1u, max_grid));
     if (!orig)
         k_inverse_rows<0><<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out, blocked, orig,
-                                                       part);
-    else if (dtype == 1)
+                                                       part, npairs);
+    else if (dtype == 1 && ((uintptr_t)orig & 15) == 0)
         k_inverse_rows<1><<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out, blocked, orig,
-                                                       part);
+                                                       part, npairs);
+    else if (dtype == 1)
+        k_inverse_rows<3><<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out, blocked, orig,
+                                                       part, npairs);
     else
         k_inverse_rows<2><<<grid, kThreads, lds, st>>>(tiles, ntiles, payload, offsets, rowinfo, out, blocked, orig,
-                                                       part);
+                                                       part, npairs);
     if (orig && rmse_final) k_rmse_rows_final<<<n, 64, 0, st>>>(units, part, rmse);
     return hipGetLastError();
 }
