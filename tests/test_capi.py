@@ -119,8 +119,9 @@ def test_no_kernel_spills_to_scratch(tmp_path):
     import subprocess
     from pathlib import Path
     llvm = Path("/opt/rocm/lib/llvm/bin")
-    objs = sorted((Path(__file__).resolve().parent.parent / "wavelet-compression_amd" / "build").glob("wc_*.o"))
-    objs = [o for o in objs if o.name not in ("wc_capi.o", "wc_hostmem.o")]  # host code only
+    pkg = Path(__file__).resolve().parent.parent / "wavelet-compression_amd"
+    kernels = {p.stem for p in (pkg / "csrc").glob("*.hip")}  # the .cpp objects are host code only
+    objs = sorted(o for o in (pkg / "build").glob("wc_*.o") if o.stem in kernels)
     if not llvm.exists() or not objs:
         pytest.skip("ROCm LLVM tools or built objects absent")
     seen = 0

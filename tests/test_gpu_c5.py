@@ -7,9 +7,11 @@ src/compressor.cpp:192-248 per box, src/modes.cpp:100-103):
   * payload bytes equal the oracle's on 10 units (first, last, random ones);
   * the launch-order and the ticket form of the look-backs write identical
     bytes for ALL 512 units (zeroed payload buffers compared whole);
-  * wc_inverse of the whole batch reproduces the oracle's decompress()
-    (rle_decode + inverse_wavelet_decompose, src/decompressor.cpp:14-159) on 2
-    sampled units bit for bit.
+  * wc_inverse of the whole batch (the c5.inverse leg of bench.py) reproduces
+    the oracle's decompress() (rle_decode + inverse_wavelet_decompose,
+    src/decompressor.cpp:14-159) bit for bit on ALL 512 units, and so does
+    wc_inverse_rows with the row index wc_forward_rows wrote (the payloads of
+    which equal wc_forward's).
 """
 import numpy as np
 import pytest
@@ -116,16 +118,53 @@ def test_c5_paths_identical_all_units(c5_run, wc, ordered):
     torch.cuda.empty_cache()
 
 
-def test_c5_inverse_sampled_units_match_oracle(c5_run, oracle):
+def _threads():
+    import os
+    return max(1, min(16, os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+
+
+def test_c5_inverse_every_unit_matches_oracle(c5_run, oracle):
+    """wc_inverse of all 512 payloads, then wc_forward_rows + wc_inverse_rows:
+    every reconstruction equal to the oracle's decompress() of the unit's
+    payload (on a 16-thread pool), and the rows forward's payloads equal."""
     import torch
+    from concurrent.futures import ThreadPoolExecutor
     r = c5_run
+    n = r["n"]
     regen = torch.empty(r["extent"], dtype=torch.float32, device=r["dev"])
     torch.cuda.synchronize()
-    r["ctx"].inverse(r["payload"].data_ptr(), r["offsets_dev"].data_ptr(), r["tab"], r["n"], regen.data_ptr())
+    r["ctx"].inverse(r["payload"].data_ptr(), r["offsets_dev"].data_ptr(), r["tab"], n, regen.data_ptr())
     r["ctx"].synchronize()
-    for i in (1, r["n"] - 2):
-        want = oracle.decompress_payload(_payload(r, i)).ravel()
+    pay = r["payload"].cpu().numpy()
+    got = regen.cpu().numpy()
+
+    def unit_payload(i):
+        po = int(r["offsets"][i])
+        return pay[po:po + 20 + 8 * int(r["kept"][i])].tobytes()
+
+    def check(i):
+        want = oracle.decompress_payload(unit_payload(i)).ravel()
         o = r["offs"][i]
-        assert regen[o:o + 128 ** 3].cpu().numpy().tobytes() == want.tobytes(), i
-    del regen
+        return None if got[o:o + 128 ** 3].tobytes() == want.tobytes() else i
+
+    with ThreadPoolExecutor(_threads()) as ex:
+        bad = [i for i in ex.map(check, range(n)) if i is not None]
+    assert not bad, bad[:16]
+
+    # the round trip with the forward's row index: same payloads, same cells
+    from wavelet_compression_amd.capi import WC_F32, rowindex_bytes
+    rb = rowindex_bytes(r["tab"], n)
+    rows = torch.empty(rb // 8, dtype=torch.int64, device=r["dev"])
+    other = torch.zeros_like(r["payload"])
+    offs = torch.zeros_like(r["offsets_dev"])
+    kept = torch.zeros(n, dtype=torch.int32, device=r["dev"])
+    regen.fill_(float("nan"))
+    torch.cuda.synchronize()
+    r["ctx"].forward_rows(r["cells"].data_ptr(), WC_F32, r["tab"], n, KEEP, other.data_ptr(), r["cap"],
+                          offs.data_ptr(), kept.data_ptr(), rows.data_ptr(), rb)
+    r["ctx"].inverse_rows(other.data_ptr(), offs.data_ptr(), r["tab"], n, rows.data_ptr(), regen.data_ptr())
+    r["ctx"].synchronize()
+    assert torch.equal(other, r["payload"])
+    assert regen.cpu().numpy().tobytes() == got.tobytes()
+    del regen, rows, other
     torch.cuda.empty_cache()

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Builds libwavelet_amd.so variants (one -D each) under tools/variants/<name>/ for
+# Builds libwavelet_amd.so variants (one -D each, tuning macros only: no build
+# of the product sources writes invalid results) under tools/variants/<name>/ for
 # A/B runs of tools/bin/wc_bench with LD_LIBRARY_PATH (its RUNPATH yields to it).
 set -e
 CS=wavelet-compression_amd/csrc
@@ -10,7 +11,9 @@ for spec in "$@"; do
   for f in wc_transform wc_hist wc_compact wc_inverse wc_emit; do
     /opt/rocm/bin/hipcc $FLAGS $defs -c $CS/$f.hip -o $out/obj/$f.o &
   done
-  /opt/rocm/bin/hipcc $FLAGS $defs -c $CS/wc_capi.cpp -o $out/obj/wc_capi.o &
+  for f in wc_common wc_plan wc_capi wc_hostpipe; do
+    /opt/rocm/bin/hipcc $FLAGS $defs -c $CS/$f.cpp -o $out/obj/$f.o &
+  done
   g++ -O2 -std=c++17 -fPIC -c $CS/wc_hostmem.cpp -o $out/obj/wc_hostmem.o &
   wait
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $out/libwavelet_amd.so $out/obj/*.o -lpthread
