@@ -7,7 +7,10 @@ presets 0/1/6 across 4 encode and 3 decode threads), plotfile read/write and
 the reference fixtures, .raw side files, parameters, file selection, the
 CLI's argument errors, and the core library's host pool + destination
 prefault of the _host entry points (csrc/wc_hostmem.cpp, tests/cpp/
-test_hostmem.cpp).  Any sanitizer report fails the test (halt_on_error)."""
+test_hostmem.cpp), and the _host entry points' pipeline itself (csrc/
+wc_hostpipe.cpp + wc_common.cpp) over a CPU fake of the HIP runtime with
+injected failures (tests/cpp/test_hostpipe.cpp).  Any sanitizer report fails
+the test (halt_on_error)."""
 import lzma
 import os
 import subprocess
@@ -94,3 +97,17 @@ def test_host_pool_and_prefault_under_sanitizer(san_bins, san, tmp_path):
                        env=san_env(tmp_path))
     check_clean(r, f"{san} test_hostmem")
     assert r.returncode == 0 and "checks passed" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("san", SANS)
+def test_host_pipeline_under_sanitizer(san_bins, san, tmp_path):
+    """wc_forward_host / wc_inverse_host over the fake runtime (streams are
+    threads, events order them, pageable copies block): 1..16 unit runs, 0..8
+    host threads, pinned and pageable sources (bounce slots), the ticket-form
+    retry after a look-back timeout, and an injected failure of every runtime
+    call and device entry point the pipeline makes, each followed by a freed
+    caller buffer (no copy may outlive the call) and a clean call."""
+    r = subprocess.run([str(san_bins[san] / "test_hostpipe")], capture_output=True, text=True, timeout=600,
+                       env=san_env(tmp_path))
+    check_clean(r, f"{san} test_hostpipe")
+    assert r.returncode == 0 and " 0 failed" in r.stdout, r.stdout + r.stderr
