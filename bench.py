@@ -73,6 +73,11 @@ def parse(argv=None):
                     help="diagnostic: row-indexed inverse tiles in XCD-grouped order (WC_OPT_RIX_XCD 1)")
     ap.add_argument("--inv-groups", type=int, default=0,
                     help="diagnostic: WC_OPT_INV_GROUPS of the inverse legs (0: the library default)")
+    ap.add_argument("--dist-timeout", type=float, default=120.0,
+                    help="seconds a rank waits at process-group setup or in a collective before failing "
+                         "(a rank that died leaves the others failing fast instead of hanging)")
+    ap.add_argument("--fail-rank", type=int, default=-1,
+                    help="test hook (--plumbing only): this rank raises before its first collective")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU/gloo run of the launcher, sharding and reductions (no kernels, no numbers)")
     ap.add_argument("--rehearse", action="store_true",
@@ -127,7 +132,9 @@ def alg_bytes_inverse(cells, kept, nunits):
 class Dist:
     """The rank's view of the job: world, rank, device, barrier, reductions."""
 
-    def __init__(self, plumbing: bool, rehearse: bool = False):
+    def __init__(self, plumbing: bool, rehearse: bool = False, timeout_s: float = 120.0):
+        import datetime
+
         import torch
         import torch.distributed as dist
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -135,20 +142,24 @@ class Dist:
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.plumbing = plumbing
         self.coll_dev = None  # device of the reduction tensors (None: self.dev)
+        # bounded setup and collectives: a rank that died before a collective
+        # makes the others fail after this long (torch.distributed.run also
+        # stops the remaining ranks as soon as one exits non-zero)
+        tmo = datetime.timedelta(seconds=timeout_s)
         if plumbing:
             self.dev = torch.device("cpu")
             if self.world > 1:
-                dist.init_process_group("gloo")
+                dist.init_process_group("gloo", timeout=tmo)
         elif rehearse:
             if self.world > 1:
-                dist.init_process_group("gloo")
+                dist.init_process_group("gloo", timeout=tmo)
             torch.cuda.set_device(0)
             self.dev = torch.device("cuda", 0)
             self.local = 0
             self.coll_dev = torch.device("cpu")
         else:
             if self.world > 1:
-                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local), timeout=tmo)
             torch.cuda.set_device(self.local)
             self.dev = torch.device("cuda", self.local)
 
@@ -787,8 +798,10 @@ def main():
     args.legs_set = set() if args.legs in ("none", "") else set(args.legs.split(","))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
-    d = Dist(args.plumbing, args.rehearse)
+    d = Dist(args.plumbing, args.rehearse, args.dist_timeout)
     if args.plumbing:
+        if d.rank == args.fail_rank:
+            raise RuntimeError(f"rank {d.rank}: injected failure before the first collective (--fail-rank)")
         out = plumbing_run(args, d)
         if d.rank == 0:
             print(json.dumps(out), flush=True)

@@ -190,6 +190,38 @@ def test_bench_spawns_ranks_and_merges_one_line(tmp_path):
         assert sh["rank0_span"][0] == 0 and 0 < sh["rank0_span"][1] < sh["units_total"], name
 
 
+def test_bench_rank_failure_ends_the_job_fast(tmp_path):
+    """One rank of `bench.py --gpus 2` raises before the first collective: the
+    launcher exits non-zero well within the process-group timeout and leaves
+    no rank waiting (torch.distributed.run stops the other rank; its own
+    collectives are bounded by --dist-timeout besides)."""
+    import subprocess
+    import sys
+    import time
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["WCAMD_NO_TORCH"] = "1"
+    for fail in (1, 0):
+        t0 = time.monotonic()
+        p = subprocess.Popen([sys.executable, str(root / "bench.py"), "--gpus", "2", "--plumbing",
+                              "--fail-rank", str(fail), "--dist-timeout", "30"], env=env, cwd=tmp_path,
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+        try:
+            out, err = p.communicate(timeout=120)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, 9)
+            raise AssertionError(f"rank {fail} failing left the job hanging")
+        took = time.monotonic() - t0
+        assert p.returncode != 0, out
+        assert "injected failure" in err, err[-2000:]
+        assert not [ln for ln in out.splitlines() if ln.startswith("{")], out
+        assert took < 90, took
+        # no process of the job is left behind (its session is empty)
+        r = subprocess.run(["pgrep", "-s", str(p.pid)], capture_output=True, text=True)
+        assert r.stdout.strip() == "", r.stdout
+
+
 @pytest.mark.gpu
 def test_bench_two_ranks_on_one_gpu(tmp_path):
     """The driver's multi-GPU bench path on a one-GPU box: `bench.py --gpus 2
