@@ -186,6 +186,28 @@ int wc_forward_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* un
                     double keep, uint8_t* payload, uint64_t payload_capacity,
                     uint64_t* offsets, uint32_t* kept);
 
+/* wc_forward_host with unit u's W*H*D cells at its own host pointer cells[u]
+ * (units[u].cell_offset is ignored): the C++ mirror's compress() hands over
+ * the Box3D components it was given (src/compressor.h:9-15) without packing
+ * them into one buffer first.  Same payload, offsets and kept counts as
+ * wc_forward_host of the packed components. */
+int wc_forward_host_units(wc_ctx* ctx, const void* const* cells, int dtype, const wc_unit* units, int n,
+                          double keep, uint8_t* payload, uint64_t payload_capacity,
+                          uint64_t* offsets, uint32_t* kept);
+
+/* The reference's -estimate round trip on host buffers (src/modes.cpp:236-291:
+ * compress the boxes, decompress them again, calc_rmse_per_box against the
+ * originals, src/calc-loss.cpp:12-43): wc_forward_host's outputs (packed
+ * payloads, offsets, kept counts), plus rmse[u] = the RMSE of unit u's
+ * reconstruction against its cells.  The payloads are decoded again on the
+ * device with the forward's row index (wc_forward_rows / wc_inverse_rows) and
+ * compared there with the cells already uploaded for the forward: the cells
+ * cross PCIe once and the reconstruction never does.  RMSE identical to
+ * wc_rmse_host of the decoded reconstruction. */
+int wc_round_trip_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* units, int n, double keep,
+                       uint8_t* payload, uint64_t payload_capacity, uint64_t* offsets, uint32_t* kept,
+                       double* rmse);
+
 /* Opt-in global-threshold mode (NOT the reference's rule; BASELINE north_star's
  * "keep-percentile histogram + RCCL all-reduce").  The reference thresholds each
  * box at its own max * (1 - keep) (src/compressor.cpp:212-216); this mode picks

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -334,10 +335,11 @@ const char* hipGetErrorString(hipError_t e) {
 namespace fake {
 int timeout_calls = 0;  // the next k wc_forward calls raise a look-back timeout
 
-// unit u keeps its first kept_of(u) cells (a function of the unit alone, not of its run)
+// unit u keeps its first kept_of(u) cells (a function of its shape alone: not
+// of its run, nor of where its cells sit)
 uint32_t kept_of(const wc_unit& u) {
     const uint64_t cells = (uint64_t)u.nx * u.ny * u.nz;
-    return (uint32_t)((cells * ((u.cell_offset / 4 + (uint64_t)u.nx) % 5)) / 7);
+    return (uint32_t)((cells * ((uint64_t)(u.nx + 2 * u.ny + 3 * u.nz) % 5)) / 7);
 }
 
 std::vector<uint8_t> payload_of(const wc_unit& u, const void* cells, int dtype) {
@@ -456,15 +458,49 @@ int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, c
     return WC_OK;
 }
 
-// the transform-only / RMSE _host wrappers are not what this test covers
+// wc_round_trip_host's calls: the row index is the device's business (the
+// stand-in inverse decodes from the payloads), the RMSE is calc_rmse_per_box's
+int wc_forward_rows(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, int n, double keep,
+                    uint8_t* d_payload, uint64_t cap, uint64_t* d_offsets, uint32_t* d_kept, void* d_rowinfo,
+                    uint64_t rowinfo_capacity) {
+    if (!d_rowinfo || rowinfo_capacity < wc_rowindex_bytes(units, n)) return fail(c, WC_ERR_INVALID, "fake: rows");
+    return wc_forward(c, d_cells, dtype, units, n, keep, d_payload, cap, d_offsets, d_kept);
+}
+
+int wc_inverse_rows(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
+                    const void*, const void* d_orig, int, float* d_out, double*) {
+    if (d_orig) return fail(c, WC_ERR_INVALID, "fake: fused RMSE");
+    return wc_inverse(c, d_payload, d_offsets, units, n, d_out);
+}
+
+int wc_rmse(wc_ctx* c, const void* d_orig, int dtype, const float* d_regen, const wc_unit* units, int n,
+            double* d_rmse) {
+    int rc;
+    if ((rc = validate_units(c, units, n))) return rc;
+    if (injected("wc_rmse")) return fail(c, WC_ERR_HIP, "wc_rmse: injected launch failure (fake)");
+    std::vector<wc_unit> us(units, units + n);
+    enqueue(c->stream, [=] {
+        for (int i = 0; i < n; ++i) {
+            const uint64_t nc = (uint64_t)us[i].nx * us[i].ny * us[i].nz;
+            double s = 0.0;
+            for (uint64_t j = 0; j < nc; ++j) {
+                const uint64_t o = us[i].cell_offset + j;
+                const float a = dtype == WC_F64 ? (float)((const double*)d_orig)[o] : ((const float*)d_orig)[o];
+                const float d = a - d_regen[o];
+                s += (double)d * (double)d;
+            }
+            d_rmse[i] = nc ? std::sqrt(s / (double)nc) : 0.0;
+        }
+    }, false);
+    return WC_OK;
+}
+
+// the transform-only _host wrappers are not what this test covers
 int wc_decompose(wc_ctx* c, const void*, int, const wc_unit*, int, float*) {
     return fail(c, WC_ERR_INVALID, "fake: wc_decompose");
 }
 int wc_inverse_flat(wc_ctx* c, const float*, const wc_unit*, int, float*) {
     return fail(c, WC_ERR_INVALID, "fake: wc_inverse_flat");
-}
-int wc_rmse(wc_ctx* c, const void*, int, const float*, const wc_unit*, int, double*) {
-    return fail(c, WC_ERR_INVALID, "fake: wc_rmse");
 }
 
 }  // extern "C"

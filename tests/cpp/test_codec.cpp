@@ -19,6 +19,9 @@
 #include "wavelet_amd/codec_extras.h"
 #include "wavelet_amd/compressor.h"
 #include "wavelet_amd/decompressor.h"
+#include "wavelet_amd/xz_pool.h"
+#include <fstream>
+#include <iterator>
 
 static int g_checks = 0;
 #define REQUIRE(cond)                                                                   \
@@ -108,6 +111,15 @@ static void multi_component_and_quirks_case() {
             REQUIRE(odd.get(2, y, z) == 0.0f);
             REQUIRE(odd.get(0, y, z) == 7.0f && odd.get(1, y, z) == 7.0f);
         }
+    // the components' xz streams were encoded concurrently: each file is
+    // byte for byte the serial encoder's output of the component's payload
+    const int comps[3] = {6, 25, 3};
+    for (int c = 0; c < 3; ++c) {
+        const std::string ser = serialize_compressed_wavelet(cws[c]);
+        std::ifstream f(dir / ("compressed-wavelet-2-1-" + std::to_string(comps[c]) + "-7.xz"), std::ios::binary);
+        const std::string file((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        REQUIRE(file == wavelet_amd::xz_encode(reinterpret_cast<const uint8_t*>(ser.data()), ser.size()));
+    }
     std::vector<float> flat = rle_decode(cws[1].rle_encoded, cws[1].coeff_shape[0]);
     Box3D back = inverse_wavelet_decompose(flat, 4, 4, 4);
     REQUIRE(back.equals(mb[1], 0));

@@ -13,6 +13,7 @@
 // threads; an injected failure in any call returns its error code, leaves no
 // copy running into the caller's buffers (ASan: the test frees them at once)
 // and the next call on the same context succeeds.
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -48,7 +49,7 @@ static void destroy_ctx(wc_ctx* c) {
         if (s) (void)hipStreamSynchronize(s);
     c->plan.d_units.p = nullptr;  // the fake's own tables
     for (wc::DevBuf* b : {&c->errflag, &c->h_cells, &c->h_payload, &c->h_packed, &c->h_offsets, &c->h_poff, &c->h_kept,
-                          &c->h_out})
+                          &c->h_out, &c->h_rows, &c->h_rmse})
         if (b->p) (void)hipFree(b->p);
     for (hipEvent_t e : c->hev) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->bev) (void)hipEventDestroy(e);
@@ -130,6 +131,46 @@ static void round_trip(wc_ctx* c, const Batch& b, const double* cells, const cha
     for (int i = 0; i < n && same; ++i)
         same = std::memcmp(pay.data() + woff[i], want.data() + woff[i], 20 + 8ull * wkept[i]) == 0;
     CHECK(same, "%s: payload bytes", what);
+    {  // the same units, each from its own pointer (the drop-in compress()'s call)
+        std::vector<const void*> ptrs(n);
+        for (int i = 0; i < n; ++i) ptrs[i] = cells + b.units[i].cell_offset;
+        std::vector<uint8_t> pay2(cap, 0xDD);
+        std::vector<uint64_t> offs2(n + 1, 7);
+        std::vector<uint32_t> kept2(n, 7);
+        rc = wc_forward_host_units(c, ptrs.data(), WC_F64, b.units.data(), n, 0.999, pay2.data(), cap, offs2.data(),
+                                   kept2.data());
+        CHECK(rc == WC_OK, "%s: forward_host_units rc %d (%s)", what, rc, c->err.c_str());
+        bool same2 = rc == WC_OK && offs2 == woff && kept2 == wkept;
+        for (int i = 0; i < n && same2; ++i)
+            same2 = std::memcmp(pay2.data() + woff[i], want.data() + woff[i], 20 + 8ull * wkept[i]) == 0;
+        CHECK(same2, "%s: forward_host_units bytes", what);
+    }
+    {  // the -estimate round trip: the same payloads, and each unit's RMSE against its decoded boxes
+        std::vector<uint8_t> pay3(cap, 0xCC);
+        std::vector<uint64_t> offs3(n + 1, 7);
+        std::vector<uint32_t> kept3(n, 7);
+        std::vector<double> rmse(n, -1.0);
+        rc = wc_round_trip_host(c, cells, WC_F64, b.units.data(), n, 0.999, pay3.data(), cap, offs3.data(),
+                                kept3.data(), rmse.data());
+        CHECK(rc == WC_OK, "%s: round_trip_host rc %d (%s)", what, rc, c->err.c_str());
+        bool same3 = rc == WC_OK && offs3 == woff && kept3 == wkept;
+        for (int i = 0; i < n && same3; ++i)
+            same3 = std::memcmp(pay3.data() + woff[i], want.data() + woff[i], 20 + 8ull * wkept[i]) == 0;
+        CHECK(same3, "%s: round_trip_host bytes", what);
+        const std::vector<float> box = expected_boxes(b, 0.0f);
+        bool rm = rc == WC_OK;
+        for (int i = 0; i < n && rm; ++i) {
+            const wc_unit& u = b.units[i];
+            const uint64_t nc = (uint64_t)u.nx * u.ny * u.nz;
+            double s = 0.0;
+            for (uint64_t j = 0; j < nc; ++j) {
+                const float d = (float)b.cells[u.cell_offset + j] - box[u.cell_offset + j];
+                s += (double)d * (double)d;
+            }
+            rm = rmse[i] == (nc ? std::sqrt(s / (double)nc) : 0.0);
+        }
+        CHECK(rm, "%s: round_trip_host rmse", what);
+    }
     std::vector<float> out(b.extent, -3.0f);
     rc = wc_inverse_host(c, pay.data(), offs.data(), b.units.data(), n, out.data());
     CHECK(rc == WC_OK, "%s: inverse rc %d (%s)", what, rc, c->err.c_str());
@@ -188,7 +229,7 @@ static void test_failures() {
     const int n = (int)b.units.size();
     const char* apis[] = {"H2D",          "D2H",          "hipEventRecord", "hipStreamWaitEvent", "hipEventSynchronize",
                           "hipMalloc",    "launch_pack",  "wc_forward",     "wc_inverse",         "hipStreamSynchronize",
-                          "hipSetDevice", "hipEventCreateWithFlags"};
+                          "hipSetDevice", "hipEventCreateWithFlags", "wc_rmse"};
     for (const char* api : apis)
         for (int k : {1, 2, 5})
             for (int64_t chunk : {0, 1 << 12}) {
@@ -205,7 +246,11 @@ static void test_failures() {
                     fake::fail_nth(api, k);
                     const int rf = wc_forward_host(c, b.cells.data(), WC_F64, b.units.data(), n, 0.999, pay.data(), cap,
                                                    offs.data(), kept.data());
-                    const int ri = rf ? rf : wc_inverse_host(c, pay.data(), offs.data(), b.units.data(), n, out.data());
+                    int ri = rf ? rf : wc_inverse_host(c, pay.data(), offs.data(), b.units.data(), n, out.data());
+                    std::vector<double> rmse(n);
+                    if (!ri)
+                        ri = wc_round_trip_host(c, b.cells.data(), WC_F64, b.units.data(), n, 0.999, pay.data(), cap,
+                                                offs.data(), kept.data(), rmse.data());
                     fake::clear_failures();
                     CHECK(ri == WC_OK || ri == WC_ERR_HIP || ri == WC_ERR_NOMEM, "%s: rc %d", w.c_str(), ri);
                     CHECK(ri == WC_OK || !c->err.empty(), "%s: no message", w.c_str());

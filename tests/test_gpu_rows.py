@@ -256,3 +256,22 @@ def test_misaligned_device_buffers_rejected(wc, ctx):
                     offsets.data_ptr(), kept.data_ptr())
     with pytest.raises(WaveletError):
         ctx.inverse(payload.data_ptr(), offsets.data_ptr(), units, n, cells[2:].data_ptr())
+
+
+def test_forward_host_units_equals_forward_host(wc, ctx, oracle):
+    """wc_forward_host_units (each unit's cells at its own host pointer, the
+    drop-in compress()'s call) gives the bytes of wc_forward_host over the
+    packed units, and the oracle's."""
+    boxes = [oracle.narrow(b) for b in synth(oracle, DIMS + [(64, 64, 64)] * 3, seed0=16)]
+    keep = KEEPS[1]
+    dims = [(b.shape[2], b.shape[1], b.shape[0]) for b in boxes]
+    units, n, extent = wc.capi.make_units(dims)
+    cells = np.zeros(max(extent, 1), np.float32)
+    for i, b in enumerate(boxes):
+        cells[units[i].cell_offset:units[i].cell_offset + b.size] = b.ravel()
+    pa, oa, ka = ctx.forward_host(cells, units, n, keep)
+    pb, ob, kb = ctx.forward_host_units(boxes, units, n, keep)
+    assert np.array_equal(oa, ob) and np.array_equal(ka, kb)
+    assert np.array_equal(pa[:int(oa[n])], pb[:int(ob[n])])
+    for i, b in enumerate(boxes):
+        assert wc.capi.unit_payload(pb, ob, kb, i) == oracle.compress_payload(b, keep)[0], i

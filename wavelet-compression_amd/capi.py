@@ -29,7 +29,7 @@ EXPORTED = (
     "wc_profile_enable", "wc_profile_read", "wc_set_option", "wc_inverse_flat_host", "wc_rmse_host",
     "wc_decompose_host", "wc_device_count", "wc_forward_stage", "wc_hist_threshold",
     "wc_forward_emit", "wc_inverse_rmse", "wc_get_option", "wc_rowindex_bytes", "wc_forward_rows",
-    "wc_inverse_rows",
+    "wc_inverse_rows", "wc_forward_host_units", "wc_round_trip_host",
 )
 WC_OPT_SPARSE = 12   # sparse coefficient staging in the forward (default 1)
 WC_OPT_ORDERED = 13  # look-back tile index from the launch order (1, default) or per-unit tickets (0)
@@ -110,6 +110,8 @@ def load_library() -> ctypes.CDLL:
         "wc_rowindex_bytes": (u64, [up, i32]),
         "wc_forward_rows": (i32, [vp, vp, i32, up, i32, ctypes.c_double, vp, u64, vp, vp, vp, u64]),
         "wc_inverse_rows": (i32, [vp, vp, vp, up, i32, vp, vp, i32, vp, vp]),
+        "wc_forward_host_units": (i32, [vp, ctypes.POINTER(vp), i32, up, i32, ctypes.c_double, vp, u64, vp, vp]),
+        "wc_round_trip_host": (i32, [vp, vp, i32, up, i32, ctypes.c_double, vp, u64, vp, vp, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -308,6 +310,40 @@ class Context:
         self._check(self._L.wc_forward_host(self._h, c.ctypes.data, dtype, units, n, float(keep),
                                             payload.ctypes.data, cap, offsets.ctypes.data,
                                             kept.ctypes.data))
+        return payload, offsets, kept[:n]
+
+    def round_trip_host(self, cells: np.ndarray, units, n: int, keep: float):
+        """wc_round_trip_host: forward_host's (payload, offsets, kept) and the
+        per-unit RMSE of the reconstruction (computed on the device)."""
+        c = np.ascontiguousarray(cells)
+        if c.dtype not in (np.float32, np.float64):
+            raise TypeError("cells must be float32 or float64")
+        dtype = WC_F64 if c.dtype == np.float64 else WC_F32
+        cap = payload_bound(units, n)
+        payload = np.empty(cap, np.uint8)
+        offsets = np.zeros(n + 1, np.uint64)
+        kept = np.zeros(max(n, 1), np.uint32)
+        rmse = np.zeros(max(n, 1), np.float64)
+        self._check(self._L.wc_round_trip_host(self._h, c.ctypes.data, dtype, units, n, float(keep),
+                                               payload.ctypes.data, cap, offsets.ctypes.data, kept.ctypes.data,
+                                               rmse.ctypes.data))
+        return payload, offsets, kept[:n], rmse[:n]
+
+    def forward_host_units(self, boxes, units, n: int, keep: float):
+        """wc_forward_host_units: unit u's cells from boxes[u] (its own host
+        array, all float32 or all float64) -> (payload, offsets, kept)."""
+        arrs = [np.ascontiguousarray(b) for b in boxes]
+        dt = {a.dtype for a in arrs if a.size}
+        if not dt <= {np.dtype(np.float32)} and not dt <= {np.dtype(np.float64)}:
+            raise TypeError("boxes must be all float32 or all float64")
+        dtype = WC_F64 if dt == {np.dtype(np.float64)} else WC_F32
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+        cap = payload_bound(units, n)
+        payload = np.empty(cap, np.uint8)
+        offsets = np.zeros(n + 1, np.uint64)
+        kept = np.zeros(max(n, 1), np.uint32)
+        self._check(self._L.wc_forward_host_units(self._h, ptrs, dtype, units, n, float(keep), payload.ctypes.data,
+                                                  cap, offsets.ctypes.data, kept.ctypes.data))
         return payload, offsets, kept[:n]
 
     def decompose_host(self, cells: np.ndarray, units, n: int, extent: int) -> np.ndarray:

@@ -1,9 +1,10 @@
 // compressor.cpp — C++ mirror of the reference's compress() (src/compressor.cpp:192-297).
 //
-// All components of the box go to the GPU in ONE wc_forward_host call (the
-// reference loops per component, :203); the serialized payloads come back
-// byte-identical to serialize_compressed_wavelet, and the host only does the
-// xz stage and the file write.
+// All components of the box go to the GPU in ONE wc_forward_host_units call,
+// each straight from its Box3D (the reference loops per component, :203); the
+// serialized payloads come back byte-identical to serialize_compressed_wavelet,
+// and the host only does the xz stage and the file write, the components'
+// independent xz streams on a pool of host threads (same bytes as one by one).
 #include <lzma.h>
 
 #include <cmath>
@@ -11,6 +12,7 @@
 #include <cstring>
 #include <filesystem>
 #include <fstream>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -18,6 +20,7 @@
 #include "wavelet_amd/codec_extras.h"
 #include "wavelet_amd/compressor.h"
 #include "wavelet_amd/decompressor.h"
+#include "wavelet_amd/xz_pool.h"
 
 namespace wavelet_amd {
 
@@ -87,28 +90,36 @@ std::vector<CompressedWavelet> compress(multiBox3D& box, std::vector<int> compon
     const int n = static_cast<int>(components.size());
     std::vector<CompressedWavelet> out;
     if (n == 0) return out;
-    // Pack box[0..n) (positional, src/compressor.cpp:203-206) into one buffer.
+    // box[0..n) (positional, src/compressor.cpp:203-206), each component from
+    // its own Box3D storage: no packing copy on the host
     std::vector<wc_unit> units(n);
-    uint64_t cursor = 0;
+    std::vector<const void*> cells(n);
     for (int c = 0; c < n; ++c) {
         const Box3D& b = box.at(c);
-        cursor = (cursor + 3) & ~uint64_t(3);
-        units[c] = wc_unit{cursor, (int32_t)b.width(), (int32_t)b.height(), (int32_t)b.depth(), 0};
-        cursor += b.data_size();
+        units[c] = wc_unit{0, (int32_t)b.width(), (int32_t)b.height(), (int32_t)b.depth(), 0};
+        cells[c] = b.data();
     }
-    std::vector<float> cells(cursor ? cursor : 1);
-    for (int c = 0; c < n; ++c)
-        if (box[c].data_size()) std::memcpy(cells.data() + units[c].cell_offset, box[c].data(), 4 * box[c].data_size());
+    // the payload buffer of this thread, reused across calls (grow-only, never
+    // zero-filled: the library writes every byte it reports)
     const uint64_t cap = wc_payload_bound(units.data(), n);
-    std::vector<uint8_t> payload(cap);
+    thread_local std::unique_ptr<uint8_t[]> t_payload;
+    thread_local uint64_t t_cap = 0;
+    if (t_cap < cap) {
+        t_payload.reset(new uint8_t[cap]);
+        t_cap = cap;
+    }
     std::vector<uint64_t> offsets(n + 1);
     std::vector<uint32_t> kept(n);
     wc_ctx* ctx = thread_ctx();
-    check(ctx, wc_forward_host(ctx, cells.data(), WC_F32, units.data(), n, keep, payload.data(), cap, offsets.data(),
-                               kept.data()),
+    check(ctx, wc_forward_host_units(ctx, cells.data(), WC_F32, units.data(), n, keep, t_payload.get(), cap,
+                                     offsets.data(), kept.data()),
           "GPU forward");
-    for (int c = 0; c < n; ++c) {
-        const std::string serialized(reinterpret_cast<const char*>(payload.data() + offsets[c]), 20 + 8ull * kept[c]);
+    // per component: the struct, and the .xz file (src/compressor.cpp:250-291);
+    // the components' xz streams are independent: encoded concurrently
+    out.resize(n);
+    const uint8_t* payload = t_payload.get();
+    parallel_for((size_t)n, std::min(n, host_threads()), [&](size_t c) {
+        const std::string serialized(reinterpret_cast<const char*>(payload + offsets[c]), 20 + 8ull * kept[c]);
         CompressedWavelet cw = deserialize_compressed_wavelet(serialized);
         for (const auto& pr : cw.rle_encoded)
             if (std::fabs((double)pr.second) > INT16_MAX) cw.need32 = true;  // src/compressor.cpp:229
@@ -121,7 +132,7 @@ std::vector<CompressedWavelet> compress(multiBox3D& box, std::vector<int> compon
             const std::string xz = xz_compress(serialized);
             file.write(xz.data(), (std::streamsize)xz.size());
         }
-        out.push_back(std::move(cw));
-    }
+        out[c] = std::move(cw);
+    });
     return out;
 }

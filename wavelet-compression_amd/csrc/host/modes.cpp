@@ -204,9 +204,13 @@ struct Packed {
     std::unique_ptr<uint8_t[]> payload;
     std::vector<uint64_t> offsets;
     std::vector<uint32_t> kept;
+    std::vector<double> rmse;  // round trip (estimate): calc_rmse_per_box of every unit
 };
 
-Packed forward_chunk(const Chunk& c, double keep) {
+// The chunk's forward; round_trip: also decode the payloads again and take
+// each unit's RMSE against its cells, on the device (wc_round_trip_host: the
+// reconstruction never comes back to the host).
+Packed forward_chunk(const Chunk& c, double keep, bool round_trip) {
     Packed p;
     const int n = (int)c.units.size();
     const uint64_t cap = wc_payload_bound(c.units.data(), n);
@@ -214,9 +218,16 @@ Packed forward_chunk(const Chunk& c, double keep) {
     p.offsets.resize(n + 1);
     p.kept.resize(n);
     wc_ctx* ctx = thread_ctx();
-    check(ctx, wc_forward_host(ctx, c.cells.data(), WC_F64, c.units.data(), n, keep, p.payload.get(), cap,
-                               p.offsets.data(), p.kept.data()),
-          "GPU forward");
+    if (round_trip) {
+        p.rmse.resize(n);
+        check(ctx, wc_round_trip_host(ctx, c.cells.data(), WC_F64, c.units.data(), n, keep, p.payload.get(), cap,
+                                      p.offsets.data(), p.kept.data(), p.rmse.data()),
+              "GPU round trip");
+    } else {
+        check(ctx, wc_forward_host(ctx, c.cells.data(), WC_F64, c.units.data(), n, keep, p.payload.get(), cap,
+                                   p.offsets.data(), p.kept.data()),
+              "GPU forward");
+    }
     return p;
 }
 
@@ -247,11 +258,11 @@ void inverse_batch(const std::vector<std::string>& payloads, const std::vector<w
 }
 
 // Compress every unit of `r` into `dir` (file names joined as std::filesystem
-// paths, src/compressor.cpp:250-254).  `on_chunk` sees each chunk after its
-// forward pass (estimate mode keeps the cells for the RMSE).
+// paths, src/compressor.cpp:250-254).  `on_chunk` sees each chunk and its
+// payloads after its forward pass (round_trip: with every unit's RMSE).
 template <class OnChunk>
 void compress_run(const RunIndex& r, double keep, const std::filesystem::path& dir, OnChunk on_chunk,
-                  const std::vector<int>& devs) {
+                  const std::vector<int>& devs, bool round_trip = false) {
     const size_t nc = r.comp_idxs.size();
     std::vector<Chunk> chunks = plan_chunks(r, nc, chunk_cells());
     auto jobs_of = [&](const Chunk& c, const Packed& p) {
@@ -273,14 +284,14 @@ void compress_run(const RunIndex& r, double keep, const std::filesystem::path& d
         for (size_t i = next.fetch_add(1); i < chunks.size(); i = next.fetch_add(1)) {
             Chunk& c = chunks[i];
             load_chunk(r, c, threads);
-            auto p = std::make_shared<Packed>(forward_chunk(c, keep));
+            auto p = std::make_shared<Packed>(forward_chunk(c, keep, round_trip));
             std::vector<XzJob> jobs = jobs_of(c, *p);
             if (xz_done.valid()) xz_done.get();
             xz_done = std::async(std::launch::async,
                                  [jobs = std::move(jobs), p, threads]() { xz_write_files(jobs, threads); });
             {
                 std::lock_guard<std::mutex> g(cb);
-                on_chunk(c);
+                on_chunk(c, *p);
             }
             c.cells.clear();
             c.cells.shrink_to_fit();
@@ -317,7 +328,8 @@ int compress(const Config& cfg) {
     write_amrexinfo(r.amrexinfo, cfg.compressed_dir, "amrexinfo.raw");
     log_info("Successfully processed data in " + fmt_double(since(t0)) + " seconds. Beginning compression...");
     const auto t1 = Clock::now();
-    compress_run(r, (double)cfg.keep, std::filesystem::path(cfg.compressed_dir), [](const Chunk&) {}, run_devices());
+    compress_run(r, (double)cfg.keep, std::filesystem::path(cfg.compressed_dir), [](const Chunk&, const Packed&) {},
+                 run_devices());
     log_info("Compression completed in " + fmt_double(since(t1)) + " seconds.");
     return 0;
 }
@@ -399,11 +411,16 @@ int estimate(Config& cfg) {
     RunIndex r = index_run(files, cfg.components, levels);
     if (!r.ok || files.empty()) return 1;
     const size_t nc = r.comp_idxs.size();
-    // Keep each chunk's cells for the RMSE; min/max over the narrowed values.
-    std::vector<Chunk> kept_chunks;
+    // The reference compresses the boxes, reads the files back, decompresses
+    // them and takes calc_rmse_per_box (src/modes.cpp:236-291).  Here each
+    // chunk's round trip runs on the device right after its forward
+    // (wc_round_trip_host): the files are still written (their sizes are the
+    // estimate), the RMSE comes from the same payload bytes they hold.
+    // min/max over the narrowed values.
+    std::vector<std::vector<double>> all_rmses(nc);
     std::vector<float> minv(nc, FLT_MAX), maxv(nc, FLT_MIN);  // src/preprocess.cpp:30-31 quirk
     const std::vector<int> one_device = {run_devices()[0]};
-    compress_run(r, (double)cfg.keep, scratch.path(), [&](Chunk& c) {
+    compress_run(r, (double)cfg.keep, scratch.path(), [&](Chunk& c, const Packed& p) {
         for (size_t u = 0; u < c.units.size(); ++u) {
             const size_t k = u % nc;
             const uint64_t n = (uint64_t)c.units[u].nx * c.units[u].ny * c.units[u].nz;
@@ -413,32 +430,10 @@ int estimate(Config& cfg) {
                 if (v < minv[k]) minv[k] = v;
                 if (v > maxv[k]) maxv[k] = v;
             }
+            all_rmses[k].push_back(p.rmse[u]);
         }
-        Chunk keep;
-        keep.boxes = c.boxes;
-        keep.units = c.units;
-        keep.ncells = c.ncells;
-        keep.cells.swap(c.cells);
-        kept_chunks.push_back(std::move(keep));
-    }, one_device);
+    }, one_device, /*round_trip=*/true);
     log_info("Compression complete.");
-    // Decompress from the written files, then per-box RMSE on the GPU.
-    std::vector<std::vector<double>> all_rmses(nc);
-    const int threads = host_threads();
-    if (one_device[0] >= 0) set_thread_device(one_device[0]);
-    for (Chunk& c : kept_chunks) {
-        std::vector<std::string> paths;
-        for (const BoxRef& b : c.boxes)
-            for (size_t k = 0; k < nc; ++k) paths.push_back((scratch.path() / unit_name(b.t, b.lev, r.comp_idxs[k], b.box)).string());
-        std::vector<std::string> payloads = xz_read_files(paths, threads);
-        std::vector<float> regen(std::max<uint64_t>(c.ncells, 1));
-        inverse_batch(payloads, c.units, regen.data());
-        std::vector<double> rmse(c.units.size());
-        wc_ctx* ctx = thread_ctx();
-        check(ctx, wc_rmse_host(ctx, c.cells.data(), WC_F64, regen.data(), c.units.data(), (int)c.units.size(), rmse.data()),
-              "GPU RMSE");
-        for (size_t u = 0; u < rmse.size(); ++u) all_rmses[u % nc].push_back(rmse[u]);
-    }
     log_info("Decompression complete.");
     for (int c = 0; c < num_components && c < (int)nc; ++c) {
         const double mean = std::accumulate(all_rmses[c].begin(), all_rmses[c].end(), 0.0) / all_rmses[c].size();

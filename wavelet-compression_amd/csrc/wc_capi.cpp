@@ -142,6 +142,7 @@ void wc_ctx_destroy(wc_ctx* c) {
     DevBuf* bufs[] = {&c->coef,          &c->part,           &c->errflag,        &c->state,
                       &c->flags,         &c->h_cells,        &c->h_payload,      &c->h_packed,
                       &c->h_offsets,     &c->h_poff,         &c->h_kept,         &c->h_out,
+                      &c->h_rows,        &c->h_rmse,
                       &c->plan.d_units,  &c->plan.d_xtiles,  &c->plan.d_ftiles,  &c->plan.d_dtiles,
                       &c->plan.d_edesc, &c->plan.d_ixtiles, &c->plan.d_rtiles,
                       &c->plan.d_rdtiles, &c->rowinfo,    &c->istate,        &c->npairs};

@@ -147,6 +147,7 @@ struct wc_ctx {
     uint32_t epoch = 0;
     // host-path staging
     wc::DevBuf h_cells, h_payload, h_packed, h_offsets, h_poff, h_kept, h_out;
+    wc::DevBuf h_rows, h_rmse;  // wc_round_trip_host: a run's row index, the per-unit RMSE
     // wc_forward_host pipeline: copy streams, per-run events, pinned metadata
     int64_t opt_host_chunk = int64_t(1) << 25;  // WC_OPT_HOST_CHUNK
     hipStream_t up = nullptr, down = nullptr;

@@ -235,13 +235,29 @@ static int host_streams(wc_ctx* c, int nr) {
     return WC_OK;
 }
 
-static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_unit* units, int n, double keep,
-                             uint8_t* payload, uint64_t cap, uint64_t* offsets, uint32_t* kept) {
+// Where a _host forward's cells come from: one host buffer at the units' cell
+// offsets (wc_forward_host), or one host pointer per unit (wc_forward_host_units:
+// the units' cell offsets are then the packed device layout).
+struct CellSource {
+    const uint8_t* base = nullptr;
+    const void* const* per_unit = nullptr;
+};
+
+// rmse != null (wc_round_trip_host): each run's forward also writes its row
+// index, and the run's payloads are decoded again on the device with it
+// (wc_inverse_rows) and compared with the run's cells there (wc_rmse): the
+// reconstruction never leaves the device, the cells cross PCIe once.
+static int forward_host_once(wc_ctx* c, CellSource src, int dtype, const wc_unit* units, int n, double keep,
+                             uint8_t* payload, uint64_t cap, uint64_t* offsets, uint32_t* kept, double* rmse) {
     int rc;
     if ((rc = validate_units(c, units, n))) return rc;
     if (dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
     if (n == 0) return WC_OK;
-    if (!cells || !payload || !offsets || !kept) return fail(c, WC_ERR_INVALID, "null buffer");
+    if ((!src.base && !src.per_unit) || !payload || !offsets || !kept) return fail(c, WC_ERR_INVALID, "null buffer");
+    if (src.per_unit)
+        for (int i = 0; i < n; ++i)
+            if (!src.per_unit[i] && (uint64_t)units[i].nx * units[i].ny * units[i].nz)
+                return fail(c, WC_ERR_INVALID, "null buffer (unit " + std::to_string(i) + ")");
     const uint64_t bound = wc_payload_bound(units, n);
     if (cap < bound) return fail(c, WC_ERR_INVALID, "payload_capacity < wc_payload_bound");
     if ((rc = set_device(c))) return rc;
@@ -258,8 +274,17 @@ static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_u
     const int nr = (int)rb.size() - 1;
     // per run: payload slot base (device), metadata base (pinned): poff[n_r + 1] | kept[n_r]
     std::vector<uint64_t> pbase(nr + 1, 0);
-    for (int r = 0; r < nr; ++r) pbase[r + 1] = pbase[r] + wc_payload_bound(units + rb[r], rb[r + 1] - rb[r]);
+    // (16-B aligned: each run's slots start like a device buffer's, pairs 8-B aligned)
+    for (int r = 0; r < nr; ++r)
+        pbase[r + 1] = round_up(pbase[r] + wc_payload_bound(units + rb[r], rb[r + 1] - rb[r]), 16);
     const size_t meta_bytes = sizeof(uint64_t) * (size_t)(n + nr) + 4ull * n;
+    uint64_t rows_cap = 0;  // the largest run's row index (wc_round_trip_host)
+    if (rmse) {
+        for (int r = 0; r < nr; ++r) rows_cap = std::max(rows_cap, wc_rowindex_bytes(units + rb[r], rb[r + 1] - rb[r]));
+        if ((rc = ensure(c, c->h_rows, rows_cap)) || (rc = ensure(c, c->h_out, sizeof(float) * ext)) ||
+            (rc = ensure(c, c->h_rmse, sizeof(double) * n)))
+            return rc;
+    }
     if ((rc = ensure(c, c->h_cells, esz * ext)) || (rc = ensure(c, c->h_payload, pbase[nr])) ||
         (rc = ensure(c, c->h_packed, pbase[nr])) || (rc = ensure(c, c->h_offsets, sizeof(uint64_t) * (n + nr))) ||
         (rc = ensure(c, c->h_poff, sizeof(uint64_t) * (n + nr))) || (rc = ensure(c, c->h_kept, 4 * n)))
@@ -294,10 +319,18 @@ static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_u
             }
             hipStream_t cs = nr > 1 ? c->up : c->stream;
             hipError_t e;
-            if (hi > lo &&
-                (e = host_upload(c, d_cells + esz * lo, (const uint8_t*)cells + esz * lo, esz * (hi - lo), cs)) !=
-                    hipSuccess)
-                return hip_fail(c, e, "cells upload");
+            if (src.base) {  // one span of the caller's buffer
+                if (hi > lo &&
+                    (e = host_upload(c, d_cells + esz * lo, src.base + esz * lo, esz * (hi - lo), cs)) != hipSuccess)
+                    return hip_fail(c, e, "cells upload");
+            } else {  // unit by unit, each from its own pointer
+                for (int i = a; i < a + m; ++i) {
+                    const uint64_t cnt = (uint64_t)units[i].nx * units[i].ny * units[i].nz;
+                    if (cnt && (e = host_upload(c, d_cells + esz * units[i].cell_offset, src.per_unit[i], esz * cnt,
+                                                cs)) != hipSuccess)
+                        return hip_fail(c, e, "cells upload");
+                }
+            }
             if (nr > 1 && ((e = hipEventRecord(c->hev[2 * r], c->up)) != hipSuccess ||
                            (e = hipStreamWaitEvent(c->stream, c->hev[2 * r], 0)) != hipSuccess))
                 return hip_fail(c, e, "upload event");
@@ -307,8 +340,10 @@ static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_u
             uint64_t* dpoff = (uint64_t*)c->h_poff.p + (a + r);
             uint32_t* dkept = (uint32_t*)c->h_kept.p + a;
             int rc2;
-            if ((rc2 = wc_forward(c, c->h_cells.p, dtype, units + a, m, keep, pay, pbase[r + 1] - pbase[r], doff,
-                                  dkept)))
+            if ((rc2 = rmse ? wc_forward_rows(c, c->h_cells.p, dtype, units + a, m, keep, pay, pbase[r + 1] - pbase[r],
+                                              doff, dkept, c->h_rows.p, rows_cap)
+                            : wc_forward(c, c->h_cells.p, dtype, units + a, m, keep, pay, pbase[r + 1] - pbase[r], doff,
+                                         dkept)))
                 return rc2;
             // Pack the slots densely (offsets stay == 4 mod 8), sizes to pinned memory.
             e = launch_pack(c->stream, (const UnitDev*)c->plan.d_units.p, m, dkept, pay, dpoff, packed);
@@ -319,6 +354,13 @@ static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_u
                 (e = hipEventRecord(c->hev[2 * r + 1], c->stream)) != hipSuccess)
                 return hip_fail(c, e, "sizes readback");
             gate.publish(r + 1);
+            // the round trip: this run's payloads back to cells with the row
+            // index just written, and calc_rmse_per_box against its cells
+            if (rmse && ((rc2 = wc_inverse_rows(c, pay, doff, units + a, m, c->h_rows.p, nullptr, WC_F32,
+                                                (float*)c->h_out.p, nullptr)) ||
+                         (rc2 = wc_rmse(c, c->h_cells.p, dtype, (const float*)c->h_out.p, units + a, m,
+                                        (double*)c->h_rmse.p + a))))
+                return rc2;
         }
         mark("enqueued", nr);
         return WC_OK;
@@ -355,6 +397,9 @@ static int forward_host_once(wc_ctx* c, const void* cells, int dtype, const wc_u
     if ((rc = with_helper(c, nr, gate, hs, enqueue, download))) return rc;
     offsets[n] = R - 4;
     hipError_t e2;
+    if (rmse && (e2 = hipMemcpyAsync(rmse, c->h_rmse.p, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream)) !=
+                    hipSuccess)
+        return hip_fail(c, e2, "rmse readback");
     if ((e2 = hipStreamSynchronize(c->stream)) != hipSuccess) return hip_fail(c, e2, "sync");
     mark("done");
     return check_kernel_errors(c);
@@ -514,7 +559,36 @@ int wc_forward_host(wc_ctx* c, const void* cells, int dtype, const wc_unit* unit
                     uint8_t* payload, uint64_t cap, uint64_t* offsets, uint32_t* kept) {
     if (!c) return WC_ERR_INVALID;
     return with_ticket_retry(
-        c, [&] { return forward_host_once(c, cells, dtype, units, n, keep, payload, cap, offsets, kept); });
+        c, [&] { return forward_host_once(c, CellSource{(const uint8_t*)cells, nullptr}, dtype, units, n, keep, payload,
+                                          cap, offsets, kept, nullptr); });
+}
+
+int wc_round_trip_host(wc_ctx* c, const void* cells, int dtype, const wc_unit* units, int n, double keep,
+                       uint8_t* payload, uint64_t cap, uint64_t* offsets, uint32_t* kept, double* rmse) {
+    if (!c) return WC_ERR_INVALID;
+    if (n > 0 && !rmse) return fail(c, WC_ERR_INVALID, "null buffer");
+    return with_ticket_retry(c, [&] {
+        return forward_host_once(c, CellSource{(const uint8_t*)cells, nullptr}, dtype, units, n, keep, payload, cap,
+                                 offsets, kept, rmse);
+    });
+}
+
+int wc_forward_host_units(wc_ctx* c, const void* const* cells, int dtype, const wc_unit* units, int n, double keep,
+                          uint8_t* payload, uint64_t cap, uint64_t* offsets, uint32_t* kept) {
+    if (!c) return WC_ERR_INVALID;
+    if (n < 0 || (n > 0 && (!units || !cells))) return fail(c, WC_ERR_INVALID, "null buffer");
+    // the device layout: the units back to back, 4-element aligned (16-B loads)
+    std::vector<wc_unit> packed(units, units + n);
+    uint64_t cursor = 0;
+    for (wc_unit& u : packed) {
+        cursor = (cursor + 3) & ~uint64_t(3);
+        u.cell_offset = cursor;
+        if (u.nx > 0 && u.ny > 0 && u.nz > 0) cursor += (uint64_t)u.nx * u.ny * u.nz;
+    }
+    return with_ticket_retry(c, [&] {
+        return forward_host_once(c, CellSource{nullptr, cells}, dtype, packed.data(), n, keep, payload, cap, offsets,
+                                 kept, nullptr);
+    });
 }
 
 int wc_inverse_host(wc_ctx* c, const uint8_t* payload, const uint64_t* offsets, const wc_unit* units, int n,
