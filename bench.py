@@ -48,6 +48,7 @@ sys.path.insert(0, str(ROOT))
 
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 ALL_LEGS = ("inverse", "host", "f32_64", "c3", "c5", "c4")
+OPT_LEGS = ("cli", "dropin")  # opt-in (--legs ...): subprocess runs of the CLI and of the drop-in driver
 
 
 def parse(argv=None):
@@ -58,7 +59,7 @@ def parse(argv=None):
     ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5", "f32_64"), default="c2",
                     help="headline workload (default: BASELINE configs[1], C2)")
     ap.add_argument("--legs", default=",".join(ALL_LEGS),
-                    help="comma list of extra legs (inverse,host,f32_64,c3,c5,c4) or 'none'")
+                    help="comma list of extra legs (inverse,host,f32_64,c3,c5,c4; opt-in: cli,dropin) or 'none'")
     ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of each extra leg")
     ap.add_argument("--hist-quantile", type=float, default=0.7,
                     help="c4 leg: quantile of the opt-in global-threshold mode (NOT the reference rule)")
@@ -775,6 +776,62 @@ def cpu_baseline(args, b: Batch, rmse_dev):
 
 
 # ---------------------------------------------------------------------------
+# opt-in legs: the command line and the literal drop-in path, in their own processes
+
+def _cpu_compress_rate(cpu):
+    """The reference's compress() work (transform ... serialize + xz preset 6)
+    per host thread, from cpu_baseline.with_xz (xz is per unit, so the pool's
+    rate / its threads is the single-thread rate)."""
+    try:
+        wx = cpu["with_xz"]
+        return wx["value"] / max(1, wx["cores"])
+    except (TypeError, KeyError):
+        return None
+
+
+def _last_json(text):
+    for ln in reversed(text.splitlines()):
+        if ln.startswith("{"):
+            return json.loads(ln)
+    raise RuntimeError("no JSON line in:\n" + text[-2000:])
+
+
+def cli_leg(args, cpu):
+    """End-to-end -c / -d / -estimate of the CLI on a C3-like plotfile (tools/bench_cli.py)."""
+    out = ROOT / "gpurun_out" / "cli_e2e.json"
+    cmd = [sys.executable, str(ROOT / "tools" / "bench_cli.py"), "--scale", "1.0", "--ncomp", "4", "--out", str(out)]
+    rate = _cpu_compress_rate(cpu)
+    if rate:
+        cmd += ["--cpu-cells-per-s", str(rate)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=1500)
+    if r.returncode:
+        return {"error": r.stderr[-2000:]}
+    res = _last_json(r.stdout)
+    res.pop("cli_logs", None)
+    return res
+
+
+def dropin_leg(args, cpu):
+    """INTEGRATION.md Option A: the reference's per-box loops over the C++ mirror
+    (compress() per box, decompress() per file) on the C3 layout, 4 fp32
+    components per box (tools/dropin_bench.cpp), beside the CPU rate of the
+    reference's compress() work per box (single thread, xz preset 6)."""
+    import tempfile
+    exe = ROOT / "tools" / "bin" / "dropin_bench"
+    with tempfile.TemporaryDirectory(prefix="wcamd_dropin_") as d:
+        r = subprocess.run([str(exe), d + "/files", "4", "0.999"], capture_output=True, text=True, timeout=1500)
+    if r.returncode:
+        return {"error": r.stderr[-2000:]}
+    res = _last_json(r.stdout)
+    rate = _cpu_compress_rate(cpu)
+    if rate:
+        res["cpu_compress_single_thread"] = {
+            "cells_per_s": rate, "ms_per_box": res["cells"] / res["boxes"] / rate * 1e3,
+            "note": "the reference's compress() work per host thread (cpu_baseline.with_xz / its threads: oracle "
+                    "transform+threshold+RLE+serialize + xz preset 6), per box of this layout's mean size"}
+        res["speedup_vs_cpu_single_thread"] = res["compress_cells_per_s"] / rate
+    return res
+
 
 def plumbing_run(args, d: Dist):
     """CPU check of the launcher: ranks, shard plans and the metric reduction."""
@@ -829,6 +886,10 @@ def main():
         out["c5"] = sharded_forward_leg(args, d, "c5", inverse=True)
     if "c4" in args.legs_set:
         out["c4"] = sharded_forward_leg(args, d, "c4", hist=True)
+    if d.world == 1 and "cli" in args.legs_set:
+        out["cli"] = cli_leg(args, out.get("cpu_baseline"))
+    if d.world == 1 and "dropin" in args.legs_set:
+        out["dropin"] = dropin_leg(args, out.get("cpu_baseline"))
     if d.rank == 0:
         print(json.dumps(out), flush=True)
     d.close()

@@ -1,12 +1,12 @@
 """End-to-end timing of the wavelet-compression command line (-c, -d, -estimate)
-on a synthetic AMR run, with the reference-faithful CPU path timed beside it.
+on a synthetic AMR run, with the reference-faithful CPU rate passed in (bench.py's cpu_baseline measures it).
 
 Layout (scaled by --scale): level 0 = 64 boxes of 64^3,
 level 1 = 96 x 64^3, level 2 = 128 x 32^3, level 3 = 256 x 16^3 + 32 x (48x32x16),
 NCOMP components in the plotfile, all compressed, keep 0.999, fp64 FABs.
-Reported: wall seconds per mode, input GB/s of -c, units/s, and the CPU
-baseline = oracle transform/threshold/RLE/serialize + xz preset 6 (what the
-reference's compress() does per unit, single thread) on a sample of units.
+Reported: wall seconds per mode, input GB/s of -c, units/s, and -c's speedup
+over --cpu-cells-per-s (the reference's per-unit compress() work incl. xz
+preset 6, as bench.py's cpu_baseline times it) when given.
 
 -c is also run with each of --fast-presets (the optional faster xz preset,
 `xzpreset=N`): time, .xz bytes, and that -d regenerates identical plotfiles.
@@ -71,13 +71,21 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--ncomp", type=int, default=4)
     ap.add_argument("--keep", type=float, default=0.999)
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--cpu-cells-per-s", type=float, default=None,
+                    help="the reference-faithful compress() rate (cells/s incl. xz preset 6) to compare -c with: "
+                         "bench.py measures it in its cpu_baseline leg (this tool runs no CPU restatement)")
     ap.add_argument("--fast-presets", default="0,1", help="xzpreset= values timed beside the default 6")
     ap.add_argument("--out", default=str(ROOT / "profiles" / "r03" / "cli_e2e.json"))
     args = ap.parse_args()
     import wcamd  # noqa: F401  (registers the package as wavelet_compression_amd)
-    from oracle import oracle as O
     from wavelet_compression_amd import plotfile as pf
+
+    def field(seed, lo, W, H, D):
+        """SURVEY.md §8(d) field on a box at global corner lo, (D, H, W) fp64."""
+        z, y, x = np.meshgrid(np.arange(D), np.arange(H), np.arange(W), indexing="ij")
+        g = np.random.default_rng(seed).standard_normal((D, H, W))
+        return (300.0 + 50.0 * np.sin(0.1 * (lo[0] + x)) * np.cos(0.07 * (lo[1] + y)) + 0.01 * (lo[2] + z)
+                + 0.05 * g)
 
     names = [f"var_{chr(97 + i)}" for i in range(args.ncomp)]
     base = digit_free_dir()
@@ -88,8 +96,7 @@ def main():
         for l, boxes in enumerate(layout(args.scale)):
             fabs = []
             for b, (lo, (W, H, D)) in enumerate(place(boxes)):
-                comps = [O.synth_box_f64(O.unit_seed(0, l, b, c), lo, W, H, D, sigma=0.05) + 100.0 * c
-                         for c in range(args.ncomp)]
+                comps = [field((l * 100003 + b) * 16 + c, lo, W, H, D) + 100.0 * c for c in range(args.ncomp)]
                 fabs.append((lo, np.stack(comps)))
                 ncells += W * H * D * args.ncomp
             levels.append(fabs)
@@ -138,24 +145,6 @@ def main():
                         f"compresseddir={base}/x/", "-estimate"])
         nunits = sum(len(f) for f in levels) * args.ncomp
 
-        # CPU baseline: the reference's per-unit compress() work, single thread
-        keep = float(np.float32(args.keep))
-        done, cells, t_cpu = 0, 0, 0.0
-        order = [(l, b) for l, fabs in enumerate(levels) for b in range(len(fabs))]
-        random.Random(1).shuffle(order)
-        for (l, b) in order:
-            arr = levels[l][b][1]
-            for c in range(args.ncomp):
-                a32 = O.narrow(arr[c])
-                t = time.perf_counter()
-                p, _k = O.compress_payload(a32, keep)
-                lzma.compress(p, format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64, preset=6)
-                t_cpu += time.perf_counter() - t
-                done += 1
-                cells += a32.size
-            if t_cpu > args.cpu_seconds:
-                break
-        cpu_cells_s = cells / t_cpu
         res = {
             "workload": f"C3-like synthetic plotfile x{args.scale}: 4 levels, {args.ncomp} comps, {nunits} units, "
                         f"{ncells} cells fp64 ({ncells * 8 / 1e9:.2f} GB), keep={args.keep}",
@@ -166,10 +155,8 @@ def main():
             "xz_bytes": xz_bytes, "compressed_fraction": xz_bytes / (ncells * 8),
             "xz_preset": 6, "fast_xz_presets": fast,
             "host_threads": int(os.environ.get("WCAMD_THREADS", os.environ.get("OMP_NUM_THREADS", os.cpu_count()))),
-            "cpu_baseline": {"value": cpu_cells_s, "unit": "cells/s", "cores": 1, "kind": "port",
-                             "sample": f"{done} random units ({cells} cells): oracle transform+threshold+RLE+serialize "
-                                       f"+ xz preset 6 (Python lzma = liblzma), {t_cpu:.1f} s"},
-            "speedup_vs_cpu_compress": (ncells / t_c) / cpu_cells_s,
+            "cpu_compress_cells_per_s": args.cpu_cells_per_s,
+            "speedup_vs_cpu_compress": (ncells / t_c) / args.cpu_cells_per_s if args.cpu_cells_per_s else None,
             "generate_s": t_gen,
             "estimate_output": [ln for ln in est.splitlines() if "Predicted" in ln],
             "cli_logs": logs,

@@ -12,6 +12,7 @@
 // every reconstructed cell ("paths_identical" in the JSON line).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -157,7 +158,9 @@ int main(int argc, char** argv) {
     if (inv_mode >= 2) CK(hipMalloc(&rmse, 8 * boxes));
     void* rowinfo = nullptr;
     const uint64_t rowinfo_bytes = wc_rowindex_bytes(units.data(), boxes);
-    if (inv_mode == 3) CK(hipMalloc(&rowinfo, rowinfo_bytes));
+    // 4 (diagnostic): wc_forward_rows, then wc_inverse_rows WITHOUT the row index (the
+    // row index kernel runs); 5: wc_inverse, then wc_inverse_rows with it, per step
+    if (inv_mode >= 3) CK(hipMalloc(&rowinfo, rowinfo_bytes));
 
     wc_ctx* ctx = nullptr;
     if (wc_ctx_create(0, &ctx) != WC_OK) {
@@ -196,9 +199,28 @@ int main(int argc, char** argv) {
             std::exit(2);
         }
     };
+    // WCB_TOUCH=payload|rows (diagnostic, inverse_mode 3): before each inverse, a
+    // device-to-device copy that streams the payloads (or the row index) through
+    // the caches, on the context's stream: does K6r wait on those reads?
+    const char* touch = std::getenv("WCB_TOUCH");
+    hipStream_t tstream = nullptr;
+    void* tbuf = nullptr;
+    if (touch) {
+        CK(hipStreamCreate(&tstream));
+        wc_set_stream(ctx, tstream);
+        CK(hipMalloc(&tbuf, std::max<uint64_t>(cap, rowinfo_bytes)));
+    }
     auto inv = [&]() {
+        if (touch && std::strcmp(touch, "payload") == 0) CK(hipMemcpyAsync(tbuf, payload, cap, hipMemcpyDeviceToDevice, tstream));
+        if (touch && std::strcmp(touch, "rows") == 0 && rowinfo)
+            CK(hipMemcpyAsync(tbuf, rowinfo, rowinfo_bytes, hipMemcpyDeviceToDevice, tstream));
+        if (inv_mode == 5 && wc_inverse(ctx, payload, offsets, units.data(), boxes, regen) != WC_OK) std::exit(2);
         int rc = inv_mode == 3   ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, rowinfo, cells,
                                                    f64 ? WC_F64 : WC_F32, regen, rmse)
+                 : inv_mode == 4 ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, nullptr, cells,
+                                                   f64 ? WC_F64 : WC_F32, regen, rmse)
+                 : inv_mode == 5 ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, rowinfo, nullptr,
+                                                   WC_F32, regen, nullptr)
                  : inv_mode == 2 ? wc_inverse_rmse(ctx, payload, offsets, units.data(), boxes, cells,
                                                    f64 ? WC_F64 : WC_F32, regen, rmse)
                                  : wc_inverse(ctx, payload, offsets, units.data(), boxes, regen);

@@ -307,6 +307,8 @@ int wc_forward_rows(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* un
         (rc = check_aligned(c, d_rowinfo, "rowinfo", 8)))
         return rc;
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
+    if (c->plan.rowinfo_entries > 0xffffffffull)  // the emit descriptors keep 32-bit row offsets
+        return fail(c, WC_ERR_INVALID, "wc_forward_rows: more than 2^32 row-index entries in one batch");
     if ((rc = ensure_scratch(c))) return rc;
     return forward_staged(c, d_cells, dtype, n, keep, d_payload, d_offsets, d_kept, (uint2*)d_rowinfo);
 }

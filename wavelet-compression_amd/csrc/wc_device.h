@@ -366,36 +366,36 @@ __device__ __forceinline__ uint32_t wave_incl_sum32(uint32_t v) {
 // pairs (wc_emit.h, wc_forward_rows); read by K6r.
 
 // floor(p / D) for p < 2^31 (Granlund-Montgomery, N = 31): dmagic = m |
-// (31 + l) << 32, l = ceil(log2 D), m = floor(2^(31+l) / D) + 1 < 2^32.
+// (31 + l) << 32, l = ceil(log2 D), m = floor(2^(31+l) / D) + 1 < 2^32; for
+// D a power of two m = 0 and the high word is log2 D: a shift (uniform branch).
 __device__ __forceinline__ uint32_t div_rows(uint32_t p, uint64_t dmagic) {
+    if ((uint32_t)dmagic == 0u) return p >> (uint32_t)(dmagic >> 32);
     return (uint32_t)(((uint64_t)p * (uint32_t)dmagic) >> (uint32_t)(dmagic >> 32));
 }
 
 // Rows [r_lo, r_lo + cnt) of this lane get (k, p - r * D).  Most lanes write 0
-// or 1 row; a long run of zeros (empty rows) is spread over the whole wave.
+// or 1 row.  A lane whose pair follows a long run of zeros (an empty
+// stretch of rows: the high-frequency sub-bands of a smooth field) has many:
+// ranges of more than WC_ROWS_BIG rows are written by the whole wave, one
+// range at a time, with coalesced stores; shorter ones by their own lane.
 // Every lane of the wave calls it (uniform control flow).
+#ifndef WC_ROWS_BIG
+#define WC_ROWS_BIG 4
+#endif
 __device__ __forceinline__ void write_rows(uint2* __restrict__ ri, uint32_t r_lo, uint32_t cnt, uint32_t k,
                                            uint32_t p, uint32_t D, int l) {
     if (!__ballot(cnt > 1)) {
         if (cnt) ri[r_lo] = make_uint2(k, p - r_lo * D);
         return;
     }
-    const uint32_t incl = wave_incl_sum32(cnt);
-    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-    const uint32_t excl = incl - cnt;
-    for (uint32_t j0 = 0; j0 < total; j0 += 64) {
-        const uint32_t job = j0 + (uint32_t)l;
-        int o = 0;  // first lane whose inclusive count exceeds job
-#pragma unroll
-        for (int s = 32; s >= 1; s >>= 1)
-            if ((uint32_t)__shfl(incl, o + s - 1) <= job) o += s;
-        o = o > 63 ? 63 : o;
-        const uint32_t orl = __shfl(r_lo, o), oex = __shfl(excl, o), ok = __shfl(k, o), op = __shfl(p, o);
-        if (job < total) {
-            const uint32_t r = orl + (job - oex);
-            ri[r] = make_uint2(ok, op - r * D);
-        }
+    for (unsigned long long big = __ballot(cnt > WC_ROWS_BIG); big; big &= big - 1) {  // uniform
+        const int src = __ffsll((long long)big) - 1;
+        const uint32_t rl = __builtin_amdgcn_readlane(r_lo, src), c = __builtin_amdgcn_readlane(cnt, src);
+        const uint32_t kk = __builtin_amdgcn_readlane(k, src), pp = __builtin_amdgcn_readlane(p, src);
+        for (uint32_t j = (uint32_t)l; j < c; j += 64) ri[rl + j] = make_uint2(kk, pp - (rl + j) * D);
     }
+    if (cnt <= WC_ROWS_BIG)
+        for (uint32_t j = 0; j < cnt; ++j) ri[r_lo + j] = make_uint2(k, p - (r_lo + j) * D);
 }
 
 // Uniform reads of launch-constant tables (plan descriptors, tile lists) through

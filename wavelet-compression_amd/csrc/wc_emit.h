@@ -231,7 +231,7 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
     const uint32_t et = U.et_begin + index;
     const int w = tid >> 6, l = tid & 63;
     // Sparse staging: this thread's 8 segment flags, loaded before the key.
-    const bool sparse = P.flags && U.sparse;
+    const bool sparse = P.flags && (U.mode & 1u);
     constexpr bool kKeyPar = (WC_EMIT_KEYPAR >> (EW == 8 ? 1 : 0)) & 1;
     // The key's scalar load is issued with the flag load, and the threshold is
     // needed only by the keep test: the chain before the coefficient loads is
@@ -241,16 +241,16 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
     unsigned long long ukey = 0;
     if constexpr (kKeyPar) ukey = src.key(P, u);
     RowOut ro{nullptr, 0ull, 0u};
-    if constexpr (kRows) {  // uniform scalar loads, first needed at the pair copy-out
-        ro.dmagic = cst(P.units)[u].dmagic;
-        ro.ri = P.rowinfo + cst(P.units)[u].row_off;
+    if constexpr (kRows) {  // from the descriptor (a load of the unit's record would stall the tile's start)
+        ro.dmagic = (uint64_t)U.dmul | ((uint64_t)((U.mode >> 8) & 0xffu) << 32);
+        ro.ri = P.rowinfo + U.row_off;
         ro.D = (uint32_t)U.nz;
     }
     uint32_t segf = 0xffu;  // bit it: group it may hold kept coefficients
     if (sparse) {
         // one flag byte per segment of TZ = 2^lbz coefficients (16 or 32)
-        const uint8_t* fl = P.flags + U.flag_off + (((uint64_t)index * kTile) >> U.lbz);
-        const int sh = U.lbz;
+        const int sh = (int)((U.mode >> 1) & 7u);  // lbz
+        const uint8_t* fl = P.flags + U.flag_off + (((uint64_t)index * kTile) >> sh);
 #if WC_FLAG_PERM
         // this thread's 8 flags in 8 consecutive bytes (flag_pos): bytes 0 / 1
         const uint2 f8 = *reinterpret_cast<const uint2*>(fl + ((uint32_t)w << (11 - sh)) + ((((uint32_t)l << 2) >> sh) << 3));
@@ -266,7 +266,7 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
     float tf = 0.0f;
     if constexpr (!kKeyPar) tf = unit_thresh(P, src.key(P, u));
     const uint32_t start = index * kTile;
-    const uint32_t len = (uint32_t)min((uint64_t)kTile, U.ncells - start);
+    const uint32_t len = min(kTile, U.ncells - start);
 
     // 1. coefficients -> keep bits (bit it*4 + j).  The flat scratch is 16-B
     // aligned per unit with kFlatTile slack past the last unit.  Sparse units
@@ -378,6 +378,10 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
     for (int i = 0; i < w; ++i) {
         rank += sm[4 + i];
         if (sm[4 + EW + i]) prev = start + sm[4 + EW + i] - 1u;
+    }
+    if constexpr (kRows) {  // wave-uniform: scalar registers
+        rank = __builtin_amdgcn_readfirstlane(rank);
+        prev = __builtin_amdgcn_readfirstlane(prev);
     }
     uint2* __restrict__ pairs = reinterpret_cast<uint2*>(P.payload + U.pay_off + 20);
     emit_pairs<kRows>(q, kb, start, w, l, rank, prev, pairs, stage, ro);

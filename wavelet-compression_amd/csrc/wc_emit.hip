@@ -29,7 +29,7 @@ namespace wc {
 #define WC_EMIT_MINB 8  // 4-wave launch: workgroups per CU the register budget is sized for (64 VGPRs)
 #endif
 #ifndef WC_EMIT_MINB_ROWS
-#define WC_EMIT_MINB_ROWS 6  // the same with the row-index output (wc_forward_rows): 80 VGPRs (72 spill)
+#define WC_EMIT_MINB_ROWS 7  // the same with the row-index output (wc_forward_rows): 72 VGPRs
 #endif
 #ifndef WC_EMIT_MINB8
 #define WC_EMIT_MINB8 2  // 8-wave launch (units of >= 2^21 cells)

@@ -109,16 +109,19 @@ constexpr uint64_t kEmitBigCells = uint64_t(1) << 21;  // 128^3: longer tiles pa
 struct EmitDesc {
     uint64_t coef_off;  // the unit's staged coefficients (UnitDev::coef_off)
     uint64_t pay_off;   // the unit's payload slot
-    uint64_t ncells;    // W*H*D
+    uint32_t ncells;    // W*H*D (< 2^31)
     uint32_t unit;
     uint32_t index;     // tile index within the unit (the ordered form's)
     uint32_t et_begin;  // the unit's first look-back granule
     uint32_t net;       // emit tiles of the unit
     int32_t nx, ny, nz;
-    uint32_t sparse;    // UnitDev::sparse
-    int32_t lbz;        // log2 of the staged segment length (UnitDev::lbz)
+    uint32_t mode;      // bit 0: UnitDev::sparse; bits 1-3: lbz, log2 of the staged segment length;
+                        // bits 8-15: the row divisor's shift (div_rows)
     uint32_t flag_off;  // UnitDev::flag_off (the plan keeps every flag range below 4 GiB)
+    uint32_t row_off;   // the unit's first row-index entry (UnitDev::row_off; the plan keeps it < 2^32)
+    uint32_t dmul;      // the row divisor's multiplier (div_rows; UnitDev::dmagic); row_shift 0: no row index
 };
+static_assert(sizeof(EmitDesc) == 64, "one 64-B descriptor per emit block (one scalar load)");
 
 struct EmitParams {
     const UnitDev* units;

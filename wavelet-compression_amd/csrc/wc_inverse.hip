@@ -605,10 +605,7 @@ struct RixRange {
     uint32_t ks, c0, e;  // rowinfo[r0] = (ks, c0), rowinfo[r0 + tyv].x = e
 };
 
-// Pair indices are clamped to the payload's pair count npairs: an entry past
-// it (a row index that does not belong to this payload) reads no pair.
-__device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* __restrict__ rowinfo, uint32_t npairs,
-                                                   int w, int l) {
+__device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* __restrict__ rowinfo, int w, int l) {
     RixRange R{0u, 0u, 0u};
     const int TX = 1 << T.lbx;
     if (l < TX) {
@@ -617,9 +614,9 @@ __device__ __forceinline__ RixRange rix_load_range(const RTile& T, const uint2* 
         if (bx < hx) {
             const uint64_t r0 = (uint64_t)(bx + ssx * hx) * T.H + T.by0 + ssy * hy;
             const uint2 a = rowinfo[T.row_off + r0];
-            R.ks = min(a.x, npairs);
+            R.ks = a.x;
             R.c0 = a.y;
-            R.e = min(rowinfo[T.row_off + r0 + T.tyv].x, npairs);
+            R.e = rowinfo[T.row_off + r0 + T.tyv].x;
         }
     }
     return R;
@@ -640,10 +637,16 @@ struct RixPlan {
     uint32_t cnt;
 };
 
-__device__ __forceinline__ RixPlan rix_plan(const RTile& T, const RixRange& R, int l) {
+// Pair indices are clamped to the payload's pair count np (an entry past it,
+// from a row index that does not belong to this payload, reads no pair) here,
+// where the range is first used: clamping at the load would wait for the row
+// entries there, behind the pair prefetch issued before them.
+__device__ __forceinline__ RixPlan rix_plan(const RTile& T, RixRange& R, uint32_t np, int l) {
     const uint32_t rlen = (uint32_t)(T.tyv * T.D);
+    R.ks = min(R.ks, np);
+    const uint32_t e = min(R.e, np);
     RixPlan p;
-    p.cnt = (l < (1 << T.lbx) && R.e > R.ks) ? min(R.e - R.ks, rlen) : 0u;
+    p.cnt = (l < (1 << T.lbx) && e > R.ks) ? min(e - R.ks, rlen) : 0u;
     return p;
 }
 
@@ -795,8 +798,8 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
     RTile T = tiles[t];
     uint32_t np;
     const uint2* pr = rix_payload(payload, offsets, npairs, T, np);
-    RixRange R = rix_load_range(T, rowinfo, np, w, l);
-    RixPlan PL = rix_plan(T, R, l);
+    RixRange R = rix_load_range(T, rowinfo, w, l);
+    RixPlan PL = rix_plan(T, R, np, l);
     // prefetch slots, one per range (a wave owns at most 16 ranges at the
     // default WC_OPT_RIX_TX); the RMSE sums need registers
     constexpr int NR = OT ? kRixRounds - WC_RIX_RMSE_ROUNDS_LESS : kRixRounds;
@@ -806,11 +809,11 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
     RTile T1 = T;
     RixRange R1{0u, 0u, 0u};
     const uint2* pr1 = pr;
+    uint32_t np1 = 0;
     if (t1 < tend) {
         T1 = tiles[t1];
-        uint32_t np1;
         pr1 = rix_payload(payload, offsets, npairs, T1, np1);
-        R1 = rix_load_range(T1, rowinfo, np1, w, l);
+        R1 = rix_load_range(T1, rowinfo, w, l);
     }
 
     for (;;) {
@@ -835,15 +838,15 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
         RTile T2 = T1;
         RixRange R2{0u, 0u, 0u};
         const uint2* pr2 = pr1;
+        uint32_t np2 = 0;
         RixPlan PL1{0u};
         if (t1 < tend) {
-            PL1 = rix_plan(T1, R1, l);
+            PL1 = rix_plan(T1, R1, np1, l);
             rix_prefetch<NR>(q, pr1, R1, PL1, T1, l);
             if (t2 < tend) {
                 T2 = tiles[t2];
-                uint32_t np2;
                 pr2 = rix_payload(payload, offsets, npairs, T2, np2);
-                R2 = rix_load_range(T2, rowinfo, np2, w, l);
+                R2 = rix_load_range(T2, rowinfo, w, l);
             }
         }
 
@@ -1017,6 +1020,7 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
         t1 = t2;
         T1 = T2;
         pr1 = pr2;
+        np1 = np2;
         R1 = R2;
     }
 }

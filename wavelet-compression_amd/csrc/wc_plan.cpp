@@ -95,7 +95,7 @@ static void build_etiles(Plan& P, int n) {
                     EmitDesc e{};
                     e.coef_off = d.coef_off;
                     e.pay_off = d.pay_off;
-                    e.ncells = d.ncells;
+                    e.ncells = (uint32_t)d.ncells;
                     e.unit = (uint32_t)i;
                     e.index = t;
                     e.et_begin = d.et_begin;
@@ -103,9 +103,10 @@ static void build_etiles(Plan& P, int n) {
                     e.nx = d.nx;
                     e.ny = d.ny;
                     e.nz = d.nz;
-                    e.sparse = d.sparse;
-                    e.lbz = d.lbz;
+                    e.mode = (d.sparse ? 1u : 0u) | ((uint32_t)d.lbz << 1) | ((uint32_t)(d.dmagic >> 32) << 8);
                     e.flag_off = (uint32_t)d.flag_off;
+                    e.row_off = (uint32_t)d.row_off;
+                    e.dmul = (uint32_t)d.dmagic;
                     P.edesc.push_back(e);
                 }
         }
@@ -248,10 +249,10 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
             P.lds_gen = std::max(P.lds_gen, transform_lds_bytes(d.lbx, d.lby, d.lbz));
         P.lds_inverse = std::max(P.lds_inverse, transform_lds_bytes(d.lbx, d.lby, d.lbz));
         if (d.fast) {  // the row-indexable shape: the forward can emit its row index (wc_forward_rows)
-            // floor(p / D) = (p * m) >> (31 + l), p < 2^31 (wc_device.h div_rows)
+            // floor(p / D) = (p * m) >> (31 + l), p < 2^31, or p >> l for D = 2^l (wc_device.h div_rows)
             const int lg = ceil_log2(d.nz);
             const uint64_t m = (uint64_t(1) << (31 + lg)) / (uint64_t)d.nz + 1;
-            d.dmagic = m | ((uint64_t)(31 + lg) << 32);
+            d.dmagic = (d.nz & (d.nz - 1)) == 0 ? (uint64_t)lg << 32 : m | ((uint64_t)(31 + lg) << 32);
         }
         if (P.inv_rows && set_rix_tiling(d, P.rix_lds, P.rix_lx)) {
             d.rt_begin = (uint32_t)P.rtiles.size();
