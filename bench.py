@@ -66,7 +66,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="time budget of each CPU-baseline sample (boxes run until it is spent)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r04"),
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r05"),
                     help="PMC traffic summaries (tools/pmc_summary.py): a file or a directory of pmc_*.json, "
                          "one per workload; merged into roofline.traffic and each leg's roofline_path.traffic "
                          "when measured on the same workload AND the same kernel sources")
@@ -589,7 +589,21 @@ def sharded_inverse(args, d: Dist, ctx, b: Batch, name):
     m = d.reduce({"seconds": secs, "cells": b.ncells})
     ms = m["seconds"] / args.leg_steps * 1e3
     alg = alg_bytes_inverse(b.ncells, kept, b.n)
+    # the in-process round trip's inverse (wc_inverse_rows with the row index
+    # wc_forward_rows wrote): no row index kernel
+    b.forward_rows(ctx)
+    ctx.synchronize()
+    rsecs = timed(d, ctx, lambda: b.inverse_rows(ctx), args.leg_steps, 2)
+    rst = stage_times(ctx, lambda: b.inverse_rows(ctx), args.leg_steps)
+    rms = d.reduce({"seconds": rsecs})["seconds"] / args.leg_steps * 1e3
     return {"value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
+            "with_forward_row_index": {
+                "ms_per_step": rms, "value": m["cells"] / (rms * 1e-3), "unit": "cells/s",
+                "stage_ms_per_launch": {k: round(v[0], 4) for k, v in rst.items()},
+                "roofline_path": {"achieved_per_gpu": alg / (rms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS,
+                                  "unit": "GB/s", "frac": alg / (rms * 1e-3) / 1e9 / PEAK_HBM_GBPS},
+                "note": "wc_inverse_rows of the same payloads with the forward's row index (the round-trip "
+                        "form; `ms_per_step` above: wc_inverse from the payloads alone, the -d form)"},
             "stage_ms_per_launch": {k: round(v[0], 4) for k, v in st.items()},
             "roofline_path": {"achieved_per_gpu": alg / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                               "frac": alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, "bytes_per_step": alg,
@@ -667,6 +681,18 @@ def host_leg(args, d: Dist, ctx, b: Batch):
     fms = timed(lambda: res.update(r=ctx.forward_host(arr, b.tab, b.n, b.keep)))
     fims = timed(lambda: res.update(o=ctx.inverse_host(payload, offs[:b.n], b.tab, b.n, arr.size)))
     assert np.array_equal(res["r"][0][:d2h + 4], payload[:d2h + 4]) and np.array_equal(res["o"], out[:arr.size])
+    # the same four with huge pages advised on the destinations (WC_OPT_HOST_THP 1,
+    # opt-in since round 5: it changes the caller's memory policy)
+    ctx.set_option(b.capi.WC_OPT_HOST_THP, 1)
+    try:
+        thp = {"ms_per_step": timed(lambda: ctx.forward_host(arr, b.tab, b.n, b.keep, out=bufs)),
+               "fresh_ms_per_step": timed(lambda: res.update(r=ctx.forward_host(arr, b.tab, b.n, b.keep))),
+               "inverse_ms_per_step": timed(lambda: ctx.inverse_host(payload, offs[:b.n], b.tab, b.n, arr.size,
+                                                                     out=out)),
+               "inverse_fresh_ms_per_step": timed(lambda: res.update(
+                   o=ctx.inverse_host(payload, offs[:b.n], b.tab, b.n, arr.size)))}
+    finally:
+        ctx.set_option(b.capi.WC_OPT_HOST_THP, 0)
     del res
     return {"value": b.ncells / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
             "h2d_bytes": h2d, "d2h_bytes": d2h, "host_GBps": (h2d + d2h) / (ms * 1e-3) / 1e9,
@@ -678,8 +704,11 @@ def host_leg(args, d: Dist, ctx, b: Batch):
                               "note": "max(bytes of the larger direction / 57 GB/s, bytes of both / 74.5 GB/s): "
                                       "the box's measured PCIe rates, one direction and both at once "
                                       "(profiles/r04/experiments/gpu_pcie.txt)"},
-            "note": "PCIe-inclusive (pinned host cells in, packed payloads out to reused pageable host buffers), "
-                    "one rank; fresh_ms_per_step allocates new result arrays per call; "
+            "thp_on": thp,
+            "note": "PCIe-inclusive (pinned host cells in, packed payloads out to pageable host buffers), one rank. "
+                    "ms_per_step (since round 4): the caller's output buffers REUSED across calls; "
+                    "fresh_ms_per_step: new result arrays every call (round 3's ms_per_step definition). "
+                    "Compare reused with reused and fresh with fresh. Default WC_OPT_HOST_THP 0; thp_on: 1. "
                     "`value` above is the HBM-resident rate"}
 
 

@@ -152,6 +152,7 @@ int main(int argc, char** argv) {
         }
     }
     wc_ctx_destroy(ctx);
+    std::fprintf(stderr, "dropin_bench: GPU stage alone %.3f s per pass\n", gpu_s);
 
     // -c: compress() per box, the reference's loop order
     std::vector<double> per_box(specs.size());
@@ -161,6 +162,7 @@ int main(int argc, char** argv) {
         std::vector<CompressedWavelet> cw = compress(boxes[i], comps, keep, 0, specs[i].lev, specs[i].box, dir.string());
         per_box[i] = secs(t0, clk::now());
         if ((int)cw.size() != ncomp) return 2;
+        if ((i + 1) % 64 == 0) std::fprintf(stderr, "dropin_bench: -c %zu / %zu boxes\n", i + 1, specs.size());
     }
     const double c_s = secs(c0, clk::now());
     uint64_t xz_bytes = 0;
@@ -188,6 +190,7 @@ int main(int argc, char** argv) {
                 max_err = std::max(max_err, (double)std::fabs(b.data()[j] - o.data()[j]));
         }
     const double d_s = secs(d0, clk::now());
+    std::fprintf(stderr, "dropin_bench: -d %zu files in %.1f s\n", files.size(), d_s);
     std::sort(per_box.begin(), per_box.end());
     std::printf(
         "{\"workload\": \"C3 layout, %zu boxes x %d fp32 components (Box3D), keep %.9g\", \"boxes\": %zu, "

@@ -22,7 +22,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
 STAGE_OF = [("k_transform_fallback", "fallback"), ("k_transform", "transform"), ("k_emit", "emit"),
-            ("k_rowindex", "rowindex"), ("k_decode", "decode"), ("k_inverse", "inverse"), ("k_rmse", "rmse"),
+            ("k_rowindex", "rowindex"), ("k_pair_counts", "pairs"), ("k_decode", "decode"), ("k_inverse", "inverse"), ("k_rmse", "rmse"),
             ("k_hist", "hist")]
 
 

@@ -55,9 +55,11 @@ __global__ void synth(T* out, int dim, long long nboxes, unsigned long long seed
     }
 }
 
-// One box of any shape (the C3 layout): the same field at global origin (gx0, gy0, gz0).
+// One box of any shape (the C3 layout): the field at global origin (gx0, gy0, gz0)
+// with the component's mean and amplitude.
 template <typename T>
-__global__ void synth_box(T* out, int W, int H, int D, int gx0, int gy0, int gz0, unsigned long long seed) {
+__global__ void synth_box(T* out, int W, int H, int D, int gx0, int gy0, int gz0, unsigned long long seed,
+                          double mean = 300.0, double amp = 50.0) {
     const long long total = (long long)W * H * D;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
          i += (long long)gridDim.x * blockDim.x) {
@@ -68,9 +70,14 @@ __global__ void synth_box(T* out, int W, int H, int D, int gx0, int gy0, int gz0
         const double u1 = ((double)(h1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);
         const double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
         const double g = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-        out[i] = (T)(300.0 + 50.0 * sin(0.1 * gx) * cos(0.07 * gy) + 0.01 * gz + 0.05 * g);
+        out[i] = (T)(mean + amp * sin(0.1 * gx) * cos(0.07 * gy) + 0.01 * gz + 0.05 * g);
     }
 }
+
+// per-component field mean and amplitude, as bench_workloads.py COMP_MEAN / COMP_AMP
+// (components 3 and 7: negative signed max, the fallback's dense re-staging)
+static const double kCompMean[8] = {300.0, 1000.0, 5.0, 0.0, 300.0, 1.0, 50.0, 0.0};
+static const double kCompAmp[8] = {50.0, 120.0, 2.0, 40.0, 80.0, 0.5, 10.0, 3.0};
 
 // BASELINE configs[2] (C3) layout, SURVEY §8(d): L0 64 x 64^3, L1 96 x 64^3,
 // L2 128 x 32^3, L3 256 x 16^3 + 32 x (48 x 32 x 16), `ncomp` components per box.
@@ -133,10 +140,12 @@ int main(int argc, char** argv) {
         for (int i = 0; i < boxes; ++i) {
             const wc_unit& u = units[i];
             const int gx = 64 * (i % 16), gy = 64 * ((i / 16) % 8), gz = 64 * (i / 128);
+            const int comp = i % boxes_arg;  // the C3 layout's units: box-major, components inner
+            const double m = kCompMean[comp % 8], a = kCompAmp[comp % 8];
             if (f64)
-                synth_box<double><<<512, 256>>>((double*)cells + u.cell_offset, u.nx, u.ny, u.nz, gx, gy, gz, 1234 + i);
+                synth_box<double><<<512, 256>>>((double*)cells + u.cell_offset, u.nx, u.ny, u.nz, gx, gy, gz, 1234 + i, m, a);
             else
-                synth_box<float><<<512, 256>>>((float*)cells + u.cell_offset, u.nx, u.ny, u.nz, gx, gy, gz, 1234 + i);
+                synth_box<float><<<512, 256>>>((float*)cells + u.cell_offset, u.nx, u.ny, u.nz, gx, gy, gz, 1234 + i, m, a);
         }
     } else if (f64) {
         synth<double><<<4096, 256>>>((double*)cells, dim, boxes, 1234);
