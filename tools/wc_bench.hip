@@ -81,10 +81,15 @@ static const double kCompAmp[8] = {50.0, 120.0, 2.0, 40.0, 80.0, 0.5, 10.0, 3.0}
 
 // BASELINE configs[2] (C3) layout, SURVEY §8(d): L0 64 x 64^3, L1 96 x 64^3,
 // L2 128 x 32^3, L3 256 x 16^3 + 32 x (48 x 32 x 16), `ncomp` components per box.
+// WCB_C3_MASK (diagnostic): bit g keeps group g of the five (L0, L1, L2, L3 cubes, L3 slabs).
 static std::vector<wc_unit> c3_layout(int ncomp) {
     std::vector<wc_unit> u;
     uint64_t off = 0;
+    const char* me = std::getenv("WCB_C3_MASK");
+    const int mask = me ? std::atoi(me) : 31;
+    int group = 0;
     auto add = [&](int n, int W, int H, int D) {
+        if (!((mask >> group++) & 1)) return;
         for (int b = 0; b < n; ++b)
             for (int c = 0; c < ncomp; ++c) {
                 u.push_back(wc_unit{off, W, H, D, 0});
@@ -168,7 +173,8 @@ int main(int argc, char** argv) {
     void* rowinfo = nullptr;
     const uint64_t rowinfo_bytes = wc_rowindex_bytes(units.data(), boxes);
     // 4 (diagnostic): wc_forward_rows, then wc_inverse_rows WITHOUT the row index (the
-    // row index kernel runs); 5: wc_inverse, then wc_inverse_rows with it, per step
+    // row index kernel runs); 5: wc_inverse, then wc_inverse_rows with it, per step;
+    // 6: wc_forward_rows + wc_inverse_rows without the RMSE
     if (inv_mode >= 3) CK(hipMalloc(&rowinfo, rowinfo_bytes));
 
     wc_ctx* ctx = nullptr;
@@ -228,7 +234,8 @@ int main(int argc, char** argv) {
                                                    f64 ? WC_F64 : WC_F32, regen, rmse)
                  : inv_mode == 4 ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, nullptr, cells,
                                                    f64 ? WC_F64 : WC_F32, regen, rmse)
-                 : inv_mode == 5 ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, rowinfo, nullptr,
+                 : inv_mode == 5 || inv_mode == 6
+                                 ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, rowinfo, nullptr,
                                                    WC_F32, regen, nullptr)
                  : inv_mode == 2 ? wc_inverse_rmse(ctx, payload, offsets, units.data(), boxes, cells,
                                                    f64 ? WC_F64 : WC_F32, regen, rmse)

@@ -666,25 +666,32 @@ __device__ __forceinline__ uint2 rix_load_first(const uint2* __restrict__ pr, co
     return (uint32_t)l < cnt ? pr[ks + (uint32_t)l] : make_uint2(0u, 0u);
 }
 
-// Scatter range j's pairs into its LDS range (q0: its first 64 pairs, or
-// loaded here when !have0).
+// One round of a range: pair i = m0 + l (q) lands at carry + the inclusive
+// scan of run + 1 over the round (the range's first pair: + 0).  Returns the
+// carry of the next round.
+__device__ __forceinline__ uint32_t rix_round(float* __restrict__ rg, uint32_t rlen, uint2 q, uint32_t i,
+                                              uint32_t cnt, uint32_t carry) {
+    const int32_t run = (int32_t)q.x;
+    const uint32_t x = (i < cnt && i > 0) ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
+    const uint32_t pos = carry + wave_incl_sum32(x);
+    if (i < cnt && pos < rlen) rg[pos] = __uint_as_float(q.y);
+    return __builtin_amdgcn_readlane(pos, 63);
+}
+
+// Scatter range j's pairs from round m0 on (q0: round m0's pairs, or loaded
+// here when !have0; later rounds are loaded here).
 __device__ __forceinline__ void rix_scatter_range(float* __restrict__ reg, int RS, uint32_t rlen, uint2 q0, bool have0,
                                                   const uint2* __restrict__ pr, const RixRange& R, const RixPlan& p,
-                                                  int l, int j) {
+                                                  int l, int j, uint32_t m0 = 0, uint32_t carry0 = ~0u) {
     const uint32_t cnt = __builtin_amdgcn_readlane(p.cnt, j);
     const uint32_t ks = __builtin_amdgcn_readlane(R.ks, j);
-    const uint32_t c0 = __builtin_amdgcn_readlane(R.c0, j);
     float* __restrict__ rg = reg + j * RS;
-    uint32_t carry = c0;
-    for (uint32_t m0 = 0; m0 < cnt; m0 += 64) {  // uniform
-        const uint32_t i = m0 + (uint32_t)l;
+    uint32_t carry = m0 == 0 ? __builtin_amdgcn_readlane(R.c0, j) : carry0;
+    for (uint32_t m = m0; m < cnt; m += 64) {  // uniform
+        const uint32_t i = m + (uint32_t)l;
         uint2 q = q0;
-        if (m0 != 0 || !have0) q = i < cnt ? pr[ks + i] : make_uint2(0u, 0u);
-        const int32_t run = (int32_t)q.x;
-        const uint32_t x = (i < cnt && i > 0) ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
-        const uint32_t pos = carry + wave_incl_sum32(x);
-        carry = __builtin_amdgcn_readlane(pos, 63);
-        if (i < cnt && pos < rlen) rg[pos] = __uint_as_float(q.y);
+        if (m != m0 || !have0) q = i < cnt ? pr[ks + i] : make_uint2(0u, 0u);
+        carry = rix_round(rg, rlen, q, i, cnt, carry);
     }
 }
 
@@ -731,7 +738,13 @@ __device__ __forceinline__ void rix_prefetch(uint2 (&q)[NR], const uint2* __rest
 #define WC_RIX_RMSE_INLINE 1  // fp64 originals: fused RMSE summed inside the x-quad synthesis (no re-read of the output)
 #endif
 #ifndef WC_RIX_RMSE_ROUNDS_LESS
-#define WC_RIX_RMSE_ROUNDS_LESS 3  // prefetch slots given up by the fused-RMSE forms (no spills)
+// prefetch slots given up by the inline fused-RMSE form (OT 1): 3 is the fewest
+// without spills; 9 measured 3 % faster at C3, 1 % at C2 (profiles/r05/
+// experiments/gpu_k6r_rmse_slots.txt)
+#define WC_RIX_RMSE_ROUNDS_LESS 9
+#endif
+#ifndef WC_RIX_RMSE_PASS_ROUNDS_LESS
+#define WC_RIX_RMSE_PASS_ROUNDS_LESS 3  // the same for the separate-pass forms (OT 2, 3): no spills
 #endif
 // Original cells of one z-block pair of an x-quad column (fused RMSE): at
 // cell index base + sy dy + sz dz, 4 consecutive x cells, narrowed to float
@@ -802,7 +815,9 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
     RixPlan PL = rix_plan(T, R, np, l);
     // prefetch slots, one per range (a wave owns at most 16 ranges at the
     // default WC_OPT_RIX_TX); the RMSE sums need registers
-    constexpr int NR = OT ? kRixRounds - WC_RIX_RMSE_ROUNDS_LESS : kRixRounds;
+    constexpr int NR = OT == 1   ? kRixRounds - WC_RIX_RMSE_ROUNDS_LESS
+                       : OT != 0 ? kRixRounds - WC_RIX_RMSE_PASS_ROUNDS_LESS
+                                 : kRixRounds;
     uint2 q[NR];
     rix_prefetch<NR>(q, pr, R, PL, T, l);
     uint32_t t1 = t + G;
