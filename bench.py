@@ -280,13 +280,11 @@ class Batch:
 
 
 def new_context(args, d: Dist):
-    """The rank's library context.  Ranks sharing one GPU (--rehearse) use the
-    look-backs' ticket form: the launch-order form assumes one process owns the
-    device's dispatch (DESIGN.md §Forward progress)."""
+    """The rank's library context (the default launch-order look-backs, also
+    for ranks sharing one GPU under --rehearse: no wait depends on which
+    process's workgroups are dispatched, DESIGN.md §Forward progress)."""
     import wcamd
     ctx = wcamd.capi.Context(d.local)
-    if args.rehearse and d.world > 1:
-        ctx.set_option(wcamd.capi.WC_OPT_ORDERED, 0)
     if args.rix_xcd:
         ctx.set_option(wcamd.capi.WC_OPT_RIX_XCD, 1)
     if args.inv_groups:

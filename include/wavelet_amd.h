@@ -104,26 +104,24 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
  *   slower on MI355X (C2: 0.53 ms at 1 group, 0.62 at 2, 0.59 at 4), kept as
  *   an option for workloads whose row index dominates.
  * WC_OPT_ORDERED (default 1): the look-back kernels (forward emit, inverse
- *   decode) take each block's tile index from the launch order, relying on
- *   workgroups being dispatched in increasing id (DESIGN.md §Forward
- *   progress); 0 takes it from a per-unit ticket atomic instead, which needs no
- *   assumption about dispatch order.  Same bytes out either way.  Every wait
- *   between workgroups is bounded: a wait that never ends is reported as
- *   WC_ERR_HIP at the next wc_synchronize, not a hang.
- *   The launch-order form is for a device this process owns.  It is NOT safe
- *   when several PROCESSES run look-back kernels on one GPU at once (each can
- *   fill an XCD with waiting blocks): set WCAMD_SHARED_DEVICE=1 in their
- *   environment (every context of the process then uses the tickets), or
- *   WC_OPT_ORDERED 0.  Contexts of ONE process that share a device switch to
- *   the tickets by themselves, and a context whose look-back timed out keeps
- *   the tickets for every later call (sticky; WC_OPT_TICKETS reads it); the
- *   _host entry points then also re-run the failed call once.  wc_get_option
- *   (WC_OPT_ORDERED) returns the form the next launch takes.
+ *   row index and decode) take each block's tile index from the launch order
+ *   (no atomic per block); 0 takes it from a per-unit ticket atomic instead.
+ *   Same bytes out either way, and neither form depends on the order in which
+ *   the hardware dispatches workgroups or on other kernels sharing the device:
+ *   a block that has waited its bound (WC_OPT_SPIN_LIMIT) for a predecessor
+ *   tile to publish derives that tile's count from the tile's own inputs and
+ *   goes on (DESIGN.md §Forward progress).  Several contexts or processes may
+ *   share a GPU in either form.  wc_get_option(WC_OPT_ORDERED) returns the form
+ *   the next launch takes.
  * WC_OPT_TICKETS (default 0): 1 = this context uses the ticket form whatever
- *   WC_OPT_ORDERED says (set by the library after a look-back timeout).
- * WC_OPT_SPIN_LIMIT (default 0 = ~2^20 polls, about 2 s): bound of every wait
- *   between workgroups, in polls.  Diagnostic: a tiny bound forces the timeout
- *   path (tests); results of a call that timed out are not valid.
+ *   WC_OPT_ORDERED says.
+ * WC_OPT_SPIN_LIMIT (default 0 = 64 polls, about 0.1 ms): unanswered polls of
+ *   an unpublished predecessor before a waiting block derives it itself.  Any
+ *   value gives the same bytes; 1 makes nearly every wait take that path
+ *   (tests).
+ * WC_OPT_REVERSE_TILES (default 0; test hook): the launch-order form with each
+ *   unit's tile indices reversed, so that every look-back waits on blocks
+ *   dispatched after it (the worst dispatch order).  Same bytes, slower.
  * WC_OPT_INVERSE_ROWS (default 1): the inverse of even-dims units (W, H even,
  *   D % 8 == 0) indexes the payload's pairs by flat row and reconstructs each
  *   tile straight from the payload; 0 decodes every unit into a dense fp32
@@ -161,6 +159,7 @@ int wc_synchronize(wc_ctx* ctx);  /* also reports (and clears) kernel-side error
 #define WC_OPT_HOST_CHUNK 18
 #define WC_OPT_SPIN_LIMIT 19
 #define WC_OPT_TICKETS 20
+#define WC_OPT_REVERSE_TILES 29
 #define WC_OPT_RIX_XCD 22
 #define WC_OPT_INV_GROUPS 23
 /* 24, 25: retired (the round-4 cohort forward, removed: slower than the

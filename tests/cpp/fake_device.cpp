@@ -333,7 +333,7 @@ const char* hipGetErrorString(hipError_t e) {
 // stand-ins for the device entry points (the kernels' side of the pipeline)
 
 namespace fake {
-int timeout_calls = 0;  // the next k wc_forward calls raise a look-back timeout
+int kernel_error_calls = 0;  // the next k wc_forward calls raise a kernel-detected error (malformed header)
 
 // unit u keeps its first kept_of(u) cells (a function of its shape alone: not
 // of its run, nor of where its cells sit)
@@ -412,8 +412,8 @@ int wc_forward(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, 
     }
     c->plan.d_units.p = tab->data();  // launch_pack reads the slots from here
     std::vector<wc_unit> us(units, units + n);
-    const bool timeout = fake::timeout_calls > 0 && !c->force_tickets;
-    if (timeout) --fake::timeout_calls;
+    const bool kerr = fake::kernel_error_calls > 0;
+    if (kerr) --fake::kernel_error_calls;
     uint32_t* err = (uint32_t*)c->errflag.p;
     enqueue(c->stream, [=] {
         for (int i = 0; i < n; ++i) {
@@ -423,7 +423,7 @@ int wc_forward(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* units, 
             d_kept[i] = fake::kept_of(us[i]);
         }
         d_offsets[n] = d_offsets[n - 1] + 20 + 8ull * d_kept[n - 1];
-        if (timeout) *err |= kErrTimeout;
+        if (kerr) *err |= kErrHeader;
     }, false);
     c->err_check_pending = true;
     return WC_OK;

@@ -14,7 +14,7 @@ void fail_nth(const char* api, int k);  // the k-th next call of api fails (H2D,
 void clear_failures();
 long calls();
 size_t live_allocations();
-extern int timeout_calls;  // the next k wc_forward calls raise a look-back timeout (ticket form: none)
+extern int kernel_error_calls;  // the next k wc_forward calls raise a kernel-detected error
 uint32_t kept_of(const wc_unit& u);
 std::vector<uint8_t> payload_of(const wc_unit& u, const void* cells, int dtype);
 void release_context_tables(const wc_ctx* c);

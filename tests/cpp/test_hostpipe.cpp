@@ -260,16 +260,26 @@ static void test_failures() {
             }
 }
 
-// A look-back wait that timed out (another process's kernels on the device):
-// the _host call reruns once in the ticket form, which stays on (sticky).
-static void test_ticket_retry() {
+// An error a kernel raises in one run of a pipelined _host call (the word is
+// read at the call's end) fails the call after every copy has drained; the
+// next call of the context succeeds.
+static void test_kernel_error() {
     const Batch b = make_batch(30, 8);
     wc_ctx* c = make_ctx();
     c->opt_host_chunk = 1 << 10;
-    fake::timeout_calls = 1;
-    round_trip(c, b, b.cells.data(), "timeout then tickets");
-    CHECK(c->force_tickets, "ticket form not sticky after a timeout");
-    CHECK(fake::timeout_calls == 0, "the timeout was not raised");
+    const int n = (int)b.units.size();
+    const uint64_t cap = wc_payload_bound(b.units.data(), n);
+    {
+        std::vector<uint8_t> pay(cap);
+        std::vector<uint64_t> offs(n + 1);
+        std::vector<uint32_t> kept(n);
+        fake::kernel_error_calls = 1;
+        const int rc = wc_forward_host(c, b.cells.data(), WC_F64, b.units.data(), n, 0.999, pay.data(), cap,
+                                       offs.data(), kept.data());
+        CHECK(rc == WC_ERR_FORMAT, "kernel error: rc %d", rc);
+        CHECK(fake::kernel_error_calls == 0, "the error was not raised");
+    }  // the caller's buffers are gone: a copy still running would write into freed memory
+    round_trip(c, b, b.cells.data(), "after a kernel error");
     destroy_ctx(c);
 }
 
@@ -295,7 +305,7 @@ static void test_argument_errors() {
 int main() {
     test_argument_errors();
     test_runs_and_threads();
-    test_ticket_retry();
+    test_kernel_error();
     test_failures();
     test_bounce_slots();
     std::printf("test_hostpipe: %d checks, %d failed, %ld fake runtime calls, %zu allocations left\n", g_checks, g_fail,

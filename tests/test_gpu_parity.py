@@ -796,10 +796,9 @@ def test_plan_cache_eviction(wc, ctx, oracle):
 
 
 def test_two_contexts_on_one_device(wc, ctx, oracle):
-    """A second live context on the same device switches both to the
-    look-backs' ticket form (the launch-order form assumes one owner of the
-    device's dispatch); payloads and reconstructions stay the oracle's, with
-    both contexts' work in flight on their own streams."""
+    """A second live context on the same device (both in the launch-order
+    form of the look-backs, which depends on no dispatch order); payloads and
+    reconstructions stay the oracle's through the host-buffer calls."""
     keep = KEEPS[1]
     boxes = synth(oracle, DIMS, seed0=23)
     units, n, extent, cells = pack(wc, boxes)

@@ -103,8 +103,8 @@ def test_host_pool_and_prefault_under_sanitizer(san_bins, san, tmp_path):
 def test_host_pipeline_under_sanitizer(san_bins, san, tmp_path):
     """wc_forward_host / wc_inverse_host over the fake runtime (streams are
     threads, events order them, pageable copies block): 1..16 unit runs, 0..8
-    host threads, pinned and pageable sources (bounce slots), the ticket-form
-    retry after a look-back timeout, and an injected failure of every runtime
+    host threads, pinned and pageable sources (bounce slots), a kernel-raised
+    error in a pipelined call, and an injected failure of every runtime
     call and device entry point the pipeline makes, each followed by a freed
     caller buffer (no copy may outlive the call) and a clean call."""
     r = subprocess.run([str(san_bins[san] / "test_hostpipe")], capture_output=True, text=True, timeout=600,

@@ -38,8 +38,9 @@ WC_OPT_RIX_LDS = 15  # row-indexed inverse: LDS floats per workgroup (default 92
 WC_OPT_RIX_TX = 16  # row-indexed inverse: log2 of the tile's x blocks (default 4)
 WC_OPT_RIX_BLOCKED = 17  # row-indexed inverse: contiguous tile runs per workgroup (default 0)
 WC_OPT_HOST_CHUNK = 18  # wc_forward_host: cells per pipelined unit run (default 2^25, 0 = one run)
-WC_OPT_SPIN_LIMIT = 19  # polls before a look-back wait is declared timed out (0: default, ~2 s)
-WC_OPT_TICKETS = 20  # 1: ticket form whatever WC_OPT_ORDERED says (set by a look-back timeout: sticky)
+WC_OPT_SPIN_LIMIT = 19  # polls of an unpublished look-back predecessor before a block derives it itself (0: 64)
+WC_OPT_TICKETS = 20  # 1: ticket form whatever WC_OPT_ORDERED says
+WC_OPT_REVERSE_TILES = 29  # test hook: each unit's look-back tiles in reverse launch order
 WC_OPT_RIX_XCD = 22  # row-indexed inverse tiles dealt to XCDs in contiguous runs (default 0)
 WC_OPT_INV_GROUPS = 23  # row-indexed inverse in N unit groups, row index of g+1 beside K6r of g (default 1)
 WC_OPT_HOST_THREADS = 27  # _host calls: threads that fault in a copy's host destination first (0 = off)

@@ -66,7 +66,7 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
     p.units = (const UnitDev*)P.d_units.p;
     p.edesc = (const EmitDesc*)P.d_edesc.p;
     p.n = n;
-    p.ordered = use_ordered(c) ? 1u : 0u;
+    p.ordered = use_ordered(c) ? (c->opt_reverse ? 2u : 1u) : 0u;
     p.key = (const unsigned long long*)(st + 16);
     p.tickets = (uint32_t*)(st + 16 + 8ull * n);
     p.status = (unsigned long long*)(st + round_up(16 + 20ull * n, 8));
@@ -85,7 +85,6 @@ int stage_emit(wc_ctx* c, int n, double keep, const float* gthresh, uint8_t* d_p
     hipError_t e = launch_emit(c->stream, p, (const float*)c->coef.p, P.nedesc_small,
                                (uint32_t)P.edesc.size() - P.nedesc_small);
     if (e != hipSuccess) return hip_fail(c, e, "emit launch");
-    c->err_check_pending = true;  // a look-back wait that timed out surfaces at wc_synchronize
     return WC_OK;
 }
 
@@ -128,14 +127,12 @@ int wc_ctx_create(int device, wc_ctx** out) {
         wc_ctx_destroy(c);
         return WC_ERR_NOMEM;
     }
-    register_ctx(c);
     *out = c;
     return WC_OK;
 }
 
 void wc_ctx_destroy(wc_ctx* c) {
     if (!c) return;
-    unregister_ctx(c);
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     if (c->aux) (void)hipStreamSynchronize(c->aux);
@@ -229,6 +226,9 @@ int wc_set_option(wc_ctx* c, int option, int64_t value) {
         case WC_OPT_TICKETS:
             c->force_tickets = value != 0;
             return WC_OK;
+        case WC_OPT_REVERSE_TILES:
+            c->opt_reverse = value != 0;
+            return WC_OK;
         case WC_OPT_HOST_THREADS:
             if (value < -1 || value > 256) return fail(c, WC_ERR_INVALID, "WC_OPT_HOST_THREADS: -1..256");
             c->opt_host_threads = (int)value;
@@ -255,6 +255,7 @@ int wc_get_option(const wc_ctx* c, int option, int64_t* value) {
         case WC_OPT_HOST_CHUNK: *value = c->opt_host_chunk; return WC_OK;
         case WC_OPT_SPIN_LIMIT: *value = c->opt_spin_limit; return WC_OK;
         case WC_OPT_TICKETS: *value = c->force_tickets ? 1 : 0; return WC_OK;
+        case WC_OPT_REVERSE_TILES: *value = c->opt_reverse ? 1 : 0; return WC_OK;
         case WC_OPT_HOST_THREADS:
             *value = c->opt_host_threads < 0 ? host_threads_default() : c->opt_host_threads;
             return WC_OK;
@@ -462,7 +463,7 @@ int inverse_impl(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets,
                              dense ? (uint32_t)P.dtiles.size() : 0u, (const FTile*)P.d_rdtiles.p + (dense ? 0 : P.ig_rd[g]),
                              dense ? 0u : P.ig_rd[g + 1] - P.ig_rd[g], (unsigned long long*)c->istate.p, c->epoch,
                              d_payload, d_offsets, (uint32_t*)st, (unsigned long long*)(st + round_up(4ull * n, 8)),
-                             (float*)c->coef.p, (uint2*)c->rowinfo.p, (uint32_t*)c->errflag.p, ord ? 1 : 0,
+                             (float*)c->coef.p, (uint2*)c->rowinfo.p, (uint32_t*)c->errflag.p, ord ? (c->opt_reverse ? 2 : 1) : 0,
                              (uint32_t*)c->npairs.p);
     };
     if (piped) {

@@ -85,49 +85,14 @@ int set_device(wc_ctx* c) {
     return e == hipSuccess ? WC_OK : hip_fail(c, e, "hipSetDevice");
 }
 
-// Live contexts per device, process-wide.  The look-backs' launch-order form
-// (WC_OPT_ORDERED 1) assumes the kernel owns the device's dispatch: with two
-// contexts' kernels in flight on one device, each can fill an XCD with blocks
-// that wait on blocks of its own kernel that the other's occupancy keeps from
-// being dispatched.  Contexts sharing a device therefore use the per-unit
-// tickets (blocks wait only on tiles that running blocks hold).
-static std::mutex g_dev_mu;
-static std::map<int, int> g_dev_ctx;
+// The launch-order form of the look-backs needs no assumption about dispatch
+// order or about other kernels on the device (a wait past its bound derives
+// the predecessor itself, wc_device.h spin_wait): it is the form unless the
+// caller asks for the tickets.
+bool use_ordered(const wc_ctx* c) { return c->opt_ordered && !c->force_tickets; }
 
-// WCAMD_SHARED_DEVICE=1 (read once per process): this process shares its GPUs
-// with other processes that run look-back kernels, so every context takes the
-// ticket form (the launch-order form's dispatch assumption does not hold).
-static bool shared_device_env() {
-    static const bool v = [] {
-        const char* e = std::getenv("WCAMD_SHARED_DEVICE");
-        return e && *e && std::strcmp(e, "0") != 0;
-    }();
-    return v;
-}
-
-void register_ctx(wc_ctx* c) {
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    ++g_dev_ctx[c->device];
-    c->registered = true;
-}
-
-void unregister_ctx(wc_ctx* c) {
-    if (!c->registered) return;
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    --g_dev_ctx[c->device];
-    c->registered = false;
-}
-
-bool use_ordered(const wc_ctx* c) {
-    if (!c->opt_ordered || c->force_tickets || shared_device_env()) return false;
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    auto it = g_dev_ctx.find(c->device);
-    return it == g_dev_ctx.end() || it->second <= 1;
-}
-
-// Surface an error bit a kernel raised (malformed payload in the decode, a
-// look-back wait that timed out) at the next synchronisation point, and clear
-// the word.  The reference exits on a malformed payload
+// Surface an error bit a kernel raised (malformed payload in the decode) at
+// the next synchronisation point, and clear the word.  The reference exits on a malformed payload
 // (src/decompressor.cpp:228-231); here it is WC_ERR_FORMAT.
 int check_kernel_errors(wc_ctx* c) {
     if (!c->err_check_pending) return WC_OK;
@@ -141,14 +106,6 @@ int check_kernel_errors(wc_ctx* c) {
         char buf[128];
         std::snprintf(buf, sizeof buf, "malformed payload (flags 0x%x: 1 header, 2 negative run)", flag);
         return fail(c, WC_ERR_FORMAT, buf);
-    }
-    if (flag & kErrTimeout) {
-        // Sticky: a launch-order look-back that timed out means another
-        // kernel holds the dispatch slots its predecessors need (a shared
-        // device); every later call of this context takes the ticket form.
-        c->timed_out = true;
-        c->force_tickets = true;
-        return fail(c, WC_ERR_HIP, "a dependency wait between workgroups timed out");
     }
     return WC_OK;
 }

@@ -115,10 +115,9 @@ struct wc_ctx {
     wc::Plan plan;
     bool plan_valid = false;
     bool opt_ordered = true;  // WC_OPT_ORDERED (see include/wavelet_amd.h)
-    bool force_tickets = false;  // WC_OPT_TICKETS: sticky ticket form (set by a look-back timeout)
-    uint32_t opt_spin_limit = 0; // WC_OPT_SPIN_LIMIT (0: kSpinLimit), mirrored in errflag[1]
-    bool timed_out = false;      // the last error was a look-back wait that timed out
-    bool registered = false;     // counted in g_dev_ctx
+    bool force_tickets = false;  // WC_OPT_TICKETS: the ticket form of the look-backs
+    bool opt_reverse = false;    // WC_OPT_REVERSE_TILES (test hook): each unit's look-back tiles in reverse launch order
+    uint32_t opt_spin_limit = 0; // WC_OPT_SPIN_LIMIT (0: kSpinSelf), mirrored in errflag[1]
     bool opt_sparse = true;   // WC_OPT_SPARSE
     bool opt_inv_rows = true; // WC_OPT_INVERSE_ROWS
     int opt_rix_lds = kRixLds; // WC_OPT_RIX_LDS
@@ -190,8 +189,6 @@ int check_aligned(wc_ctx* c, const void* p, const char* what, uintptr_t align = 
 hipEvent_t take_event(wc_ctx* c);
 int upload(wc_ctx* c, DevBuf& d, const void* h, size_t bytes, const char* what);
 int set_device(wc_ctx* c);
-void register_ctx(wc_ctx* c);    // counted in the per-device registry (use_ordered)
-void unregister_ctx(wc_ctx* c);
 bool use_ordered(const wc_ctx* c);
 int check_kernel_errors(wc_ctx* c);
 uint64_t cells_extent(const wc_unit* units, int n);

@@ -219,8 +219,8 @@ __device__ __forceinline__ ScanOut block_scan_sum_max(S v, uint32_t m, S* s_sum,
 // ---------------------------------------------------------------------------
 // Hand-offs between workgroups of one launch (MI355X_MICROARCH.md, Valid
 // forms): relaxed agent-scope atomics on self-validating 8-B granules (the
-// word carries its own data, so no fence is needed), bounded spins.
-constexpr uint32_t kSpinLimit = 1u << 20;  // x ~1.7 us: ~2 s before a wait is declared hung
+// word carries its own data, so no fence is needed), bounded waits.
+constexpr uint32_t kSpinSelf = 64;  // polls (~0.1 ms with the backoff) before a wave derives a predecessor itself
 constexpr unsigned long long kFlagAgg = 1ull << 62;   // granule holds this tile's aggregate
 constexpr unsigned long long kFlagIncl = 2ull << 62;  // granule holds the inclusive prefix
 constexpr unsigned long long kMask62 = (1ull << 62) - 1;
@@ -238,23 +238,26 @@ __device__ __forceinline__ void add_rlx(uint32_t* p, uint32_t v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Bounded spin with backoff: pollers share the memory system with the
+// Look-back waits with backoff: pollers share the memory system with the
 // streaming loads (MI355X_MICROARCH.md: 255 pollers cut chip bandwidth
-// 37-71 %), so re-polls slow down from ~0.2 us to ~1.7 us.  err[0] is the
-// context's error word, err[1] its poll bound (WC_OPT_SPIN_LIMIT; 0 = the
-// default kSpinLimit), read only by a wave that is already waiting.
+// 37-71 %), so re-polls slow down from ~0.2 us to ~1.7 us.  A wait is never
+// left to another workgroup's progress: once a wave has polled an
+// unpublished predecessor tile err[1] times (WC_OPT_SPIN_LIMIT; 0 = the default
+// kSpinSelf, ~0.1 ms), it derives that tile's aggregate from the tile's own
+// inputs (which an earlier launch wrote) and moves on.  So no wait depends on
+// which workgroups the hardware has dispatched, in any order, beside any other
+// kernel (DESIGN.md §Forward progress).  err[1] is read only by a wave that is
+// already waiting.
 #ifndef WC_SPIN_S0
 #define WC_SPIN_S0 8  // s_sleep units (64 clocks) before re-polls 1-3
 #endif
 #ifndef WC_SPIN_S1
 #define WC_SPIN_S1 24  // ... before re-polls 4-15
 #endif
-__device__ __forceinline__ bool spin_fail(uint32_t& spins, uint32_t* err) {
-    const uint32_t lim = __hip_atomic_load(err + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (++spins >= (lim ? lim : kSpinLimit)) {  // lim 1: the first unanswered poll fails
-        atomicOr(err, kErrTimeout);
-        return true;
-    }
+__device__ __forceinline__ bool spin_wait(uint32_t& spins, const uint32_t* err) {
+    const uint32_t lim = __hip_atomic_load(const_cast<uint32_t*>(err + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (spins >= (lim ? lim : kSpinSelf)) return true;  // lim 1: after the first unanswered poll
+    ++spins;
     if (spins < 4)
         __builtin_amdgcn_s_sleep(WC_SPIN_S0);
     else if (spins < 16)
@@ -269,9 +272,12 @@ __device__ __forceinline__ bool spin_fail(uint32_t& spins, uint32_t* err) {
 // tile pos - l; indices below 0 read as an inclusive 0) is summed up to the
 // nearest inclusive granule once every lane before it has published; a run
 // of published aggregates before the first unpublished tile is summed and
-// the window slides past it.
+// the window slides past it.  A predecessor still unpublished after the wait
+// bound is summed from agg(tile) (a wave-uniform call by the whole wave: the
+// tile's aggregate derived from its inputs, as its own block would publish it).
+template <class Agg>
 __device__ __forceinline__ unsigned long long lookback_sum62(const unsigned long long* st, int64_t t, int l,
-                                                             uint32_t* err) {
+                                                             const uint32_t* err, Agg agg) {
     unsigned long long excl = 0;
     int64_t pos = t - 1;
     for (uint32_t spins = 0;;) {
@@ -285,7 +291,7 @@ __device__ __forceinline__ unsigned long long lookback_sum62(const unsigned long
         if (take > 0) excl += wave_sum(l < take ? (v & kMask62) : 0ull);
         if (kI < kZ) break;
         pos -= take;
-        if (take == 0 && spin_fail(spins, err)) break;
+        if (take == 0 && spin_wait(spins, err)) excl += agg(pos--) & kMask62;  // tile pos: derived here
     }
     return excl & kMask62;
 }
@@ -297,10 +303,11 @@ __device__ __forceinline__ unsigned long long granule_e(unsigned long long flag,
     return flag | ((unsigned long long)(epoch & kEpochMask) << 32) | sum;
 }
 
-// lookback_sum62 over epoch-tagged granules; the result saturates at 2^32 - 1.
-// timed_out: the wait hit its bound (the sum is then partial).
-__device__ __forceinline__ uint32_t lookback_sum32e(const unsigned long long* st, int64_t t, int l, uint32_t* err,
-                                                    uint32_t epoch, bool& timed_out) {
+// lookback_sum62 over epoch-tagged granules; the result saturates at 2^32 - 1
+// (agg: a tile's saturated 32-bit sum).
+template <class Agg>
+__device__ __forceinline__ uint32_t lookback_sum32e(const unsigned long long* st, int64_t t, int l,
+                                                    const uint32_t* err, uint32_t epoch, Agg agg) {
     unsigned long long excl = 0;
     int64_t pos = t - 1;
     const uint32_t ep = epoch & kEpochMask;
@@ -316,10 +323,7 @@ __device__ __forceinline__ uint32_t lookback_sum32e(const unsigned long long* st
         if (take > 0) excl += wave_sum(l < take ? (v & 0xffffffffull) : 0ull);
         if (kI < kZ) break;
         pos -= take;
-        if (take == 0 && spin_fail(spins, err)) {
-            timed_out = true;
-            break;
-        }
+        if (take == 0 && spin_wait(spins, err)) excl += agg(pos--);  // tile pos: derived here
     }
     return excl > 0xffffffffull ? 0xffffffffu : (uint32_t)excl;
 }

@@ -215,8 +215,37 @@ struct PlainSrc {
     __device__ __forceinline__ PlainTile tile(const EmitDesc& U, uint32_t start) const {
         return PlainTile{reinterpret_cast<const float4*>(coef + U.coef_off + start)};
     }
+    __device__ __forceinline__ const float* unit_coef(const EmitDesc& U) const { return coef + U.coef_off; }
     __device__ __forceinline__ void consumed(const EmitDesc&, int) const {}
 };
+
+// The look-back aggregate of full tile j of unit U (kept count, unit-relative
+// last kept index + 1 or 0), derived by one wave from the tile's staged
+// coefficients exactly as its own block counts them: the look-back's path
+// when tile j has not published within the wait bound (its block may not have
+// been dispatched).  Elements of unflagged segments of a sparse unit were
+// never staged and count as 0, as in emit_tile.  Rare: one 4-B load per lane
+// per 64 elements and a ballot.
+template <int EW>
+__device__ __forceinline__ uint2 emit_tile_agg(const uint8_t* __restrict__ flags, const float* __restrict__ c,
+                                                         uint32_t flag_off, uint32_t j, int sh, bool dense, float tf,
+                                                         int l) {
+    constexpr uint32_t kTile = EW * 2048;
+    const uint32_t s0 = j * kTile;
+    const float* __restrict__ ct = c + s0;
+    uint32_t C = 0, L = 0;
+#pragma unroll 1
+    for (uint32_t e0 = 0; e0 < kTile; e0 += 64) {
+        // a sparse unit's flag of this lane's segment (unflagged: never staged, counts as 0)
+        bool on = true;
+        if (!dense) on = flags[flag_off + flag_pos32((s0 + e0 + (uint32_t)l) >> sh, sh)] != 0;
+        const float v = on ? ct[e0 + (uint32_t)l] : 0.0f;
+        const unsigned long long b = __ballot(fabsf(v) > tf);
+        C += (uint32_t)__popcll(b);
+        if (b) L = e0 + 64u - (uint32_t)__clzll(b);
+    }
+    return make_uint2(C, L ? s0 + L : 0u);
+}
 
 
 // Threshold + ordered pack of tile `index` of unit `u`.  Thread t = (wave w,
@@ -328,15 +357,15 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
             if (l == 0) st_rlx(P.status + et, kFlagIncl | ((unsigned long long)C << 31) | L1);
         } else {
             if (l == 0) st_rlx(P.status + et, kFlagAgg | ((unsigned long long)C << 31) | L1);
-            int64_t pos = (int64_t)et - 1;
-            const int64_t first = U.et_begin;
+            int32_t pos = (int32_t)et - 1;  // emit tiles of a launch: < 2^31
+            const int32_t first = (int32_t)U.et_begin;
             // Window of the 64 nearest predecessors (lane l = tile et-1-l; tiles
             // before the unit read as an inclusive 0).  Lanes up to the nearest
             // inclusive one are summed once every one of them has published;
             // a run of published aggregates before the first unpublished tile
             // is summed and the window slides past it.
             for (uint32_t spins = 0;;) {
-                const int64_t idx = pos - l;
+                const int32_t idx = pos - l;
                 const unsigned long long v = idx >= first ? ld_rlx(P.status + idx) : kFlagIncl;
                 const unsigned long long incl = __ballot((v >> 62) == 2);
                 const unsigned long long zero = __ballot((v >> 62) == 0);
@@ -353,7 +382,14 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
                 }
                 if (kI < kZ) break;
                 pos -= take;
-                if (take == 0 && spin_fail(spins, P.err)) break;
+                if (take == 0 && spin_wait(spins, P.err)) {  // tile pos unpublished: derive its aggregate here
+                    const uint2 a = emit_tile_agg<EW>(P.flags, src.unit_coef(U), U.flag_off,
+                                                      (uint32_t)(pos - first), (int)((U.mode >> 1) & 7u),
+                                                      !sparse || !(tf >= 0.0f), tf, l);
+                    ecnt += a.x;
+                    if (elast == 0 && a.y) elast = a.y;
+                    --pos;
+                }
             }
             if (l == 0)
                 st_rlx(P.status + et, kFlagIncl | ((unsigned long long)(ecnt + C) << 31) | (L1 ? L1 : elast));

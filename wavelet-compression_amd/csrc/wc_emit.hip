@@ -15,12 +15,15 @@
 //
 // Tile index within the unit, two runtime forms (wc_set_option WC_OPT_ORDERED):
 //   1 (default): from the launch order.  Blocks are listed so that a tile's
-//      look-back waits only on tiles of its unit with LOWER block ids; with
-//      in-order dispatch (DESIGN.md §Forward progress) every wait is on a block
-//      that is running or done.  No atomic per block.
+//      look-back waits only on tiles of its unit with LOWER block ids, which
+//      in-order dispatch has started.  No atomic per block.
 //   0: from a per-unit ticket (atomicAdd): a tile's predecessors have always
-//      started whatever the dispatch order.  One atomic round trip per block.
-// Every spin is bounded (spin_fail) and raises kErrTimeout, never a hang.
+//      started.  One atomic round trip per block.
+// Neither form's progress depends on dispatch order: a predecessor that has
+// not published within the wait bound is counted by the waiting wave itself
+// from its staged coefficients (emit_tile_agg; DESIGN.md §Forward progress).
+// P.ordered 2 (test hook WC_OPT_REVERSE_TILES): the launch-order form with
+// each unit's tile indices reversed, the worst dispatch order for the waits.
 #include "wc_emit.h"
 
 namespace wc {
@@ -49,7 +52,7 @@ __global__ __launch_bounds__(EW * kWave, EW == 8 ? WC_EMIT_MINB8 : (ROWS ? WC_EM
     uint2* stage = stage_all[tid >> 6];
     const EmitDesc E = P.edesc[blockIdx.x];
     if (P.ordered) {
-        emit_tile<EW, ROWS>(P, PlainSrc{coef}, E, E.index, sm, stage, tid);
+        emit_tile<EW, ROWS>(P, PlainSrc{coef}, E, P.ordered == 2 ? E.net - 1u - E.index : E.index, sm, stage, tid);
         return;
     }
     if (tid == 0) sm[31] = atomicAdd(P.tickets + E.unit, 1u);

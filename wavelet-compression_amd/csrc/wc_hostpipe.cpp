@@ -539,38 +539,21 @@ static int inverse_host_once(wc_ctx* c, const uint8_t* payload, const uint64_t* 
     return check_kernel_errors(c);
 }
 
-// The host-buffer entry points own their inputs until they return, so a
-// launch-order look-back that timed out (another process's kernels holding the
-// dispatch slots its predecessors need, DESIGN.md §Forward progress) is run
-// again once with the per-unit tickets, which need no dispatch order.
-template <class F>
-static int with_ticket_retry(wc_ctx* c, F once) {
-    c->timed_out = false;
-    const bool was_tickets = c->force_tickets;
-    int rc = once();
-    // check_kernel_errors made the ticket form sticky; run once more with it
-    if (rc == WC_ERR_HIP && c->timed_out && !was_tickets) rc = once();
-    return rc;
-}
-
 extern "C" {
 
 int wc_forward_host(wc_ctx* c, const void* cells, int dtype, const wc_unit* units, int n, double keep,
                     uint8_t* payload, uint64_t cap, uint64_t* offsets, uint32_t* kept) {
     if (!c) return WC_ERR_INVALID;
-    return with_ticket_retry(
-        c, [&] { return forward_host_once(c, CellSource{(const uint8_t*)cells, nullptr}, dtype, units, n, keep, payload,
-                                          cap, offsets, kept, nullptr); });
+    return forward_host_once(c, CellSource{(const uint8_t*)cells, nullptr}, dtype, units, n, keep, payload, cap,
+                             offsets, kept, nullptr);
 }
 
 int wc_round_trip_host(wc_ctx* c, const void* cells, int dtype, const wc_unit* units, int n, double keep,
                        uint8_t* payload, uint64_t cap, uint64_t* offsets, uint32_t* kept, double* rmse) {
     if (!c) return WC_ERR_INVALID;
     if (n > 0 && !rmse) return fail(c, WC_ERR_INVALID, "null buffer");
-    return with_ticket_retry(c, [&] {
-        return forward_host_once(c, CellSource{(const uint8_t*)cells, nullptr}, dtype, units, n, keep, payload, cap,
-                                 offsets, kept, rmse);
-    });
+    return forward_host_once(c, CellSource{(const uint8_t*)cells, nullptr}, dtype, units, n, keep, payload, cap,
+                             offsets, kept, rmse);
 }
 
 int wc_forward_host_units(wc_ctx* c, const void* const* cells, int dtype, const wc_unit* units, int n, double keep,
@@ -585,16 +568,14 @@ int wc_forward_host_units(wc_ctx* c, const void* const* cells, int dtype, const 
         u.cell_offset = cursor;
         if (u.nx > 0 && u.ny > 0 && u.nz > 0) cursor += (uint64_t)u.nx * u.ny * u.nz;
     }
-    return with_ticket_retry(c, [&] {
-        return forward_host_once(c, CellSource{nullptr, cells}, dtype, packed.data(), n, keep, payload, cap, offsets,
-                                 kept, nullptr);
-    });
+    return forward_host_once(c, CellSource{nullptr, cells}, dtype, packed.data(), n, keep, payload, cap, offsets,
+                             kept, nullptr);
 }
 
 int wc_inverse_host(wc_ctx* c, const uint8_t* payload, const uint64_t* offsets, const wc_unit* units, int n,
                     float* out) {
     if (!c) return WC_ERR_INVALID;
-    return with_ticket_retry(c, [&] { return inverse_host_once(c, payload, offsets, units, n, out); });
+    return inverse_host_once(c, payload, offsets, units, n, out);
 }
 
 // Stage host arrays through the context's staging buffers for the

@@ -91,7 +91,6 @@ constexpr unsigned long long kKeyNaNFirst = ~0ull;
 // Error bits raised by kernels (ctx->d_err).
 constexpr uint32_t kErrHeader = 1u;      // payload header disagrees with the unit
 constexpr uint32_t kErrNegativeRun = 2u; // a run length < 0 (reference: UB)
-constexpr uint32_t kErrTimeout = 8u;     // a look-back wait between workgroups hit its bound
 
 constexpr uint32_t kEpochMask = 0x3fffffffu;  // epoch bits of a look-back granule (wc_device.h granule_e)
 

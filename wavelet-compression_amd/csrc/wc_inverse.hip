@@ -109,15 +109,15 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDe
     // tiles up to the one holding the virtual pair k = n (the plan launches
     // floor(ncoeff / kRixTile) + 1, enough for the first dropped pair)
     if (ft.index > n / (uint32_t)kRixTile) return;  // uniform
-    uint32_t t = ft.index;
+    uint32_t t = ordered == 2 ? n / (uint32_t)kRixTile - ft.index : ft.index;  // 2: reversed (test hook)
     if (!ordered) {
         if (tid == 0) s_x[0] = atomicAdd(ticket + u, 1u);
         __syncthreads();
         t = s_x[0];
     }
+    const uint32_t* __restrict__ runs = reinterpret_cast<const uint32_t*>(ph + 20);
     uint32_t v[kRixRounds5];
     {
-        const uint32_t* __restrict__ runs = reinterpret_cast<const uint32_t*>(ph + 20);
         const uint32_t kw = t * (uint32_t)kRixTile + (uint32_t)w * (kRixTile / 4);
 #pragma unroll
         for (int r = 0; r < kRixRounds5; ++r) {
@@ -159,31 +159,25 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDe
     if (w == 0) {
         unsigned long long* st = status + U.dt_begin;
         uint32_t excl = 0;
-        bool timed_out = false;
         if (t == 0) {
             if (l == 0) st_rlx(st, granule_e(kFlagIncl, epoch, tot));
         } else {
             if (l == 0) st_rlx(st + t, granule_e(kFlagAgg, epoch, tot));
-            excl = lookback_sum32e(st, (int64_t)t, l, err, epoch, timed_out);
+            // a predecessor tile unpublished after the wait bound: its sum from its pairs
+            excl = lookback_sum32e(st, (int64_t)t, l, err, epoch, [&](int64_t j) -> uint32_t {
+                const uint32_t k0 = (uint32_t)j * (uint32_t)kRixTile, k1 = min(k0 + (uint32_t)kRixTile, n);
+                uint32_t a = 0;
+                for (uint32_t k = k0 + (uint32_t)l; k < k1; k += 64) {
+                    const int32_t run = (int32_t)runs[2 * k];
+                    a = sat_add(a, run < 0 ? 1u : (uint32_t)run + 1u);
+                }
+                return __builtin_amdgcn_readlane(wave_incl_sum32_sat(a), 63);
+            });
             if (l == 0) st_rlx(st + t, granule_e(kFlagIncl, epoch, sat_add(excl, tot)));
         }
-        if (l == 0) {
-            s_x[0] = timed_out ? 1u : 0u;
-            s_x[1] = (uint32_t)excl;
-        }
+        if (l == 0) s_x[1] = (uint32_t)excl;
     }
     __syncthreads();
-    if (s_x[0]) {
-        // The wait timed out (reported as WC_ERR_HIP): this tile's positions are
-        // unknown, so the rows it should have written would keep an earlier
-        // call's entries, which K6r could follow past this payload.  Overwrite
-        // every row of the unit with an empty range (k = 0): any mix of these
-        // and correctly written entries keeps every pair index within [0, n].
-        uint2* __restrict__ ri = rowinfo + U.row_off;
-        const uint32_t rows = (uint32_t)U.nx * (uint32_t)U.ny + 1u;
-        for (uint32_t r = tid; r < rows; r += kThreads) ri[r] = make_uint2(0u, 0u);
-        return;
-    }
     const uint32_t nc = (uint32_t)U.ncells;
     const uint32_t A = sat_add(s_x[1], wexcl);
 
@@ -246,7 +240,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(const UnitDev* __restrict__
     // interleaves tiles by index across units, so a tile's look-back waits
     // only on lower block ids of its unit (DESIGN.md §Forward progress);
     // ticket form = the unit's next ticket, whatever the dispatch order.
-    uint32_t t = ft.index;
+    uint32_t t = ordered == 2 ? ntile - 1u - ft.index : ft.index;  // 2: reversed (test hook)
     if (!ordered) {
         if (tid == 0) s_x[0] = atomicAdd(ticket + u, 1u);
         __syncthreads();
@@ -295,7 +289,13 @@ __global__ __launch_bounds__(kThreads) void k_decode(const UnitDev* __restrict__
             if (l == 0) st_rlx(st, kFlagIncl | (tot & kMask62));
         } else {
             if (l == 0) st_rlx(st + t, kFlagAgg | (tot & kMask62));
-            excl = lookback_sum62(st, (int64_t)t, l, err);
+            // a predecessor tile unpublished after the wait bound: its sum from its pairs
+            excl = lookback_sum62(st, (int64_t)t, l, err, [&](int64_t j) -> unsigned long long {
+                const int64_t k0 = j * kFlatTile, k1 = min(k0 + (int64_t)kFlatTile, n);
+                unsigned long long a = 0;
+                for (int64_t k = k0 + l; k < k1; k += 64) a += (unsigned long long)((int64_t)(int32_t)pr[k].x + 1);
+                return wave_sum(a);
+            });
             if (l == 0) st_rlx(st + t, kFlagIncl | ((excl + tot) & kMask62));
         }
         if (l == 0) s_x[1] = excl;
@@ -586,11 +586,10 @@ __global__ __launch_bounds__(kThreads) void k_inverse_fast(const float* __restri
 // when scattered) and the row entries of tile t + 2G.
 //
 // The row index of a unit is complete and monotone whatever the payload
-// (k_rowindex), negative runs count as 0 as there, a row-index tile whose
-// look-back timed out empties every row entry of its unit (so no entry of an
-// earlier call survives to point past this payload) and every LDS address is
-// checked against the range: a malformed payload (reported by K5) gives
-// garbage cells, never an out-of-bounds access.
+// (k_rowindex: every tile's look-back completes, negative runs count as 0),
+// pair indices are clamped to the payload's pair count, and every LDS address
+// is checked against the range: a malformed payload (reported by K5) or a row
+// index of other payloads gives garbage cells, never an out-of-bounds access.
 #ifndef WC_RIX_ROUNDS
 #define WC_RIX_ROUNDS 16  // prefetch slots (one per range): 128 VGPRs with the x-quad synthesis, 4 waves per SIMD, no spills
 #endif
