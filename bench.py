@@ -857,6 +857,8 @@ def dropin_leg(args, cpu):
             "note": "the reference's compress() work per host thread (cpu_baseline.with_xz / its threads: oracle "
                     "transform+threshold+RLE+serialize + xz preset 6), per box of this layout's mean size"}
         res["speedup_vs_cpu_single_thread"] = res["compress_cells_per_s"] / rate
+        if isinstance(res.get("write_behind"), dict):
+            res["write_behind"]["speedup_vs_cpu_single_thread"] = res["write_behind"]["compress_cells_per_s"] / rate
     return res
 
 

@@ -127,6 +127,47 @@ static void multi_component_and_quirks_case() {
     std::filesystem::remove_all(dir);
 }
 
+// Write-behind (opt-in): compress() returns before its files exist; after
+// flush_writes() every file holds the bytes the write-through compress()
+// writes, and decompress() flushes by itself before it reads.
+static void write_behind_case() {
+    const auto d1 = scratch(), d2 = scratch();
+    std::vector<multiBox3D> boxes;
+    for (int b = 0; b < 24; ++b) {
+        multiBox3D mb;
+        for (int c = 0; c < 3; ++c) {
+            Box3D x(8 + 2 * (b % 3), 8, 16, 0.0f);
+            for (int z = 0; z < 16; ++z)
+                for (int y = 0; y < 8; ++y)
+                    for (int i = 0; i < x.width(); ++i)
+                        x.set(i, y, z, (float)(c * 100 + b) + 0.5f * (float)((i * 7 + y * 3 + z * 5 + b) % 11));
+            mb.push_back(std::move(x));
+        }
+        boxes.push_back(std::move(mb));
+    }
+    for (int b = 0; b < 24; ++b) compress(boxes[b], {0, 1, 2}, 0.99, 0, 1, b, d1.string());
+    wavelet_amd::set_write_behind(true);
+    REQUIRE(wavelet_amd::write_behind());
+    for (int b = 0; b < 24; ++b) compress(boxes[b], {0, 1, 2}, 0.99, 0, 1, b, d2.string());
+    // decompress() of a queued file: complete before it is read
+    Box3D r = decompress((d2 / "compressed-wavelet-0-1-2-23.xz").string(), 0, 1, 2, 23);
+    Box3D w = decompress((d1 / "compressed-wavelet-0-1-2-23.xz").string(), 0, 1, 2, 23);
+    REQUIRE(r.equals(w, 0));
+    wavelet_amd::flush_writes();
+    for (int b = 0; b < 24; ++b)
+        for (int c = 0; c < 3; ++c) {
+            const std::string name = "compressed-wavelet-0-1-" + std::to_string(c) + "-" + std::to_string(b) + ".xz";
+            std::ifstream f1(d1 / name, std::ios::binary), f2(d2 / name, std::ios::binary);
+            const std::string a((std::istreambuf_iterator<char>(f1)), std::istreambuf_iterator<char>());
+            const std::string e((std::istreambuf_iterator<char>(f2)), std::istreambuf_iterator<char>());
+            REQUIRE(!a.empty() && a == e);
+        }
+    wavelet_amd::set_write_behind(false);
+    REQUIRE(!wavelet_amd::write_behind());
+    std::filesystem::remove_all(d1);
+    std::filesystem::remove_all(d2);
+}
+
 static void calc_rmse_case() {
     Box3D a(2, 2, 2, 0.0f), b(2, 2, 2, 3.5f);
     multiBox3D t1, t2;
@@ -147,6 +188,7 @@ int main() {
                  {"Wavelet decomposition", wavelet_case},
                  {"File writing/compression", file_writing_case},
                  {"Multi-component + quirks", multi_component_and_quirks_case},
+                 {"Write-behind", write_behind_case},
                  {"Calc RMSE", calc_rmse_case}};
     for (auto& c : cases) {
         c.fn();

@@ -41,4 +41,4 @@ def test_host_library_links_codec_and_liblzma():
 def test_reference_unit_tests_against_cpp_mirror():
     r = subprocess.run([str(TEST_BIN)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "6 cases" in r.stdout
+    assert "7 cases" in r.stdout

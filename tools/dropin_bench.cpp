@@ -8,7 +8,9 @@
 //       streams at the current preset, one file per component;
 //   -d: decompress(file) for every file (src/modes.cpp:151-166);
 //   GPU stage alone: the same per-box wc_forward_host_units call without the
-//       xz stage and the files (what compress() spends outside liblzma).
+//       xz stage and the files (what compress() spends outside liblzma);
+//   -c with write-behind (opt-in): the same loop, files queued to the xz
+//       workers, flushed after it, compared byte for byte with the first pass.
 // Prints one JSON line.  Benchmark tool: links only the product libraries.
 //
 // usage: dropin_bench <scratch dir> [ncomp=4] [keep=0.999] [boxes per level: all]
@@ -18,6 +20,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <filesystem>
+#include <fstream>
+#include <iterator>
 #include <string>
 #include <thread>
 #include <vector>
@@ -176,6 +180,31 @@ int main(int argc, char** argv) {
             files.push_back(f);
         }
 
+    // -c again with write-behind (opt-in, xz_pool.h): compress() queues its
+    // components' files and returns; the loop's time, the flush after it, and
+    // every file compared byte for byte with the write-through pass's
+    const std::filesystem::path dir2 = dir / "write_behind";
+    std::filesystem::create_directories(dir2);
+    wavelet_amd::set_write_behind(true);
+    const auto w0 = clk::now();
+    for (size_t i = 0; i < specs.size(); ++i)
+        (void)compress(boxes[i], comps, keep, 0, specs[i].lev, specs[i].box, dir2.string());
+    const double wb_loop_s = secs(w0, clk::now());
+    wavelet_amd::flush_writes();
+    const double wb_s = secs(w0, clk::now());
+    wavelet_amd::set_write_behind(false);
+    bool wb_same = true;
+    for (const std::string& f : files) {
+        const std::filesystem::path g = dir2 / std::filesystem::path(f).filename();
+        std::ifstream a(f, std::ios::binary), b(g, std::ios::binary);
+        const std::string sa((std::istreambuf_iterator<char>(a)), std::istreambuf_iterator<char>());
+        const std::string sb((std::istreambuf_iterator<char>(b)), std::istreambuf_iterator<char>());
+        if (sa.empty() || sa != sb) wb_same = false;
+    }
+    std::filesystem::remove_all(dir2);
+    std::fprintf(stderr, "dropin_bench: -c with write-behind %.1f s (loop %.1f s), files identical %d\n", wb_s,
+                 wb_loop_s, (int)wb_same);
+
     // -d: decompress() per file; every box compared with the compressed one
     // through the same codec (lossy: rle_decode + inverse of the kept set)
     const auto d0 = clk::now();
@@ -199,12 +228,13 @@ int main(int argc, char** argv) {
         "\"compress_cells_per_s\": %.6e, \"gpu_stage_s\": %.4f, \"gpu_stage_ms_per_box\": %.4f, "
         "\"gpu_stage_cells_per_s\": %.6e, \"kept_fraction\": %.6f, \"payload_bytes\": %llu, \"xz_bytes\": %llu, "
         "\"decompress_s\": %.4f, \"decompress_ms_per_file\": %.4f, \"decompress_cells_per_s\": %.6e, "
-        "\"max_abs_err_sampled\": %.6g}\n",
+        "\"max_abs_err_sampled\": %.6g, \"write_behind\": {\"compress_s\": %.4f, \"loop_s\": %.4f, "
+        "\"compress_cells_per_s\": %.6e, \"files_identical\": %s}}\n",
         specs.size(), ncomp, keep, specs.size(), specs.size() * ncomp, (unsigned long long)cells,
         wavelet_amd::xz_preset(), wavelet_amd::host_threads(), c_s, 1e3 * c_s / specs.size(),
         1e3 * per_box[per_box.size() / 2], 1e3 * per_box.back(), cells / c_s, gpu_s, 1e3 * gpu_s / specs.size(),
         cells / gpu_s, (double)kept_total / cells, (unsigned long long)payload_bytes, (unsigned long long)xz_bytes,
-        d_s, 1e3 * d_s / files.size(), cells / d_s, max_err);
+        d_s, 1e3 * d_s / files.size(), cells / d_s, max_err, wb_s, wb_loop_s, cells / wb_s, wb_same ? "true" : "false");
     std::filesystem::remove_all(dir);
     return 0;
 }

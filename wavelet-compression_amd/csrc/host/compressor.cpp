@@ -115,11 +115,14 @@ std::vector<CompressedWavelet> compress(multiBox3D& box, std::vector<int> compon
                                      offsets.data(), kept.data()),
           "GPU forward");
     // per component: the struct, and the .xz file (src/compressor.cpp:250-291);
-    // the components' xz streams are independent: encoded concurrently
+    // the components' xz streams are independent: encoded concurrently, or
+    // queued for the write-behind workers (opt-in, xz_pool.h)
     out.resize(n);
     const uint8_t* payload = t_payload.get();
-    parallel_for((size_t)n, std::min(n, host_threads()), [&](size_t c) {
-        const std::string serialized(reinterpret_cast<const char*>(payload + offsets[c]), 20 + 8ull * kept[c]);
+    const bool behind = write_behind();
+    if (behind) note_write_behind_used();
+    parallel_for((size_t)n, behind ? 1 : std::min(n, host_threads()), [&](size_t c) {
+        std::string serialized(reinterpret_cast<const char*>(payload + offsets[c]), 20 + 8ull * kept[c]);
         CompressedWavelet cw = deserialize_compressed_wavelet(serialized);
         for (const auto& pr : cw.rle_encoded)
             if (std::fabs((double)pr.second) > INT16_MAX) cw.need32 = true;  // src/compressor.cpp:229
@@ -127,10 +130,14 @@ std::vector<CompressedWavelet> compress(multiBox3D& box, std::vector<int> compon
             std::filesystem::path(compressed_dir) / ("compressed-wavelet-" + std::to_string(time) + "-" +
                                                      std::to_string(level) + "-" + std::to_string(components[c]) +
                                                      "-" + std::to_string(box_index) + ".xz");
-        std::ofstream file(fname, std::ios::binary);
-        if (file.is_open()) {  // a failed open silently skips the file, as the reference does (:256-257)
-            const std::string xz = xz_compress(serialized);
-            file.write(xz.data(), (std::streamsize)xz.size());
+        if (behind) {
+            write_behind_submit(std::move(serialized), fname.string());
+        } else {
+            std::ofstream file(fname, std::ios::binary);
+            if (file.is_open()) {  // a failed open silently skips the file, as the reference does (:256-257)
+                const std::string xz = xz_compress(serialized);
+                file.write(xz.data(), (std::streamsize)xz.size());
+            }
         }
         out[c] = std::move(cw);
     });

@@ -12,6 +12,7 @@
 #include "host_ctx.h"
 #include "wavelet_amd/codec_extras.h"
 #include "wavelet_amd/decompressor.h"
+#include "wavelet_amd/xz_pool.h"
 
 namespace wavelet_amd {
 
@@ -98,6 +99,7 @@ Box3D inverse_wavelet_decompose(std::vector<float> flat, int x, int y, int z) {
 }
 
 Box3D decompress(std::string file_path, int /*time*/, int /*level*/, int /*component*/, int /*box_idx*/) {
+    flush_writes();  // a file compress() queued (write-behind, opt-in) is complete before it is read
     const std::string payload = xz_decompress(read_file(file_path));
     if (payload.size() < 20) fatal("Deserialization failed: payload shorter than its header");
     int32_t hdr[5];

@@ -1,0 +1,145 @@
+// write_behind.cpp — opt-in write-behind of compress()'s .xz files.
+//
+// The reference's compress() (src/compressor.cpp:250-291) encodes and writes
+// each component's file before it returns, and its -c loop calls it once per
+// box (src/modes.cpp:100-103): only the box's few components can encode at
+// once, so the drop-in -c is bound by one xz stream per component per box.
+// With write-behind on ($WCAMD_WRITE_BEHIND=1 or set_write_behind(true)),
+// compress() hands each component's serialized payload to this process-wide
+// queue and returns; host_threads() workers encode and write the files while
+// the caller's loop moves on to the next boxes.  Every file is complete, with
+// the bytes compress() would have written, by the time
+//   * flush_writes() returns (explicit),
+//   * decompress() reads (it flushes first: -estimate reads what -c wrote), or
+//   * the process exits normally (the queue's static destructor flushes).
+// A file that cannot be opened is skipped, as in compress(); the queued bytes
+// are bounded ($WCAMD_WRITE_BEHIND_MB, default 2048): submit() waits while the
+// queue holds more.
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <deque>
+#include <fstream>
+#include <mutex>
+#include <thread>
+
+#include "host_ctx.h"
+#include "wavelet_amd/xz_pool.h"
+
+namespace wavelet_amd {
+
+namespace {
+
+std::atomic<int> g_on{-1};  // -1: not chosen yet ($WCAMD_WRITE_BEHIND)
+
+struct Job {
+    std::string payload;
+    std::string path;
+};
+
+class Writer {
+public:
+    Writer() {
+        const char* mb = std::getenv("WCAMD_WRITE_BEHIND_MB");
+        const long v = mb ? std::atol(mb) : 0;
+        limit_ = (uint64_t)(v > 0 ? v : 2048) << 20;
+        const int n = std::max(1, host_threads());
+        for (int i = 0; i < n; ++i) workers_.emplace_back([this] { run(); });
+    }
+    ~Writer() {
+        flush();
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        work_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+    void submit(std::string payload, std::string path) {
+        std::unique_lock<std::mutex> lk(mu_);
+        const uint64_t b = payload.size();
+        // one job larger than the bound still goes in once the queue is empty
+        room_.wait(lk, [&] { return queued_ == 0 || queued_ + b <= limit_; });
+        queued_ += b;
+        ++pending_;
+        q_.push_back(Job{std::move(payload), std::move(path)});
+        lk.unlock();
+        work_.notify_one();
+    }
+    void flush() {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+    }
+
+private:
+    void run() {
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                work_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;  // stop_ with nothing left
+                j = std::move(q_.front());
+                q_.pop_front();
+            }
+            {
+                std::ofstream f(j.path, std::ios::binary);
+                if (f.is_open()) {  // the reference skips a file it cannot open (src/compressor.cpp:256-257)
+                    const std::string xz = xz_encode(reinterpret_cast<const uint8_t*>(j.payload.data()),
+                                                     j.payload.size());
+                    f.write(xz.data(), (std::streamsize)xz.size());
+                }
+            }
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                queued_ -= j.payload.size();
+                if (--pending_ == 0) done_.notify_all();
+            }
+            room_.notify_all();
+        }
+    }
+
+    std::mutex mu_;
+    std::condition_variable work_, room_, done_;
+    std::deque<Job> q_;
+    uint64_t queued_ = 0, limit_ = 0;
+    size_t pending_ = 0;  // queued + being written
+    bool stop_ = false;
+    std::vector<std::thread> workers_;
+};
+
+Writer& writer() {
+    static Writer w;  // destroyed at exit: every queued file is written first
+    return w;
+}
+
+}  // namespace
+
+bool write_behind() {
+    int v = g_on.load(std::memory_order_relaxed);
+    if (v < 0) {
+        const char* e = std::getenv("WCAMD_WRITE_BEHIND");
+        v = e && *e && std::string(e) != "0" ? 1 : 0;
+        int expect = -1;
+        g_on.compare_exchange_strong(expect, v);
+        v = g_on.load(std::memory_order_relaxed);
+    }
+    return v == 1;
+}
+
+void set_write_behind(bool on) {
+    if (!on) flush_writes();
+    g_on.store(on ? 1 : 0, std::memory_order_relaxed);
+}
+
+void write_behind_submit(std::string payload, std::string path) { writer().submit(std::move(payload), std::move(path)); }
+
+static std::atomic<bool> g_used{false};
+
+void flush_writes() {
+    if (g_used.load(std::memory_order_acquire)) writer().flush();
+}
+
+void note_write_behind_used() { g_used.store(true, std::memory_order_release); }
+
+}  // namespace wavelet_amd
