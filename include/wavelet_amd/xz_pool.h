@@ -45,13 +45,17 @@ std::vector<std::string> xz_read_files(const std::vector<std::string>& paths, in
 
 // One buffer -> one .xz stream (preset xz_preset(), or `preset` when >= 0; CRC64).
 std::string xz_encode(const uint8_t* data, size_t size, int preset = -1);
+// The same without exiting: false and a message on an encoder failure.
+bool xz_encode_try(const uint8_t* data, size_t size, std::string& out, const char*& err, int preset = -1);
 
 // Opt-in write-behind of compress()'s files ($WCAMD_WRITE_BEHIND=1 or
 // set_write_behind(true); default off = the reference's behaviour, every file
 // written before compress() returns).  On: compress() queues each component's
 // payload and returns; host_threads() workers encode and write the files.
 // They are complete once flush_writes() returns, before decompress() reads, and
-// at normal process exit.  set_write_behind(false) flushes first.
+// at normal process exit.  set_write_behind(false) flushes first.  An encoder
+// failure in a worker is reported (log + exit(EXIT_FAILURE), as compress()
+// would) by the next flush, or at exit.
 bool write_behind();
 void set_write_behind(bool on);
 void write_behind_submit(std::string payload, std::string path);

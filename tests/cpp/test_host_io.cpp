@@ -17,6 +17,7 @@
 #include <iterator>
 #include <random>
 #include <string>
+#include <thread>
 
 #include "wavelet_amd/argparse.h"
 #include "wavelet_amd/codec_extras.h"
@@ -160,6 +161,37 @@ static void xz_pool_case() {
     }
     const auto back = wavelet_amd::xz_read_files(paths, 5);
     for (size_t i = 0; i < payloads.size(); ++i) REQUIRE(back[i] == payloads[i]);
+}
+
+// The write-behind queue of compress() (opt-in; the GPU test checks compress()
+// itself): payloads submitted from 4 threads through a 1 MiB bound (submit
+// waits for room), a path that cannot be opened (skipped, as compress() does),
+// a flush, and every file equal to the serial encoder's bytes.
+static void write_behind_case() {
+    setenv("WCAMD_WRITE_BEHIND_MB", "1", 1);  // read when the queue starts (first submit)
+    TempDir dir;
+    std::vector<std::string> payloads(48);
+    std::mt19937 rng(5);
+    for (size_t i = 0; i < payloads.size(); ++i) {
+        payloads[i].resize(20 + 8 * (2000 + 3000 * (i % 5)));
+        for (auto& ch : payloads[i]) ch = (char)(rng() % 7);
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < 4; ++t)
+        th.emplace_back([&, t] {
+            for (size_t i = t; i < payloads.size(); i += 4)
+                wavelet_amd::write_behind_submit(payloads[i], (dir.path() / ("w" + std::to_string(i) + ".xz")).string());
+        });
+    for (auto& x : th) x.join();
+    wavelet_amd::write_behind_submit(payloads[0], (dir.path() / "missing" / "w.xz").string());
+    wavelet_amd::note_write_behind_used();
+    wavelet_amd::flush_writes();
+    REQUIRE(!fs::exists(dir.path() / "missing" / "w.xz"));
+    for (size_t i = 0; i < payloads.size(); ++i) {
+        std::ifstream f(dir.path() / ("w" + std::to_string(i) + ".xz"), std::ios::binary);
+        const std::string got((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        REQUIRE(got == wavelet_amd::xz_compress(payloads[i]));
+    }
 }
 
 // The optional faster xz preset: preset parsing, the
@@ -338,6 +370,7 @@ int main(int argc, char** argv) {
     params_case();
     format_files_case();
     xz_pool_case();
+    write_behind_case();
     xz_preset_case();
     plotfile_roundtrip_case();
     bool ref = false;

@@ -12,11 +12,15 @@
 //   * flush_writes() returns (explicit),
 //   * decompress() reads (it flushes first: -estimate reads what -c wrote), or
 //   * the process exits normally (the queue's static destructor flushes).
-// A file that cannot be opened is skipped, as in compress(); the queued bytes
-// are bounded ($WCAMD_WRITE_BEHIND_MB, default 2048): submit() waits while the
+// A file that cannot be opened is skipped, as in compress(); an encoder
+// failure (compress() would log and exit) is logged and exits the process from
+// the next flush, or at exit, once every other queued file is written (a
+// worker never exits the process itself: exit would wait on the queue it
+// holds).  The queued bytes are bounded ($WCAMD_WRITE_BEHIND_MB, default 2048): submit() waits while the
 // queue holds more.
 #include <atomic>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <deque>
 #include <fstream>
@@ -47,7 +51,11 @@ public:
         for (int i = 0; i < n; ++i) workers_.emplace_back([this] { run(); });
     }
     ~Writer() {
-        flush();
+        drain();
+        if (!error_.empty()) {  // at exit: report, and fail the process as compress() would have
+            std::fprintf(stderr, "[error] %s\n", error_.c_str());
+            std::_Exit(EXIT_FAILURE);
+        }
         {
             std::lock_guard<std::mutex> lk(mu_);
             stop_ = true;
@@ -67,11 +75,20 @@ public:
         work_.notify_one();
     }
     void flush() {
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [&] { return pending_ == 0; });
+        drain();
+        std::string e;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            e = error_;
+        }
+        if (!e.empty()) fatal(e);
     }
 
 private:
+    void drain() {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+    }
     void run() {
         for (;;) {
             Job j;
@@ -82,16 +99,18 @@ private:
                 j = std::move(q_.front());
                 q_.pop_front();
             }
+            const char* err = nullptr;
             {
                 std::ofstream f(j.path, std::ios::binary);
+                std::string xz;
                 if (f.is_open()) {  // the reference skips a file it cannot open (src/compressor.cpp:256-257)
-                    const std::string xz = xz_encode(reinterpret_cast<const uint8_t*>(j.payload.data()),
-                                                     j.payload.size());
-                    f.write(xz.data(), (std::streamsize)xz.size());
+                    if (xz_encode_try(reinterpret_cast<const uint8_t*>(j.payload.data()), j.payload.size(), xz, err))
+                        f.write(xz.data(), (std::streamsize)xz.size());
                 }
             }
             {
                 std::lock_guard<std::mutex> lk(mu_);
+                if (err && error_.empty()) error_ = std::string(err) + ": " + j.path;
                 queued_ -= j.payload.size();
                 if (--pending_ == 0) done_.notify_all();
             }
@@ -104,6 +123,7 @@ private:
     std::deque<Job> q_;
     uint64_t queued_ = 0, limit_ = 0;
     size_t pending_ = 0;  // queued + being written
+    std::string error_;   // the first encoder failure
     bool stop_ = false;
     std::vector<std::thread> workers_;
 };

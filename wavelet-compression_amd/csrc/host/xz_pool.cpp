@@ -78,21 +78,29 @@ uint32_t xz_preset() {
 
 void set_xz_preset(uint32_t preset) { g_preset.store((int)preset, std::memory_order_relaxed); }
 
-std::string xz_encode(const uint8_t* data, size_t size, int preset) {
+bool xz_encode_try(const uint8_t* data, size_t size, std::string& out, const char*& err, int preset) {
     lzma_stream strm = LZMA_STREAM_INIT;
     const uint32_t pr = preset >= 0 ? (uint32_t)preset : xz_preset();
-    if (lzma_easy_encoder(&strm, pr, LZMA_CHECK_CRC64) != LZMA_OK) fatal("Failed to initialize LZMA encoder");
-    std::string out(static_cast<size_t>(size * 1.1) + 128, '\0');
+    if (lzma_easy_encoder(&strm, pr, LZMA_CHECK_CRC64) != LZMA_OK) {
+        err = "Failed to initialize LZMA encoder";
+        return false;
+    }
+    out.assign(static_cast<size_t>(size * 1.1) + 128, '\0');
     strm.next_in = data;
     strm.avail_in = size;
     strm.next_out = reinterpret_cast<uint8_t*>(out.data());
     strm.avail_out = out.size();
-    if (lzma_code(&strm, LZMA_FINISH) != LZMA_STREAM_END) {
-        lzma_end(&strm);
-        fatal("LZMA compression failed");
-    }
-    out.resize(out.size() - strm.avail_out);
+    const bool ok = lzma_code(&strm, LZMA_FINISH) == LZMA_STREAM_END;
+    if (ok) out.resize(out.size() - strm.avail_out);
     lzma_end(&strm);
+    if (!ok) err = "LZMA compression failed";
+    return ok;
+}
+
+std::string xz_encode(const uint8_t* data, size_t size, int preset) {
+    std::string out;
+    const char* err = nullptr;
+    if (!xz_encode_try(data, size, out, err, preset)) fatal(err);
     return out;
 }
 
