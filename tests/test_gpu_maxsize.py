@@ -29,8 +29,11 @@ CASES = {
 }
 
 
-@pytest.mark.parametrize("name", list(CASES))
-def test_max_size_unit_matches_tiled_oracle(wc, ctx, oracle, name):
+@pytest.mark.parametrize("name,path", [(n, "payload") for n in CASES] + [("fp32_2046x1024x1024", "rows")])
+def test_max_size_unit_matches_tiled_oracle(wc, ctx, oracle, name, path):
+    """path "payload": wc_forward + wc_inverse_rmse (the inverse's own row index);
+    "rows": wc_forward_rows + wc_inverse_rows (the forward writes the unit's
+    2 095 105-entry row index, read by the inverse: the round-trip form)."""
     import torch
     cs = CASES[name]
     (w, h, d), (W, H, D) = cs["small"], cs["big"]
@@ -51,12 +54,26 @@ def test_max_size_unit_matches_tiled_oracle(wc, ctx, oracle, name):
     regen = torch.full((extent,), float("nan"), dtype=torch.float32, device=dev)
     rmse = torch.full((n,), -1.0, dtype=torch.float64, device=dev)
     torch.cuda.synchronize()  # torch's fills ran on its own stream
-    ctx.forward(cells.data_ptr(), code, units, n, KEEP, payload.data_ptr(), cap, offsets.data_ptr(),
-                kept.data_ptr())
-    ctx.inverse_rmse(payload.data_ptr(), offsets.data_ptr(), units, n, cells.data_ptr(), code, regen.data_ptr(),
-                     rmse.data_ptr())
+    if path == "rows":
+        rb = wc.capi.rowindex_bytes(units, n)
+        assert rb == 8 * (W * H + 1)
+        rows = torch.empty(rb // 8, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        ctx.forward_rows(cells.data_ptr(), code, units, n, KEEP, payload.data_ptr(), cap, offsets.data_ptr(),
+                         kept.data_ptr(), rows.data_ptr(), rb)
+        ctx.inverse_rows(payload.data_ptr(), offsets.data_ptr(), units, n, rows.data_ptr(), regen.data_ptr(),
+                         cells.data_ptr(), code, rmse.data_ptr())
+    else:
+        ctx.forward(cells.data_ptr(), code, units, n, KEEP, payload.data_ptr(), cap, offsets.data_ptr(),
+                    kept.data_ptr())
+        ctx.inverse_rmse(payload.data_ptr(), offsets.data_ptr(), units, n, cells.data_ptr(), code,
+                         regen.data_ptr(), rmse.data_ptr())
     ctx.synchronize()
     del cells
+    if path == "rows":
+        # the sentinel entry (W*H): (nrle, ncoeff - W*H*D = 0)
+        assert rows[W * H:W * H + 1].view(torch.int32).tolist() == [int(kept[0]), 0]
+        del rows
     tiles = (W // w) * (H // h) * (D // d)
     k = int(kept[0])
     assert k == ex.kept * tiles
