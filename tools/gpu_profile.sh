@@ -7,16 +7,17 @@
 #   then the default bench line carrying that traffic, the kernel trace of
 #   bench.py itself, and (DROPIN=1) the drop-in driver, (CLI=1) the end-to-end
 #   CLI, (GPUTEST=1) the -m gpu suite.
-# Paths (tools/wc_bench.hip inv_mode): c2 / c5 / f32_64 forward + wc_inverse
+# Paths (tools/wc_bench.hip inv_mode): c4 forward only; c2 / c5 / f32_64 forward + wc_inverse
 # (row index kernel + K6r), c3 wc_forward_rows + wc_inverse_rows with the fused
 # RMSE (the bench's C3 round-trip leg: no row index kernel).
-# usage: tools/gpu_profile.sh [workload ...]   (default: c2 c3 c5 f32_64)
+# usage: tools/gpu_profile.sh [workload ...]   (default: c2 c3 c5 f32_64 c4)
 set -o pipefail
-declare -A ARGS=([c2]="1024 64 f64 0.999" [c3]="4 c3 f64 0.999" [c5]="512 128 f32 0.9999" [f32_64]="1024 64 f32 0.999")
-declare -A MODE=([c2]=1 [c3]=3 [c5]=1 [f32_64]=1)
-declare -A DT=([c2]=f64 [c3]=f64 [c5]=f32 [f32_64]=f32)
+# c4: the C3 layout with 80 units per box (10 timesteps x 8 components), forward only
+declare -A ARGS=([c2]="1024 64 f64 0.999" [c3]="4 c3 f64 0.999" [c5]="512 128 f32 0.9999" [f32_64]="1024 64 f32 0.999" [c4]="80 c3 f64 0.999")
+declare -A MODE=([c2]=1 [c3]=3 [c5]=1 [f32_64]=1 [c4]=0)
+declare -A DT=([c2]=f64 [c3]=f64 [c5]=f32 [f32_64]=f32 [c4]=f64)
 wls=("$@")
-[ ${#wls[@]} -eq 0 ] && wls=(c2 c3 c5 f32_64)
+[ ${#wls[@]} -eq 0 ] && wls=(c2 c3 c5 f32_64 c4)
 # summaries of workloads not profiled in this call: the committed ones (same sources only, bench.py checks)
 steps=("seed:30:mkdir -p gpurun_out/pmc && (cp profiles/r05/pmc_*.json gpurun_out/pmc/ 2>/dev/null; true)")
 for w in "${wls[@]}"; do
