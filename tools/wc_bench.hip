@@ -55,52 +55,73 @@ __global__ void synth(T* out, int dim, long long nboxes, unsigned long long seed
     }
 }
 
-// One box of any shape (the C3 layout): the field at global origin (gx0, gy0, gz0)
-// with the component's mean and amplitude.
-template <typename T>
-__global__ void synth_box(T* out, int W, int H, int D, int gx0, int gy0, int gz0, unsigned long long seed,
-                          double mean = 300.0, double amp = 50.0) {
-    const long long total = (long long)W * H * D;
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-         i += (long long)gridDim.x * blockDim.x) {
-        const int x = (int)(i % W), y = (int)((i / W) % H), z = (int)(i / ((long long)W * H));
-        const double gx = gx0 + x, gy = gy0 + y, gz = gz0 + z;
-        const unsigned long long h1 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * i + 1));
-        const unsigned long long h2 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * i + 2));
-        const double u1 = ((double)(h1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);
-        const double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
-        const double g = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-        out[i] = (T)(mean + amp * sin(0.1 * gx) * cos(0.07 * gy) + 0.01 * gz + 0.05 * g);
-    }
-}
-
 // per-component field mean and amplitude, as bench_workloads.py COMP_MEAN / COMP_AMP
 // (components 3 and 7: negative signed max, the fallback's dense re-staging)
 static const double kCompMean[8] = {300.0, 1000.0, 5.0, 0.0, 300.0, 1.0, 50.0, 0.0};
 static const double kCompAmp[8] = {50.0, 120.0, 2.0, 40.0, 80.0, 0.5, 10.0, 3.0};
 
+// Every unit of the C3 layout in ONE launch (block row y = unit y; a launch
+// per unit made 46 080 dispatches at C4 size, which the counter passes do not
+// survive): unit i's field (bench_workloads.py synth_cells: its component's
+// mean + amplitude x sin(0.1 gx) cos(0.07 gy) + 0.01 gz + N(0, 0.05)) at its
+// box origin.
+struct SynthUnit {
+    unsigned long long off;
+    int W, H, D, gx, gy, gz;  // dims, origin
+    double mean, amp;         // the component's (host-side table)
+};
+template <typename T>
+__global__ void synth_units(T* out, const SynthUnit* units, unsigned long long seed0) {
+    const SynthUnit u = units[blockIdx.y];
+    const int i = (int)blockIdx.y;
+    const int gx0 = u.gx, gy0 = u.gy, gz0 = u.gz;
+    const double mean = u.mean, amp = u.amp;
+    const unsigned long long seed = seed0 + (unsigned long long)i;
+    const long long total = (long long)u.W * u.H * u.D;
+    for (long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x; c < total;
+         c += (long long)gridDim.x * blockDim.x) {
+        const int x = (int)(c % u.W), y = (int)((c / u.W) % u.H), z = (int)(c / ((long long)u.W * u.H));
+        const double gx = gx0 + x, gy = gy0 + y, gz = gz0 + z;
+        const unsigned long long h1 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * c + 1));
+        const unsigned long long h2 = mix64(seed + 0x9E3779B97F4A7C15ull * (2 * c + 2));
+        const double u1 = ((double)(h1 >> 11) + 1.0) * (1.0 / 9007199254740992.0);
+        const double u2 = (double)(h2 >> 11) * (1.0 / 9007199254740992.0);
+        const double g = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+        out[u.off + c] = (T)(mean + amp * sin(0.1 * gx) * cos(0.07 * gy) + 0.01 * gz + 0.05 * g);
+    }
+}
+
 // BASELINE configs[2] (C3) layout, SURVEY §8(d): L0 64 x 64^3, L1 96 x 64^3,
-// L2 128 x 32^3, L3 256 x 16^3 + 32 x (48 x 32 x 16), `ncomp` components per box.
+// L2 128 x 32^3, L3 256 x 16^3 + 32 x (48 x 32 x 16), `ncomp` units per box
+// (c: component c % 8 of timestep c / 8, so 80 = C4's 10 timesteps x 8
+// components).  Box origins as bench_workloads.py amr_levels (per level: boxes
+// on a per_row x per_plane grid, the slabs from z 256), timestep t shifted 3t
+// in x; `lo` gets each unit's origin.
 // WCB_C3_MASK (diagnostic): bit g keeps group g of the five (L0, L1, L2, L3 cubes, L3 slabs).
-static std::vector<wc_unit> c3_layout(int ncomp) {
+struct Origin {
+    int x, y, z;
+};
+static std::vector<wc_unit> c3_layout(int ncomp, std::vector<Origin>& lo) {
     std::vector<wc_unit> u;
     uint64_t off = 0;
     const char* me = std::getenv("WCB_C3_MASK");
     const int mask = me ? std::atoi(me) : 31;
     int group = 0;
-    auto add = [&](int n, int W, int H, int D) {
+    auto add = [&](int n, int W, int H, int D, int per_row, int per_plane, int z0) {
         if (!((mask >> group++) & 1)) return;
         for (int b = 0; b < n; ++b)
             for (int c = 0; c < ncomp; ++c) {
                 u.push_back(wc_unit{off, W, H, D, 0});
+                lo.push_back(Origin{(b % per_row) * W + 3 * (c / 8), ((b / per_row) % per_plane) * H,
+                                    (b / (per_row * per_plane)) * D + z0});
                 off += ((uint64_t)W * H * D + 3) & ~3ull;
             }
     };
-    add(64, 64, 64, 64);
-    add(96, 64, 64, 64);
-    add(128, 32, 32, 32);
-    add(256, 16, 16, 16);
-    add(32, 48, 32, 16);
+    add(64, 64, 64, 64, 4, 4, 0);
+    add(96, 64, 64, 64, 6, 4, 0);
+    add(128, 32, 32, 32, 8, 4, 0);
+    add(256, 16, 16, 16, 8, 8, 0);
+    add(32, 48, 32, 16, 4, 4, 256);
     return u;
 }
 
@@ -128,8 +149,9 @@ int main(int argc, char** argv) {
     const int inv_groups = argc > 16 ? std::atoi(argv[16]) : 1;
 
     std::vector<wc_unit> units;
+    std::vector<Origin> origins;
     if (c3) {
-        units = c3_layout(boxes_arg);
+        units = c3_layout(boxes_arg, origins);
     } else {
         const unsigned long long per = (unsigned long long)dim * dim * dim;
         for (int i = 0; i < boxes_arg; ++i) units.push_back(wc_unit{per * i, dim, dim, dim, 0});
@@ -142,16 +164,21 @@ int main(int argc, char** argv) {
     void* cells = nullptr;
     CK(hipMalloc(&cells, esz * extent));
     if (c3) {
-        for (int i = 0; i < boxes; ++i) {
-            const wc_unit& u = units[i];
-            const int gx = 64 * (i % 16), gy = 64 * ((i / 16) % 8), gz = 64 * (i / 128);
-            const int comp = i % boxes_arg;  // the C3 layout's units: box-major, components inner
-            const double m = kCompMean[comp % 8], a = kCompAmp[comp % 8];
-            if (f64)
-                synth_box<double><<<512, 256>>>((double*)cells + u.cell_offset, u.nx, u.ny, u.nz, gx, gy, gz, 1234 + i, m, a);
-            else
-                synth_box<float><<<512, 256>>>((float*)cells + u.cell_offset, u.nx, u.ny, u.nz, gx, gy, gz, 1234 + i, m, a);
-        }
+        std::vector<SynthUnit> su(boxes);
+        for (int i = 0; i < boxes; ++i)
+            su[i] = SynthUnit{units[i].cell_offset, units[i].nx, units[i].ny, units[i].nz, origins[i].x,
+                              origins[i].y, origins[i].z, kCompMean[(i % boxes_arg) % 8],
+                              kCompAmp[(i % boxes_arg) % 8]};
+        SynthUnit* d_su = nullptr;
+        CK(hipMalloc(&d_su, sizeof(SynthUnit) * boxes));
+        CK(hipMemcpy(d_su, su.data(), sizeof(SynthUnit) * boxes, hipMemcpyHostToDevice));
+        const dim3 grid(64, (unsigned)boxes);
+        if (f64)
+            synth_units<double><<<grid, 256>>>((double*)cells, d_su, 1234);
+        else
+            synth_units<float><<<grid, 256>>>((float*)cells, d_su, 1234);
+        CK(hipDeviceSynchronize());
+        CK(hipFree(d_su));
     } else if (f64) {
         synth<double><<<4096, 256>>>((double*)cells, dim, boxes, 1234);
     } else {
