@@ -284,3 +284,30 @@ def test_forward_host_units_equals_forward_host(wc, ctx, oracle):
     assert np.array_equal(pa[int(oa[0]):int(oa[n])], pb[int(ob[0]):int(ob[n])])
     for i, b in enumerate(boxes):
         assert wc.capi.unit_payload(pb, ob, kb, i) == oracle.compress_payload(b, keep)[0], i
+
+
+@pytest.mark.parametrize("chunk", [0, 1 << 16])
+def test_round_trip_host_runs(wc, ctx, oracle, chunk):
+    """wc_round_trip_host (the CLI's -estimate): host cells in, payloads and the
+    per-unit RMSE out, the reconstruction never leaving the device; as one run
+    (chunk 0) and as pipelined unit runs of 2^16 cells (each run's forward
+    writes its row index, its inverse reads it).  Payloads equal the oracle's,
+    RMSE within 1e-12 of calc_rmse_per_box on the oracle's reconstruction."""
+    from test_gpu_parity import pack
+    from wavelet_compression_amd.capi import WC_OPT_HOST_CHUNK
+    boxes = synth(oracle, DIMS + [(64, 64, 64)] * 6 + [(32, 32, 32)] * 12, seed0=17)
+    keep = KEEPS[1]
+    units, n, extent, cells = pack(wc, boxes)
+    before = ctx.get_option(WC_OPT_HOST_CHUNK)
+    ctx.set_option(WC_OPT_HOST_CHUNK, chunk)
+    try:
+        payload, offs, kept, rmse = ctx.round_trip_host(cells, units, n, keep)
+    finally:
+        ctx.set_option(WC_OPT_HOST_CHUNK, before)
+    for i, b in enumerate(boxes):
+        b32 = oracle.narrow(b)
+        want = oracle.compress_payload(b32, keep)[0]
+        assert wc.capi.unit_payload(payload, offs, kept, i) == want, i
+        if b.size:
+            ref = oracle.rmse(b32, oracle.decompress_payload(want))
+            assert abs(rmse[i] - ref) <= 1e-12 * abs(ref), (i, rmse[i], ref)
