@@ -296,17 +296,19 @@ int wc_inverse_rmse(wc_ctx* ctx, const uint8_t* d_payload, const uint64_t* d_off
  *   wc_inverse_rows: wc_inverse (d_orig = d_rmse = NULL) or wc_inverse_rmse
  *     (both set) of payloads whose row index d_rowinfo came from
  *     wc_forward_rows of the same payloads and units (NULL: derived from the
- *     payloads, = wc_inverse / wc_inverse_rmse).  Pair indices read from the
- *     row index are clamped to each payload's pair count, so a row index that
- *     belongs to other payloads gives wrong cells but never an access outside
- *     the payloads; headers are checked against the units (WC_ERR_FORMAT at
- *     the next wc_synchronize). */
+ *     payloads, = wc_inverse / wc_inverse_rmse; rowinfo_capacity is then
+ *     ignored, else it must be >= wc_rowindex_bytes).  Pair indices read from
+ *     the row index are clamped to each payload's pair count, so a row index
+ *     that belongs to other payloads gives wrong cells but never an access
+ *     outside the payloads; headers are checked against the units
+ *     (WC_ERR_FORMAT at the next wc_synchronize). */
 uint64_t wc_rowindex_bytes(const wc_unit* units, int n);
 int wc_forward_rows(wc_ctx* ctx, const void* d_cells, int dtype, const wc_unit* units, int n, double keep,
                     uint8_t* d_payload, uint64_t payload_capacity, uint64_t* d_offsets, uint32_t* d_kept,
                     void* d_rowinfo, uint64_t rowinfo_capacity);
 int wc_inverse_rows(wc_ctx* ctx, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
-                    const void* d_rowinfo, const void* d_orig, int dtype, float* d_out, double* d_rmse);
+                    const void* d_rowinfo, uint64_t rowinfo_capacity, const void* d_orig, int dtype, float* d_out,
+                    double* d_rmse);
 
 /* Transform only, host pointers (the reference's static wavelet_decompose). */
 int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* units, int n,

@@ -468,8 +468,9 @@ int wc_forward_rows(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* un
 }
 
 int wc_inverse_rows(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
-                    const void*, const void* d_orig, int, float* d_out, double*) {
+                    const void* d_rowinfo, uint64_t rowinfo_capacity, const void* d_orig, int, float* d_out, double*) {
     if (d_orig) return fail(c, WC_ERR_INVALID, "fake: fused RMSE");
+    if (d_rowinfo && rowinfo_capacity < wc_rowindex_bytes(units, n)) return fail(c, WC_ERR_INVALID, "fake: rows");
     return wc_inverse(c, d_payload, d_offsets, units, n, d_out);
 }
 

@@ -261,6 +261,35 @@ def test_misaligned_device_buffers_rejected(wc, ctx):
         ctx.inverse(payload.data_ptr(), offsets.data_ptr(), units, n, cells[2:].data_ptr())
 
 
+def test_row_index_capacity_checked(wc, ctx, oracle):
+    """A row index buffer smaller than wc_rowindex_bytes is rejected by both
+    calls (WC_ERR_INVALID before any launch), never read or written past."""
+    import torch
+    boxes = synth(oracle, [(16, 16, 16), (32, 16, 8)], seed0=19)
+    units, n, extent, d_cells, dev = _device_batch(wc, boxes)
+    cap = wc.capi.payload_bound(units, n)
+    rb = wc.capi.rowindex_bytes(units, n)
+    payload = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    kept = torch.zeros(n, dtype=torch.int32, device=dev)
+    rows = torch.zeros(rb // 8, dtype=torch.int64, device=dev)
+    out = torch.zeros(extent, dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    with pytest.raises(WaveletError) as e:
+        ctx.forward_rows(d_cells.data_ptr(), wc.capi.WC_F64, units, n, 0.999, payload.data_ptr(), cap,
+                         offsets.data_ptr(), kept.data_ptr(), rows.data_ptr(), rb - 8)
+    assert e.value.code == wc.capi.WC_ERR_INVALID
+    ctx.forward_rows(d_cells.data_ptr(), wc.capi.WC_F64, units, n, 0.999, payload.data_ptr(), cap,
+                     offsets.data_ptr(), kept.data_ptr(), rows.data_ptr(), rb)
+    with pytest.raises(WaveletError) as e:
+        ctx.inverse_rows(payload.data_ptr(), offsets.data_ptr(), units, n, rows.data_ptr(), out.data_ptr(),
+                         rowinfo_capacity=rb - 8)
+    assert e.value.code == wc.capi.WC_ERR_INVALID and "rowinfo_capacity" in str(e.value)
+    ctx.inverse_rows(payload.data_ptr(), offsets.data_ptr(), units, n, rows.data_ptr(), out.data_ptr(),
+                     rowinfo_capacity=rb)
+    ctx.synchronize()
+
+
 def test_forward_host_units_equals_forward_host(wc, ctx, oracle):
     """wc_forward_host_units (each unit's cells at its own host pointer, the
     drop-in compress()'s call) gives the bytes of wc_forward_host over the

@@ -257,12 +257,12 @@ int main(int argc, char** argv) {
         if (touch && std::strcmp(touch, "rows") == 0 && rowinfo)
             CK(hipMemcpyAsync(tbuf, rowinfo, rowinfo_bytes, hipMemcpyDeviceToDevice, tstream));
         if (inv_mode == 5 && wc_inverse(ctx, payload, offsets, units.data(), boxes, regen) != WC_OK) std::exit(2);
-        int rc = inv_mode == 3   ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, rowinfo, cells,
+        int rc = inv_mode == 3   ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, rowinfo, rowinfo_bytes, cells,
                                                    f64 ? WC_F64 : WC_F32, regen, rmse)
-                 : inv_mode == 4 ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, nullptr, cells,
+                 : inv_mode == 4 ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, nullptr, 0, cells,
                                                    f64 ? WC_F64 : WC_F32, regen, rmse)
                  : inv_mode == 5 || inv_mode == 6
-                                 ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, rowinfo, nullptr,
+                                 ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, rowinfo, rowinfo_bytes, nullptr,
                                                    WC_F32, regen, nullptr)
                  : inv_mode == 2 ? wc_inverse_rmse(ctx, payload, offsets, units.data(), boxes, cells,
                                                    f64 ? WC_F64 : WC_F32, regen, rmse)

@@ -110,7 +110,7 @@ def load_library() -> ctypes.CDLL:
                                   vp, vp]),
         "wc_rowindex_bytes": (u64, [up, i32]),
         "wc_forward_rows": (i32, [vp, vp, i32, up, i32, ctypes.c_double, vp, u64, vp, vp, vp, u64]),
-        "wc_inverse_rows": (i32, [vp, vp, vp, up, i32, vp, vp, i32, vp, vp]),
+        "wc_inverse_rows": (i32, [vp, vp, vp, up, i32, vp, u64, vp, i32, vp, vp]),
         "wc_forward_host_units": (i32, [vp, ctypes.POINTER(vp), i32, up, i32, ctypes.c_double, vp, u64, vp, vp]),
         "wc_round_trip_host": (i32, [vp, vp, i32, up, i32, ctypes.c_double, vp, u64, vp, vp, vp]),
     }
@@ -242,12 +242,17 @@ class Context:
                                             ctypes.c_void_p(d_kept), ctypes.c_void_p(d_rowinfo), rowinfo_capacity))
 
     def inverse_rows(self, d_payload: int, d_offsets: int, units, n: int, d_rowinfo: int | None, d_out: int,
-                     d_orig: int | None = None, dtype: int = WC_F32, d_rmse: int | None = None):
+                     d_orig: int | None = None, dtype: int = WC_F32, d_rmse: int | None = None,
+                     rowinfo_capacity: int | None = None):
         """wc_inverse (d_orig None) or wc_inverse_rmse with the row index of
-        wc_forward_rows (d_rowinfo None: derived from the payloads)."""
+        wc_forward_rows (d_rowinfo None: derived from the payloads).
+        rowinfo_capacity: bytes of the d_rowinfo buffer (default: exactly
+        rowindex_bytes(units, n), the size forward_rows needs)."""
+        cap = rowinfo_capacity if rowinfo_capacity is not None else (rowindex_bytes(units, n) if d_rowinfo else 0)
         self._check(self._L.wc_inverse_rows(self._h, ctypes.c_void_p(d_payload), ctypes.c_void_p(d_offsets),
-                                            units, n, ctypes.c_void_p(d_rowinfo or 0), ctypes.c_void_p(d_orig or 0),
-                                            dtype, ctypes.c_void_p(d_out), ctypes.c_void_p(d_rmse or 0)))
+                                            units, n, ctypes.c_void_p(d_rowinfo or 0), cap,
+                                            ctypes.c_void_p(d_orig or 0), dtype, ctypes.c_void_p(d_out),
+                                            ctypes.c_void_p(d_rmse or 0)))
 
     def forward_stage(self, d_cells: int, dtype: int, units, n: int, d_hist: int | None = None):
         """Global-threshold mode, step 1 (include/wavelet_amd.h): transform into

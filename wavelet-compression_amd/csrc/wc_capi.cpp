@@ -529,26 +529,29 @@ extern "C" {
 
 int wc_inverse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
                float* d_out) {
-    return wc_inverse_rows(c, d_payload, d_offsets, units, n, nullptr, nullptr, WC_F32, d_out, nullptr);
+    return wc_inverse_rows(c, d_payload, d_offsets, units, n, nullptr, 0, nullptr, WC_F32, d_out, nullptr);
 }
 
 int wc_inverse_rmse(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
                     const void* d_orig, int dtype, float* d_out, double* d_rmse) {
     if (!c) return WC_ERR_INVALID;
     if (n > 0 && (!d_orig || !d_rmse)) return fail(c, WC_ERR_INVALID, "null buffer");
-    return wc_inverse_rows(c, d_payload, d_offsets, units, n, nullptr, d_orig, dtype, d_out, d_rmse);
+    return wc_inverse_rows(c, d_payload, d_offsets, units, n, nullptr, 0, d_orig, dtype, d_out, d_rmse);
 }
 
 // wc_inverse / wc_inverse_rmse, and with d_rowinfo the caller's row index in
 // place of the row index kernel (wc_forward_rows wrote it for these payloads).
 int wc_inverse_rows(wc_ctx* c, const uint8_t* d_payload, const uint64_t* d_offsets, const wc_unit* units, int n,
-                    const void* d_rowinfo, const void* d_orig, int dtype, float* d_out, double* d_rmse) {
+                    const void* d_rowinfo, uint64_t rowinfo_capacity, const void* d_orig, int dtype, float* d_out,
+                    double* d_rmse) {
     if (!c) return WC_ERR_INVALID;
     int rc;
     if ((rc = validate_units(c, units, n))) return rc;
     if (d_orig && dtype != WC_F32 && dtype != WC_F64) return fail(c, WC_ERR_INVALID, "dtype");
     if (n == 0) return WC_OK;
     if (!d_payload || !d_offsets || !d_out || (!d_orig != !d_rmse)) return fail(c, WC_ERR_INVALID, "null buffer");
+    if (d_rowinfo && rowinfo_capacity < wc_rowindex_bytes(units, n))
+        return fail(c, WC_ERR_INVALID, "rowinfo_capacity < wc_rowindex_bytes");
     if ((rc = check_aligned(c, d_payload, "payload")) || (rc = check_aligned(c, d_offsets, "offsets", 8)) ||
         (rc = check_aligned(c, d_out, "out")) || (rc = check_aligned(c, d_rowinfo, "rowinfo", 8)) ||
         (rc = check_aligned(c, d_rmse, "rmse", 8)) ||

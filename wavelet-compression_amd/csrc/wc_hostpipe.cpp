@@ -356,7 +356,7 @@ static int forward_host_once(wc_ctx* c, CellSource src, int dtype, const wc_unit
             gate.publish(r + 1);
             // the round trip: this run's payloads back to cells with the row
             // index just written, and calc_rmse_per_box against its cells
-            if (rmse && ((rc2 = wc_inverse_rows(c, pay, doff, units + a, m, c->h_rows.p, nullptr, WC_F32,
+            if (rmse && ((rc2 = wc_inverse_rows(c, pay, doff, units + a, m, c->h_rows.p, rows_cap, nullptr, WC_F32,
                                                 (float*)c->h_out.p, nullptr)) ||
                          (rc2 = wc_rmse(c, c->h_cells.p, dtype, (const float*)c->h_out.p, units + a, m,
                                         (double*)c->h_rmse.p + a))))
