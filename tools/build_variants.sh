@@ -3,7 +3,9 @@
 # of the product sources writes invalid results) under tools/variants/<name>/ for
 # A/B runs of tools/bin/wc_bench with LD_LIBRARY_PATH (its RUNPATH yields to it).
 set -e
-CS=wavelet-compression_amd/csrc
+# VSRC=<dir>: compile the kernel and C-ABI sources from a patched copy of csrc
+# (diagnostic variants whose results are not valid never enter the product tree)
+CS=${VSRC:-wavelet-compression_amd/csrc}
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-gpu-flush-denormals-to-zero -fno-fast-math -Iinclude -I$CS"
 for spec in "$@"; do
   name="${spec%%:*}"; defs="${spec#*:}"
