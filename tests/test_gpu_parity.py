@@ -494,6 +494,21 @@ def test_reference_file_writing_case(wc, tmp_path):
     assert np.array_equal(back, box)
 
 
+def test_python_mirror_compress_payloads(wc, oracle):
+    """codec.compress_payloads (the Python mirror's batched compress(): each
+    box uploaded from its own array, wc_forward_host_units) over mixed shapes
+    and keeps: the oracle's bytes, and decompress_payloads inverts them."""
+    boxes = [oracle.narrow(b) for b in synth(oracle, DIMS, seed0=29)]
+    for keep in KEEPS:
+        got = wc.compress_payloads(boxes, keep)
+        for i, b in enumerate(boxes):
+            assert got[i] == oracle.compress_payload(b, keep)[0], (keep, i)
+        back = wc.decompress_payloads(got)
+        for i, b in enumerate(boxes):
+            if b.size:
+                assert back[i].tobytes() == oracle.decompress_payload(got[i]).tobytes(), (keep, i)
+
+
 def test_reference_calc_rmse_case(wc):
     """Mirror of src/calc-loss.cpp:68-86: {3.5, 3.5}."""
     a = [np.zeros((2, 2, 2), np.float32)] * 2

@@ -123,14 +123,13 @@ def _pairs_need32(vals: np.ndarray) -> bool:
 def compress_payloads(boxes: Sequence[np.ndarray], keep: float, device: int = 0):
     """Batched forward path: list of Box3D -> list of serialized payload bytes.
 
-    One wc_forward_host call for the whole list (all units in one launch set)."""
+    One wc_forward_host_units call for the whole list (all units in one launch
+    set, each uploaded from its own array: no packing copy on the host, as the
+    C++ mirror's compress())."""
     dims = [_box_dims(b) for b in boxes]
-    units, n, extent = capi.make_units(dims)
-    cells = np.zeros(max(extent, 1), np.float32)
-    for i, b in enumerate(boxes):
-        o = units[i].cell_offset
-        cells[o:o + b.size] = np.ascontiguousarray(b, np.float32).ravel()
-    payload, offsets, kept = context(device).forward_host(cells, units, n, keep)
+    units, n, _ = capi.make_units(dims)
+    arrs = [np.ascontiguousarray(b, np.float32) for b in boxes]
+    payload, offsets, kept = context(device).forward_host_units(arrs, units, n, keep)
     return [capi.unit_payload(payload, offsets, kept, i) for i in range(n)]
 
 
