@@ -23,6 +23,27 @@ def test_header_declares_expected_entry_points(wc):
     assert set(decl) == set(wc.capi.EXPORTED)
 
 
+def test_binding_constants_match_header(wc):
+    """Every status, dtype and option constant of include/wavelet_amd.h has the
+    same value in the Python binding, the stage names follow the WC_STAGE_*
+    indices, and HIST_BINS is WC_HIST_BINS: the binding cannot drift from the ABI."""
+    import re
+    from pathlib import Path
+    text = (Path(__file__).resolve().parent.parent / "include" / "wavelet_amd.h").read_text()
+    defs = {m.group(1): int(m.group(2)) for m in re.finditer(r"^#define (WC_[A-Z0-9_]+) (\d+)", text, re.M)}
+    checked = 0
+    for name, v in defs.items():
+        if name.startswith(("WC_OK", "WC_ERR_", "WC_F32", "WC_F64", "WC_OPT_")):
+            assert getattr(wc.capi, name) == v, name
+            checked += 1
+    assert checked >= 20
+    stages = sorted((v, k) for k, v in defs.items() if k.startswith("WC_STAGE_"))
+    assert len(stages) == defs["WC_NUM_STAGES"] == len(wc.capi.STAGES)
+    for (i, k), s in zip(stages, wc.capi.STAGES):
+        assert k == "WC_STAGE_" + s.upper(), (k, s)
+    assert wc.capi.HIST_BINS == defs["WC_HIST_BINS"]
+
+
 def test_library_exports_every_declared_symbol(wc):
     lib = wc.capi.load_library()
     for name in declared_functions():
