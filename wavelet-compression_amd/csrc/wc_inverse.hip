@@ -1067,7 +1067,7 @@ __global__ __launch_bounds__(kThreads) void k_rmse_partial(const T* __restrict__
     if (threadIdx.x == 0) part[blockIdx.x] = ((s_w[0] + s_w[1]) + s_w[2]) + s_w[3];
 }
 
-__global__ __launch_bounds__(64) void k_rmse_final(const UnitDev* __restrict__ units, int n,
+__global__ __launch_bounds__(64) void k_rmse_final(const UnitDev* __restrict__ units, int /*n*/,
                                                  const double* __restrict__ part,
                                                  double* __restrict__ rmse) {
     const int u = blockIdx.x;
