@@ -1,5 +1,5 @@
 """Per-kernel SQ cycle breakdown from a rocprofv3 --pmc counter_collection.csv
-(tools/gpu_sq3.sh): averages over the dispatches of each kernel, and the shares
+(tools/gpu_sq.sh): averages over the dispatches of each kernel, and the shares
 of SQ_WAVE_CYCLES spent parked (SQ_WAIT_ANY: s_waitcnt / barrier), issue-stalled
 (SQ_WAIT_INST_ANY) and issuing (SQ_ACTIVE_INST_ANY), MI355X_MICROARCH.md §PMC.
 
@@ -11,7 +11,8 @@ import re
 import sys
 
 SHORT = [("k_transform_fast", "K1 transform"), ("k_transform_fallback", "K1b fallback"), ("k_emit", "K2 emit"),
-         ("k_rowindex", "K5 row index"), ("k_inverse_rows", "K6r inverse"), ("k_rmse", "K7 rmse")]
+         ("k_rowindex", "K5 row index"), ("k_pair_counts", "K5p header check"), ("k_inverse_rows", "K6r inverse"),
+         ("k_rmse", "K7 rmse")]
 
 
 def short(name: str) -> str:
