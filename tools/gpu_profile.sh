@@ -11,6 +11,8 @@
 # (row index kernel + K6r), c3 wc_forward_rows + wc_inverse_rows with the fused
 # RMSE (the bench's C3 round-trip leg: no row index kernel).
 # usage: tools/gpu_profile.sh [workload ...]   (default: c2 c3 c5 f32_64 c4)
+#   send as: gpurun -- "WC_GIT=$(git rev-parse --short HEAD) tools/gpu_profile.sh" (the box's
+#   copy has no .git; the summaries record that commit)
 set -o pipefail
 # c4: the C3 layout with 80 units per box (10 timesteps x 8 components), forward only
 declare -A ARGS=([c2]="1024 64 f64 0.999" [c3]="4 c3 f64 0.999" [c5]="512 128 f32 0.9999" [f32_64]="1024 64 f32 0.999" [c4]="80 c3 f64 0.999")

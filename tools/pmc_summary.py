@@ -13,6 +13,7 @@ import argparse
 import csv
 import datetime
 import json
+import os
 import subprocess
 import sys
 from collections import defaultdict
@@ -66,7 +67,9 @@ def main():
             if st:
                 kern[st] = {"name": row["Name"][:80], "calls": int(row["Calls"]),
                             "avg_us": float(row["AverageNs"]) / 1e3, "pct": float(row["Percentage"])}
-    git = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True, cwd=ROOT).stdout.strip()
+    # the GPU box's copy has no .git: the sender passes the commit as WC_GIT
+    git = os.environ.get("WC_GIT") or subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True,
+                                                     text=True, cwd=ROOT).stdout.strip()
     out = {"config": {"workload": a.workload, "dtype": a.dtype}, "date": datetime.date.today().isoformat(),
            "git": git, "kernel_sources_sha": kernel_sources_sha(), "kernels": kern}
     per, step = {}, {}
