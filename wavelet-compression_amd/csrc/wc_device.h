@@ -128,6 +128,7 @@ __device__ __forceinline__ unsigned long long wave_max_u64_u(unsigned long long 
 // NT: non-temporal (streaming) vector load: the cells are read exactly once.
 using f64x2 = double __attribute__((ext_vector_type(2)));
 using f32x2 = float __attribute__((ext_vector_type(2)));
+using f32x4 = float __attribute__((ext_vector_type(4)));
 
 template <typename T, bool NT = false>
 __device__ __forceinline__ void load_xpair(const T* __restrict__ p, bool two, bool vec,

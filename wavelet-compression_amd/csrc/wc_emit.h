@@ -17,6 +17,11 @@
 #ifndef WC_EMIT_KEYPAR
 #define WC_EMIT_KEYPAR 1  // the unit key loads beside the flags (bit 0: 4-wave launch, bit 1: 8-wave: +11 VGPRs there)
 #endif
+#ifndef WC_EMIT_NTLOAD
+// staged coefficients read with nontemporal loads (their last use): emit -8 % at C2, -11 % at C3
+// (profiles/r05/experiments/gpu_nt.txt; nontemporal payload stores measured +7 %: not used)
+#define WC_EMIT_NTLOAD 1
+#endif
 
 namespace wc {
 
@@ -207,7 +212,14 @@ constexpr unsigned long long kMask31 = 0x7fffffffull;
 // by EARLIER launches (K1), read with plain (and scalar) loads.
 struct PlainTile {
     const float4* __restrict__ p;
-    __device__ __forceinline__ float4 operator[](int i) const { return p[i]; }
+    __device__ __forceinline__ float4 operator[](int i) const {
+        if constexpr (WC_EMIT_NTLOAD) {  // the staged coefficients' last use
+            const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + i));
+            return make_float4(x.x, x.y, x.z, x.w);
+        } else {
+            return p[i];
+        }
+    }
 };
 struct PlainSrc {
     const float* __restrict__ coef;

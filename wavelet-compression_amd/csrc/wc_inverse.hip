@@ -596,6 +596,11 @@ __global__ __launch_bounds__(kThreads) void k_inverse_fast(const float* __restri
 #ifndef WC_RIX_F4
 #define WC_RIX_F4 1  // x-quad (16-B) stores where the output allows them
 #endif
+#ifndef WC_RIX_NT
+// x-quad output stores nontemporal where no RMSE pass re-reads them: K6r -9 % at C2, -6 % at C3
+// (profiles/r05/experiments/gpu_nt.txt; nontemporal pair loads measured slower: not used)
+#define WC_RIX_NT 1
+#endif
 constexpr int kRixRounds = WC_RIX_ROUNDS;
   // rounds of 64 pairs prefetched per wave
 
@@ -921,8 +926,14 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
 #pragma unroll
                             for (int dy = 0; dy < 2; ++dy) {
                                 float* p = dst + lo + 2 * bxl + sy * (2 * by + dy) + sz * (2 * (bzb + qb) + dz);
-                                *reinterpret_cast<float4*>(p) =
-                                    make_float4(V[0][dz][dy][0], V[0][dz][dy][1], V[1][dz][dy][0], V[1][dz][dy][1]);
+                                if constexpr (WC_RIX_NT && OT <= 1) {  // OT 2, 3 re-read the output from L2
+                                    const f32x4 x = {V[0][dz][dy][0], V[0][dz][dy][1], V[1][dz][dy][0],
+                                                     V[1][dz][dy][1]};
+                                    __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p));
+                                } else {
+                                    *reinterpret_cast<float4*>(p) = make_float4(V[0][dz][dy][0], V[0][dz][dy][1],
+                                                                                V[1][dz][dy][0], V[1][dz][dy][1]);
+                                }
                             }
                         if constexpr (OT == 1 && WC_RIX_RMSE_INLINE) {
                             if (qb == 0)  // the second z-block pair's originals, in flight during this one's sums

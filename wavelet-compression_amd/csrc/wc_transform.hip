@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
             const unsigned long long kmax =
                 s32 ? xform_fast_p2_sparse_s32(U, td, lds, threadIdx.x, bound, mag >> 1, flags, dst)
                     : xform_fast_p2_sparse(U, td, lds, threadIdx.x, bound, mag >> 1, flags,
-                                           [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
+                                           [&](int64_t f, float4 v) { stage_store4(dst + f, v); });
             block_key_max(kmax, s_key, unit_key + td.unit);
             return;
         }
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
     unsigned long long kmax;
     if ((obase & 3) == 0) {
         kmax = xform_fast_p2<KEYS>(U, td, lds, threadIdx.x,
-                                   [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
+                                   [&](int64_t f, float4 v) { stage_store4(dst + f, v); });
     } else {
         kmax = xform_fast_p2<KEYS>(U, td, lds, threadIdx.x, [&](int64_t f, float4 v) {
             dst[f] = v.x;
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kThreads) void k_transform_fallback(const T* __rest
                 xform_fast_p1<T>(cells + U.cell_off, U, td, lds, tid);
                 __syncthreads();
                 (void)xform_fast_p2<false>(U, td, lds, tid,
-                                           [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
+                                           [&](int64_t f, float4 v) { stage_store4(dst + f, v); });
                 __syncthreads();
             }
         }
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast_pf(
         unsigned long long kmax;
         if ((obase & 3) == 0) {
             kmax = xform_fast_p2<KEYS>(U, td[cb], lds, tid,
-                                       [&](int64_t f, float4 v) { *reinterpret_cast<float4*>(dst + f) = v; });
+                                       [&](int64_t f, float4 v) { stage_store4(dst + f, v); });
         } else {
             kmax = xform_fast_p2<KEYS>(U, td[cb], lds, tid, [&](int64_t f, float4 v) {
                 dst[f] = v.x;

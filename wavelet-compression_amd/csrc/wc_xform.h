@@ -408,6 +408,19 @@ __device__ __forceinline__ double sparse_bound(uint32_t magkey, double keep) {
 #ifndef WC_K1_IDX32
 #define WC_K1_IDX32 1  // S32 phase 2: 32-bit flat indices with uniform per-row steps
 #endif
+#ifndef WC_K1_NT_STAGE
+// staged coefficients written with nontemporal stores: K1 -2 % at C2, -4 % at C5
+// (profiles/r05/experiments/gpu_nt.txt)
+#define WC_K1_NT_STAGE 1
+#endif
+__device__ __forceinline__ void stage_store4(float* __restrict__ p, const float4& v) {
+    if constexpr (WC_K1_NT_STAGE) {
+        const f32x4 x = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p));
+    } else {
+        *reinterpret_cast<float4*>(p) = v;
+    }
+}
 __device__ __forceinline__ uint32_t key_lo_max(uint32_t best, float c, uint32_t f, uint32_t amax) {
     const uint32_t bits = __float_as_uint(c);
     const uint32_t lo = ((0x7fffffffu - f) << 1) | (bits >> 31);
@@ -522,7 +535,7 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse_s32(const Uni
         const bool flag = ((__ballot(cand) >> g0) & 0xffull) != 0 || dense;
 #if WC_K1_IDX32
         const uint32_t f0 = fb + ((it & 1) ? dA : 0u) + (((it >> 1) & 1) ? dB : 0u) + ((it >> 2) ? dC : 0u);
-        if (flag) *reinterpret_cast<float4*>(dstb + (f0 << 2)) = v;
+        if (flag) stage_store4(reinterpret_cast<float*>(dstb + (f0 << 2)), v);
         if ((tid & 7) == 0) fl[flag_pos32(f0 >> lbz, lbz)] = flag ? 1 : 0;
 #else
         const int bxl = row & 31, ssx = (row >> 5) & 1, ssy = row >> 6;
