@@ -344,6 +344,40 @@ def test_rmse(wc, ctx, oracle):
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("shift", [(0, 0), (1, 0), (0, 1), (1, 1)])
+def test_rmse_base_alignment(wc, ctx, oracle, dtype, shift):
+    """wc_rmse (K7) with the originals and / or the reconstruction one element
+    past a pair-aligned base: the pair-vector loads run only where both bases
+    allow them, the scalar loop otherwise; every RMSE within 1e-12 of the oracle
+    (odd-length units included: the vector path's tail cell)."""
+    import torch
+    dims = DIMS
+    boxes = synth(oracle, dims, seed0=41)
+    units, n, extent, cells = pack(wc, boxes, dtype)
+    payload, offs, kept = ctx.forward_host(cells, units, n, KEEPS[1])
+    regen = ctx.inverse_host(payload, offs[:n], units, n, extent)
+    dev = torch.device("cuda", 0)
+    sa, sr = shift
+    d_a = torch.from_numpy(np.concatenate([np.zeros(1, cells.dtype), cells])).to(dev)[1:] if sa \
+        else torch.from_numpy(cells).to(dev)
+    d_r = torch.from_numpy(np.concatenate([np.zeros(1, np.float32), regen])).to(dev)[1:] if sr \
+        else torch.from_numpy(regen).to(dev)
+    assert (d_a.data_ptr() % (2 * cells.itemsize) != 0) == bool(sa)
+    assert (d_r.data_ptr() % 8 != 0) == bool(sr)
+    d_out = torch.zeros(n, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    code = wc.capi.WC_F64 if dtype == np.float64 else wc.capi.WC_F32
+    ctx.rmse(d_a.data_ptr(), code, d_r.data_ptr(), units, n, d_out.data_ptr())
+    ctx.synchronize()
+    got = d_out.cpu().numpy()
+    for i, b in enumerate(boxes):
+        o = units[i].cell_offset
+        orig = oracle.narrow(b) if dtype == np.float64 else b.astype(np.float32)
+        want = oracle.rmse(orig, regen[o:o + b.size].reshape(b.shape))
+        assert got[i] == pytest.approx(want, rel=1e-12, abs=1e-300), (dims[i], shift)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("which", ["rows", "mixed"])
 def test_inverse_rmse_fused(wc, ctx, oracle, dtype, which):
     """wc_inverse_rmse: the reconstruction byte-equal to wc_inverse's and the

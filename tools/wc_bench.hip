@@ -135,7 +135,7 @@ int main(int argc, char** argv) {
     const int steps = argc > 5 ? std::atoi(argv[5]) : 10;
     const int warmup = argc > 6 ? std::atoi(argv[6]) : 2;
     // 1 wc_inverse, 2 wc_inverse_rmse (fused calc_rmse_per_box), 3 the round trip with the forward's row
-    // index (wc_forward_rows + wc_inverse_rows with the RMSE)
+    // index (wc_forward_rows + wc_inverse_rows with the RMSE), 7 wc_inverse + wc_rmse (the separate calls)
     const int inv_mode = argc > 7 ? std::atoi(argv[7]) : 0;
     const bool inverse = inv_mode != 0;
     const bool check = argc > 8 ? std::atoi(argv[8]) != 0 : false;
@@ -257,6 +257,14 @@ int main(int argc, char** argv) {
         if (touch && std::strcmp(touch, "rows") == 0 && rowinfo)
             CK(hipMemcpyAsync(tbuf, rowinfo, rowinfo_bytes, hipMemcpyDeviceToDevice, tstream));
         if (inv_mode == 5 && wc_inverse(ctx, payload, offsets, units.data(), boxes, regen) != WC_OK) std::exit(2);
+        if (inv_mode == 7) {
+            if (wc_inverse(ctx, payload, offsets, units.data(), boxes, regen) != WC_OK ||
+                wc_rmse(ctx, cells, f64 ? WC_F64 : WC_F32, regen, units.data(), boxes, rmse) != WC_OK) {
+                std::fprintf(stderr, "wc_inverse + wc_rmse: %s\n", wc_last_error(ctx));
+                std::exit(2);
+            }
+            return;
+        }
         int rc = inv_mode == 3   ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, rowinfo, rowinfo_bytes, cells,
                                                    f64 ? WC_F64 : WC_F32, regen, rmse)
                  : inv_mode == 4 ? wc_inverse_rows(ctx, payload, offsets, units.data(), boxes, nullptr, 0, cells,

@@ -1067,10 +1067,27 @@ __global__ __launch_bounds__(kThreads) void k_rmse_partial(const T* __restrict__
     const T* a = orig + U.cell_off + start;
     const float* b = regen + U.cell_off + start;
     double s = 0.0;
-    for (int i = threadIdx.x; i < len; i += kThreads) {
-        const float d = (float)a[i] - b[i];  // float - float, then widened
-        const double dd = d;
-        s += dd * dd;
+    // uniform: cell pairs, one vector load each (read once: nontemporal), where both are pair-aligned
+    if ((reinterpret_cast<uintptr_t>(a) % (2 * sizeof(T))) == 0 && (reinterpret_cast<uintptr_t>(b) & 7u) == 0) {
+        const int n2 = (int)(len >> 1);
+        for (int i = threadIdx.x; i < n2; i += kThreads) {
+            float o0, o1;
+            load_xpair<T, true>(a + 2 * i, true, true, o0, o1);
+            const f32x2 r = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(b + 2 * i));
+            const float d0 = o0 - r.x, d1 = o1 - r.y;  // float - float, then widened
+            s += (double)d0 * (double)d0;
+            s += (double)d1 * (double)d1;
+        }
+        if ((len & 1) && threadIdx.x == 0) {
+            const float d = (float)a[len - 1] - b[len - 1];
+            s += (double)d * (double)d;
+        }
+    } else {
+        for (int i = threadIdx.x; i < len; i += kThreads) {
+            const float d = (float)a[i] - b[i];
+            const double dd = d;
+            s += dd * dd;
+        }
     }
     s = wave_sum(s);
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = s;
