@@ -82,6 +82,11 @@ __device__ __forceinline__ uint32_t wave_incl_sum32_sat(uint32_t v) {
 #ifndef WC_RIX_MINB
 #define WC_RIX_MINB 8  // waves per SIMD the register budget is sized for (4-wave blocks: 8 per CU, <= 64 VGPRs)
 #endif
+#ifndef WC_RIX_RUNS_NT
+// the row index's run loads nontemporal: K5 -12 % at C2, K6r after it +1 %, C5 even
+// (profiles/r05/experiments/gpu_nt.txt)
+#define WC_RIX_RUNS_NT 1
+#endif
 __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDev* __restrict__ units,
                                                      const FTile* __restrict__ tiles, uint32_t* __restrict__ ticket,
                                                      const uint8_t* __restrict__ payload,
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDe
 #pragma unroll
         for (int r = 0; r < kRixRounds5; ++r) {
             const uint32_t k = kw + r * 64 + l;
-            v[r] = k < n ? runs[2 * k] : 0u;
+            v[r] = k < n ? (WC_RIX_RUNS_NT ? __builtin_nontemporal_load(runs + 2 * k) : runs[2 * k]) : 0u;
         }
     }
     if (!hok && t == 0 && tid == 0) atomicOr(err, kErrHeader);
