@@ -81,6 +81,10 @@ def parse(argv=None):
                     help="test hook (--plumbing only): this rank raises before its first collective")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU/gloo run of the launcher, sharding and reductions (no kernels, no numbers)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="take the process-group path even at one rank (RCCL at world 1 on a one-GPU box: "
+                         "init, barriers, metric reductions, all_gather_object and the histogram all-reduce "
+                         "run over the real backend)")
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank rehearsal on a one-GPU box: every rank on device 0, gloo instead of RCCL "
                          "(the kernels, shards and reductions of --gpus N; the numbers are not a scaling result)")
@@ -133,7 +137,7 @@ def alg_bytes_inverse(cells, kept, nunits):
 class Dist:
     """The rank's view of the job: world, rank, device, barrier, reductions."""
 
-    def __init__(self, plumbing: bool, rehearse: bool = False, timeout_s: float = 120.0):
+    def __init__(self, plumbing: bool, rehearse: bool = False, timeout_s: float = 120.0, force: bool = False):
         import datetime
 
         import torch
@@ -142,6 +146,9 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.plumbing = plumbing
+        # collectives run whenever there is a process group: world > 1, or
+        # --force-dist at world 1 (the backend exercised on a one-GPU box)
+        self.distributed = self.world > 1 or force
         self.coll_dev = None  # device of the reduction tensors (None: self.dev)
         # bounded setup and collectives: a rank that died before a collective
         # makes the others fail after this long (torch.distributed.run also
@@ -149,40 +156,42 @@ class Dist:
         tmo = datetime.timedelta(seconds=timeout_s)
         if plumbing:
             self.dev = torch.device("cpu")
-            if self.world > 1:
+            if self.distributed:
                 dist.init_process_group("gloo", timeout=tmo)
         elif rehearse:
-            if self.world > 1:
+            if self.distributed:
                 dist.init_process_group("gloo", timeout=tmo)
             torch.cuda.set_device(0)
             self.dev = torch.device("cuda", 0)
             self.local = 0
             self.coll_dev = torch.device("cpu")
         else:
-            if self.world > 1:
+            if self.distributed:
                 dist.init_process_group("nccl", device_id=torch.device("cuda", self.local), timeout=tmo)
             torch.cuda.set_device(self.local)
             self.dev = torch.device("cuda", self.local)
 
     def backend(self):
+        if not self.distributed:
+            return None
         import torch.distributed as dist
         b = dist.get_backend()
         return "RCCL over xGMI" if b == "nccl" else b
 
     def barrier(self):
-        if self.world > 1:
+        if self.distributed:
             import torch.distributed as dist
             dist.barrier()
 
     def reduce(self, metrics):
-        if self.world == 1:
+        if not self.distributed:
             return dict(metrics)
         from wavelet_compression_amd.shard import reduce_metrics
         return reduce_metrics(metrics, device=self.coll_dev or self.dev)
 
     def gather(self, obj):
         """Every rank's `obj` (a small JSON-able value), in rank order."""
-        if self.world == 1:
+        if not self.distributed:
             return [obj]
         import torch.distributed as dist
         out = [None] * self.world
@@ -190,7 +199,7 @@ class Dist:
         return out
 
     def close(self):
-        if self.world > 1:
+        if self.distributed:
             import torch.distributed as dist
             dist.destroy_process_group()
 
@@ -404,6 +413,7 @@ def headline(args, d: Dist, ctx):
         "vs_baseline": None,
         "dtype": spec["dtype"],
         "data": "synthetic (SURVEY §8(d) field + N(0,0.05) noise, generated on device; bench_workloads.py)",
+        "dist_backend": d.backend(),
         "config": {"workload": f"{args.workload}: {spec['desc']}, wc_forward (payload bytes identical to the "
                                f"reference's serialize())",
                    "boxes_per_gpu": b.n, "global_batch": int(m["boxes"]),
@@ -634,7 +644,7 @@ def global_hist_leg(args, d: Dist, ctx, b: Batch):
             "quantile": args.hist_quantile, "threshold": res["thresh"], "retained": res["retained"],
             "kept_check": int(m["kept"]) == res["retained"], "kept_fraction": m["kept"] / m["cells"],
             "value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
-            "allreduce": f"{b.capi.HIST_BINS} x u64 over {d.world} rank(s)" + (f" ({d.backend()})" if d.world > 1 else " (none)")}
+            "allreduce": f"{b.capi.HIST_BINS} x u64 over {d.world} rank(s) ({d.backend() or 'none'})"}
 
 
 def link_ms(up: int, down: int) -> float:
@@ -882,9 +892,9 @@ def main():
     args = parse()
     import wcamd  # noqa: F401  (registers the package as wavelet_compression_amd; no GPU call)
     args.legs_set = set() if args.legs in ("none", "") else set(args.legs.split(","))
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if (args.gpus > 1 or args.force_dist) and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
-    d = Dist(args.plumbing, args.rehearse, args.dist_timeout)
+    d = Dist(args.plumbing, args.rehearse, args.dist_timeout, args.force_dist)
     if args.plumbing:
         if d.rank == args.fail_rank:
             raise RuntimeError(f"rank {d.rank}: injected failure before the first collective (--fail-rank)")

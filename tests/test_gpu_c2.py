@@ -8,7 +8,7 @@ ONE wc_forward, then ONE wc_inverse_rmse of the payloads:
   * every unit's reconstruction equals the oracle's decompress() minus xz
     (rle_decode + inverse_wavelet_decompose, src/decompressor.cpp:14-159) bit
     for bit, and its RMSE is within 1e-12 of calc_rmse_per_box on it
-    (src/compressor.cpp:330-353 via the oracle).
+    (src/calc-loss.cpp:12-43 via the oracle).
 The oracle runs on a thread pool (ctypes releases the GIL), so the whole batch
 is checked in seconds.
 """

@@ -16,5 +16,5 @@ fi
 $L/llvm-objcopy --dump-section=.hip_fatbin=$t/f $o
 $L/clang-offload-bundler --type=o --unbundle --input=$t/f --output=$t/co --targets=hipv4-amdgcn-amd-amdhsa--gfx950
 $L/llvm-readelf --notes $t/co | grep -E "^\s+\.(name|vgpr_count|vgpr_spill_count|private_segment_fixed_size|sgpr_count):" | \
-  paste - - - - - | grep -E "$filt" | awk '{print $2, "priv", $4, "vgpr", $8, "spill", $10}' | c++filt | cut -c1-60,150-
+  paste - - - - - | grep -E "$filt" | awk '{print $2, "priv", $4, "vgpr", $8, "spill", $10}' | c++filt | sed -E "s/\(.*\)/()/"
 rm -rf $t
