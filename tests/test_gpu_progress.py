@@ -11,6 +11,8 @@ other kernels sharing the device:
   order, so each block waits on blocks dispatched after it, on a grid larger
   than the device holds at once (the form that hangs without the derivation):
   payloads and reconstructions equal the oracle's, no error.
+  A derived tile is published for the waves after it: large units in the
+  reversed order finish within a bound (no O(tiles^2) re-derivation).
 * WC_OPT_SPIN_LIMIT 1: nearly every wait takes the derivation: the same bytes.
 * Two contexts, and two processes, run their launch-order kernels on one GPU
   at the same time: the oracle's bytes, in time.
@@ -115,6 +117,53 @@ def test_reversed_tiles_worst_dispatch_order(wc, ctx, oracle, batches):
             assert time.perf_counter() - t0 < 60
     finally:
         ctx.set_option(WC_OPT_REVERSE_TILES, 0)
+
+
+def test_reversed_tiles_large_units_bounded(wc, ctx, oracle):
+    """a wave that derives an unpublished predecessor publishes it
+    (publish_derived) and restarts its wait bound on progress, so waves after
+    it reuse the derivation.  Units of 2^24 cells (1024 emit tiles of 16384,
+    ~1800 row-index tiles each) and odd 255 x 256 x 256 units (dense decode)
+    in the reversed order: the same bytes as the normal order, the oracle's on
+    one unit of each shape, within a time bound."""
+    import torch
+    import bench_workloads as bw
+    units = [bw.Unit(0, 0, i, 0, 256, 256, 256, (256 * i, 0, 0), 900 + i) for i in range(4)]
+    units += [bw.Unit(0, 0, 4 + i, 0, 255, 256, 256, (256 * i, 256, 0), 904 + i) for i in range(2)]
+    dev = torch.device("cuda", 0)
+    cells, offs, extent = bw.synth_cells(torch, dev, units, "f32")
+    tab, n, _ = bw.units_array(wc.capi, units, offs)
+    cap = wc.capi.payload_bound(tab, n)
+    runs = {}
+    for rev in (0, 1):
+        pay = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        po = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        kept = torch.zeros(n, dtype=torch.int32, device=dev)
+        out = torch.zeros(extent, dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()
+        ctx.set_option(WC_OPT_REVERSE_TILES, rev)
+        try:
+            t0 = time.perf_counter()
+            ctx.forward(cells.data_ptr(), wc.capi.WC_F32, tab, n, KEEP, pay.data_ptr(), cap, po.data_ptr(),
+                        kept.data_ptr())
+            ctx.inverse(pay.data_ptr(), po.data_ptr(), tab, n, out.data_ptr())
+            ctx.synchronize()
+            took = time.perf_counter() - t0
+        finally:
+            ctx.set_option(WC_OPT_REVERSE_TILES, 0)
+        runs[rev] = (pay, po.cpu().numpy(), kept.cpu().numpy(), out, took)
+    (p0, o0, k0, x0, t_norm), (p1, o1, k1, x1, t_rev) = runs[0], runs[1]
+    print(f"normal order {t_norm:.3f} s, reversed {t_rev:.3f} s")
+    assert np.array_equal(o0, o1) and np.array_equal(k0, k1)
+    assert torch.equal(p0, p1) and torch.equal(x0, x1)
+    assert t_rev < 20.0, t_rev
+    for i in (0, 4):
+        u = units[i]
+        box = cells[offs[i]:offs[i] + u.cells].cpu().numpy().reshape(u.D, u.H, u.W)
+        want, wk = oracle.compress_payload(box, KEEP)
+        got = p1[int(o1[i]):int(o1[i]) + 20 + 8 * int(k1[i])].cpu().numpy().tobytes()
+        assert got == want and int(k1[i]) == wk, i
+        assert x1[offs[i]:offs[i] + u.cells].cpu().numpy().tobytes() == oracle.decompress_payload(want).tobytes()
 
 
 @pytest.mark.parametrize("tickets", [0, 1])

@@ -239,6 +239,17 @@ __device__ __forceinline__ void add_rlx(uint32_t* p, uint32_t v) {
     __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A look-back wave that derived an unpublished predecessor's aggregate
+// publishes it for the waves after it (one lane): swapped in only while the
+// granule still holds `seen`, the unpublished value that lane polled.  The
+// tile's own block, or another wave that derived it too, may have published
+// meanwhile: the same aggregate, or the inclusive prefix, which is kept.
+__device__ __forceinline__ void publish_derived(unsigned long long* p, unsigned long long seen,
+                                                unsigned long long v) {
+    __hip_atomic_compare_exchange_strong(p, &seen, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Look-back waits with backoff: pollers share the memory system with the
 // streaming loads (MI355X_MICROARCH.md: 255 pollers cut chip bandwidth
 // 37-71 %), so re-polls slow down from ~0.2 us to ~1.7 us.  A wait is never
@@ -248,7 +259,12 @@ __device__ __forceinline__ void add_rlx(uint32_t* p, uint32_t v) {
 // inputs (which an earlier launch wrote) and moves on.  So no wait depends on
 // which workgroups the hardware has dispatched, in any order, beside any other
 // kernel (DESIGN.md §Forward progress).  err[1] is read only by a wave that is
-// already waiting.
+// already waiting.  The derived aggregate is published into the predecessor's
+// granule (publish_derived), so waves after it reuse it instead of deriving
+// the same tile again, and a wave's poll count restarts whenever a poll makes
+// progress: each unpublished tile costs one bounded wait and one derivation,
+// not one per waiting wave (no O(tiles^2) work when a share of a launch's
+// workgroups is held back, e.g. by another process on one XCD).
 #ifndef WC_SPIN_S0
 #define WC_SPIN_S0 8  // s_sleep units (64 clocks) before re-polls 1-3
 #endif
@@ -275,9 +291,10 @@ __device__ __forceinline__ bool spin_wait(uint32_t& spins, const uint32_t* err) 
 // of published aggregates before the first unpublished tile is summed and
 // the window slides past it.  A predecessor still unpublished after the wait
 // bound is summed from agg(tile) (a wave-uniform call by the whole wave: the
-// tile's aggregate derived from its inputs, as its own block would publish it).
+// tile's aggregate derived from its inputs, as its own block would publish it),
+// and published there as an aggregate granule.
 template <class Agg>
-__device__ __forceinline__ unsigned long long lookback_sum62(const unsigned long long* st, int64_t t, int l,
+__device__ __forceinline__ unsigned long long lookback_sum62(unsigned long long* st, int64_t t, int l,
                                                              const uint32_t* err, Agg agg) {
     unsigned long long excl = 0;
     int64_t pos = t - 1;
@@ -289,10 +306,18 @@ __device__ __forceinline__ unsigned long long lookback_sum62(const unsigned long
         const int kI = incl ? __ffsll((long long)incl) - 1 : 64;
         const int kZ = zero ? __ffsll((long long)zero) - 1 : 64;
         const int take = kI < kZ ? kI + 1 : kZ;  // lanes [0, take) are summed
-        if (take > 0) excl += wave_sum(l < take ? (v & kMask62) : 0ull);
+        if (take > 0) {
+            excl += wave_sum(l < take ? (v & kMask62) : 0ull);
+            spins = 0;  // progress: a later unpublished tile gets a full wait
+        }
         if (kI < kZ) break;
         pos -= take;
-        if (take == 0 && spin_wait(spins, err)) excl += agg(pos--) & kMask62;  // tile pos: derived here
+        if (take == 0 && spin_wait(spins, err)) {  // tile pos (lane 0's): derived here
+            const unsigned long long a = agg(pos) & kMask62;
+            if (l == 0) publish_derived(st + pos, v, kFlagAgg | a);
+            excl += a;
+            --pos;
+        }
     }
     return excl & kMask62;
 }
@@ -307,24 +332,32 @@ __device__ __forceinline__ unsigned long long granule_e(unsigned long long flag,
 // lookback_sum62 over epoch-tagged granules; the result saturates at 2^32 - 1
 // (agg: a tile's saturated 32-bit sum).
 template <class Agg>
-__device__ __forceinline__ uint32_t lookback_sum32e(const unsigned long long* st, int64_t t, int l,
+__device__ __forceinline__ uint32_t lookback_sum32e(unsigned long long* st, int64_t t, int l,
                                                     const uint32_t* err, uint32_t epoch, Agg agg) {
     unsigned long long excl = 0;
     int64_t pos = t - 1;
     const uint32_t ep = epoch & kEpochMask;
     for (uint32_t spins = 0;;) {
         const int64_t idx = pos - l;
-        unsigned long long v = idx >= 0 ? ld_rlx(st + idx) : granule_e(kFlagIncl, ep, 0u);
-        if ((uint32_t)(v >> 32 & kEpochMask) != ep) v = 0;  // an earlier call's granule: unpublished
+        const unsigned long long raw = idx >= 0 ? ld_rlx(st + idx) : granule_e(kFlagIncl, ep, 0u);
+        const unsigned long long v = (uint32_t)(raw >> 32 & kEpochMask) != ep ? 0ull : raw;  // earlier call's: unpublished
         const unsigned long long incl = __ballot((v >> 62) == 2);
         const unsigned long long zero = __ballot((v >> 62) == 0);
         const int kI = incl ? __ffsll((long long)incl) - 1 : 64;
         const int kZ = zero ? __ffsll((long long)zero) - 1 : 64;
         const int take = kI < kZ ? kI + 1 : kZ;  // lanes [0, take) are summed
-        if (take > 0) excl += wave_sum(l < take ? (v & 0xffffffffull) : 0ull);
+        if (take > 0) {
+            excl += wave_sum(l < take ? (v & 0xffffffffull) : 0ull);
+            spins = 0;
+        }
         if (kI < kZ) break;
         pos -= take;
-        if (take == 0 && spin_wait(spins, err)) excl += agg(pos--);  // tile pos: derived here
+        if (take == 0 && spin_wait(spins, err)) {  // tile pos (lane 0's): derived here, published
+            const uint32_t a = agg(pos);
+            if (l == 0) publish_derived(st + pos, raw, granule_e(kFlagAgg, ep, a));
+            excl += a;
+            --pos;
+        }
     }
     return excl > 0xffffffffull ? 0xffffffffu : (uint32_t)excl;
 }
@@ -443,6 +476,30 @@ __device__ __forceinline__ void block_key_max(unsigned long long v, unsigned lon
         for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = s[i] > m ? s[i] : m;
         if (m != 0) atomicMax(dst, m);
     }
+}
+
+// Coefficient-magnitude histogram of the opt-in global-threshold mode
+// (wc_hist.hip, k_transform_hist): bin = fp32 bits of |c| >> kHistShift,
+// NaN not counted.  Wave-aggregated LDS increment: the coefficients of a tile
+// crowd into a few bins, and same-address LDS atomics of one wave serialize,
+// so one round takes the bin of the first pending lane, counts every lane
+// with that bin by ballot and adds the count with ONE atomic; lanes still
+// pending add their own.
+constexpr int kHistBins = 4096;
+constexpr int kHistShift = 19;
+
+__device__ __forceinline__ void hist_add(uint32_t* h, float v, bool valid) {
+    const uint32_t m = __float_as_uint(v) & 0x7fffffffu;
+    const uint32_t bin = m >> kHistShift;
+    bool pending = valid && m <= 0x7f800000u;  // NaN is not counted
+    const unsigned long long act = __ballot(pending);
+    if (!act) return;
+    const int leader = __ffsll((long long)act) - 1;
+    const uint32_t lb = __builtin_amdgcn_readlane(bin, leader);
+    const unsigned long long same = __ballot(pending && bin == lb);
+    if ((int)(threadIdx.x & 63) == leader) atomicAdd(h + lb, (uint32_t)__popcll(same));
+    pending = pending && bin != lb;
+    if (pending) atomicAdd(h + bin, 1u);
 }
 
 }  // namespace wc

@@ -247,7 +247,7 @@ __device__ __forceinline__ uint2 emit_tile_agg(const uint8_t* __restrict__ flags
     const float* __restrict__ ct = c + s0;
     uint32_t C = 0, L = 0;
 #pragma unroll 1
-    for (uint32_t e0 = 0; e0 < kTile; e0 += 64) {
+    for (uint32_t e0 = 0; e0 < kTile; e0 += 64) {  // one load per step: the 4-wave emit has no VGPR to spare
         // a sparse unit's flag of this lane's segment (unflagged: never staged, counts as 0)
         bool on = true;
         if (!dense) on = flags[flag_off + flag_pos32((s0 + e0 + (uint32_t)l) >> sh, sh)] != 0;
@@ -375,7 +375,9 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
             // before the unit read as an inclusive 0).  Lanes up to the nearest
             // inclusive one are summed once every one of them has published;
             // a run of published aggregates before the first unpublished tile
-            // is summed and the window slides past it.
+            // is summed and the window slides past it.  A tile still
+            // unpublished after the wait bound is derived here and published
+            // (publish_derived, wc_device.h), and any progress restarts the bound.
             for (uint32_t spins = 0;;) {
                 const int32_t idx = pos - l;
                 const unsigned long long v = idx >= first ? ld_rlx(P.status + idx) : kFlagIncl;
@@ -391,13 +393,15 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
                     const uint32_t hl = __builtin_amdgcn_readlane((uint32_t)(v & kMask31),
                                                                   hasl ? __ffsll((long long)hasl) - 1 : 0);  // uniform lane
                     if (elast == 0 && hasl) elast = hl;
+                    spins = 0;
                 }
                 if (kI < kZ) break;
                 pos -= take;
-                if (take == 0 && spin_wait(spins, P.err)) {  // tile pos unpublished: derive its aggregate here
+                if (take == 0 && spin_wait(spins, P.err)) {  // tile pos (lane 0's) unpublished: derive it here
                     const uint2 a = emit_tile_agg<EW>(P.flags, src.unit_coef(U), U.flag_off,
                                                       (uint32_t)(pos - first), (int)((U.mode >> 1) & 7u),
                                                       !sparse || !(tf >= 0.0f), tf, l);
+                    if (l == 0) publish_derived(P.status + pos, v, kFlagAgg | ((unsigned long long)a.x << 31) | a.y);
                     ecnt += a.x;
                     if (elast == 0 && a.y) elast = a.y;
                     --pos;
