@@ -66,7 +66,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="time budget of each CPU-baseline sample (boxes run until it is spent)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r05"),
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "r06"),
                     help="PMC traffic summaries (tools/pmc_summary.py): a file or a directory of pmc_*.json, "
                          "one per workload; merged into roofline.traffic and each leg's roofline_path.traffic "
                          "when measured on the same workload AND the same kernel sources")
@@ -333,6 +333,7 @@ def stage_times(ctx, step, steps):
 
 
 FWD_STAGES = ("transform", "fallback", "emit")
+HIST_STAGES = ("transform", "hist", "emit")
 INV_STAGES = ("rowindex", "decode", "inverse", "rmse", "pairs")
 
 
@@ -637,13 +638,24 @@ def global_hist_leg(args, d: Dist, ctx, b: Batch):
         res.update(thresh=t, retained=r)
 
     secs = timed(d, ctx, step, args.leg_steps, 1)
+    st = stage_times(ctx, step, args.leg_steps)
     kept = b.kept_total()
     m = d.reduce({"seconds": secs, "kept": kept, "cells": b.ncells})
     ms = m["seconds"] / args.leg_steps * 1e3
+    # algorithmic bytes: the forward's; the 32 KiB histogram and its all-reduce are noise
+    alg = alg_bytes_forward(b.s_in, b.ncells, kept, b.n)
     return {"mode": "global histogram threshold (opt-in, not the reference rule)",
             "quantile": args.hist_quantile, "threshold": res["thresh"], "retained": res["retained"],
             "kept_check": int(m["kept"]) == res["retained"], "kept_fraction": m["kept"] / m["cells"],
             "value": m["cells"] / (ms * 1e-3), "unit": "cells/s", "ms_per_step": ms,
+            "stage_ms_per_launch": {k: round(v[0], 4) for k, v in st.items()},
+            "roofline_path": {"achieved_per_gpu": alg / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                              "frac": alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, "bytes_per_step": alg,
+                              "note": "forward algorithmic bytes / driver-clock step (stage with the histogram folded "
+                                      "into K1, host threshold, emit)",
+                              **(path_traffic(args.pmc, "c4_hist", "f64" if b.s_in == 8 else "f32", HIST_STAGES, alg)
+                                 if d.world == 1 else {"traffic": None, "traffic_source": {
+                                     "note": "counter summaries are for the one-GPU workload"}})},
             "allreduce": f"{b.capi.HIST_BINS} x u64 over {d.world} rank(s) ({d.backend() or 'none'})"}
 
 

@@ -222,9 +222,26 @@ int main(int argc, char** argv) {
     // context's coefficient staging is one k-unit buffer reused by every call.
     const char* chunk_env = std::getenv("WCB_CHUNK");
     const int chunk = (!c3 && chunk_env) ? std::atoi(chunk_env) : 0;
+    // WCB_HIST=q: the opt-in global-threshold mode at quantile q (bench.py's c4
+    // global_hist leg): wc_forward_stage with the histogram, its threshold on
+    // the host (one rank: no all-reduce), wc_forward_emit with it.
+    const char* hist_env = std::getenv("WCB_HIST");
+    const double hist_q = hist_env ? std::atof(hist_env) : -1.0;
+    uint64_t* d_hist = nullptr;
+    std::vector<uint64_t> h_hist(WC_HIST_BINS);
+    if (hist_q >= 0.0) CK(hipMalloc(&d_hist, 8 * WC_HIST_BINS));
     auto fwd = [&]() {
         int rc = WC_OK;
-        if (chunk > 0 && chunk < boxes && boxes % chunk == 0) {
+        if (hist_q >= 0.0) {
+            float t = 0.0f;
+            CK(hipMemset(d_hist, 0, 8 * WC_HIST_BINS));
+            if ((rc = wc_forward_stage(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, d_hist)) == WC_OK &&
+                (rc = wc_synchronize(ctx)) == WC_OK) {
+                CK(hipMemcpy(h_hist.data(), d_hist, 8 * WC_HIST_BINS, hipMemcpyDeviceToHost));
+                wc_hist_threshold(h_hist.data(), hist_q, &t, nullptr);
+                rc = wc_forward_emit(ctx, units.data(), boxes, keep, &t, payload, cap, offsets, kept);
+            }
+        } else if (chunk > 0 && chunk < boxes && boxes % chunk == 0) {
             const uint64_t per = (uint64_t)dim * dim * dim;
             const uint64_t ccap = wc_payload_bound(units.data(), chunk);
             for (int g = 0; g < boxes / chunk && rc == WC_OK; ++g)
@@ -385,6 +402,7 @@ int main(int argc, char** argv) {
     (void)hipFree(kept);
     if (regen) (void)hipFree(regen);
     if (rmse) (void)hipFree(rmse);
+    if (d_hist) (void)hipFree(d_hist);
     if (rowinfo) (void)hipFree(rowinfo);
     return 0;
 }

@@ -324,14 +324,37 @@ int wc_forward_stage(wc_ctx* c, const void* d_cells, int dtype, const wc_unit* u
     if ((rc = check_aligned(c, d_cells, "cells"))) return rc;
     if ((rc = set_device(c)) || (rc = get_plan(c, units, n))) return rc;
     // dense staging: the histogram and any later threshold need every coefficient
-    if ((rc = ensure_scratch(c)) || (rc = stage_transform(c, d_cells, dtype, 0.0, false))) return rc;
-    if (d_hist) {
+    if ((rc = ensure_scratch(c))) return rc;
+    if (!d_hist) {
+        if ((rc = stage_transform(c, d_cells, dtype, 0.0, false))) return rc;
+        c->staged = true;
+        return WC_OK;
+    }
+    // The fast tiles bin their coefficients as K1 stages them (k_transform_hist:
+    // no re-read of the staged coefficients); the generic ones (odd dims, D % 8
+    // != 0) stage as usual and k_hist bins those units afterwards.
+    Plan& P = c->plan;
+    const UnitDev* du = (const UnitDev*)P.d_units.p;
+    const XTile* dxt = (const XTile*)P.d_xtiles.p;
+    unsigned long long* key = (unsigned long long*)((uint8_t*)c->state.p + 16);
+    float* coef = (float*)c->coef.p;
+    hipError_t e = hipMemsetAsync(c->state.p, 0, P.state_bytes, c->stream);
+    if (e != hipSuccess) return hip_fail(c, e, "memset state");
+    {
+        StageTimer t(c, WC_STAGE_TRANSFORM);
+        e = launch_transform(c->stream, d_cells, dtype, du, dxt, P.ngen, P.lds_gen, coef, 0, key);
+        if (e == hipSuccess)
+            e = launch_transform_hist(c->stream, d_cells, dtype, du, dxt + P.ngen, P.nfast, P.lds_fast, coef, key,
+                                      (unsigned long long*)d_hist,
+                                      persistent_grid(c, 2, transform_hist_lds_bytes(P.lds_fast)));
+        if (e != hipSuccess) return hip_fail(c, e, "transform launch");
+    }
+    c->sparse_staged = false;
+    if (P.ngen) {
         const uint32_t max_blocks = 2048;  // 8 workgroups per CU, 256 CUs
-        const Plan& P = c->plan;
         StageTimer t(c, WC_STAGE_HIST);
-        hipError_t e = launch_hist(c->stream, (const UnitDev*)P.d_units.p, (const FTile*)P.d_ftiles.p,
-                                   (uint32_t)P.ftiles.size(), (const float*)c->coef.p, max_blocks,
-                                   (unsigned long long*)d_hist);
+        e = launch_hist(c->stream, du, (const FTile*)P.d_ftiles.p, (uint32_t)P.ftiles.size(), coef, max_blocks,
+                        (unsigned long long*)d_hist, true);
         if (e != hipSuccess) return hip_fail(c, e, "histogram launch");
     }
     c->staged = true;

@@ -35,6 +35,10 @@ hipError_t launch_transform(hipStream_t, const void*, int, const UnitDev*, const
 hipError_t launch_transform_fast(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
                                  float*, int, unsigned long long*, uint8_t*, uint32_t*, double, uint32_t);
 uint32_t transform_pf_grid(size_t lds);
+size_t transform_hist_lds_bytes(size_t lds_fast);
+uint32_t transform_hist_grid(size_t lds);
+hipError_t launch_transform_hist(hipStream_t, const void*, int, const UnitDev*, const XTile*, uint32_t, size_t,
+                                 float*, unsigned long long*, unsigned long long*, uint32_t);
 uint32_t inverse_rows_grid(size_t lds);
 hipError_t launch_transform_fallback(hipStream_t, const void*, int, const UnitDev*, int, const XTile*, size_t, float*,
                                      const unsigned long long*, const uint32_t*, double);
@@ -52,7 +56,7 @@ hipError_t launch_rmse(hipStream_t, const void*, int, const float*, const UnitDe
                        uint32_t, double*, double*);
 hipError_t launch_emit(hipStream_t, const EmitParams&, const float*, uint32_t, uint32_t);
 hipError_t launch_hist(hipStream_t, const UnitDev*, const FTile*, uint32_t, const float*, uint32_t,
-                       unsigned long long*);
+                       unsigned long long*, bool);
 
 struct DevBuf {
     void* p = nullptr;

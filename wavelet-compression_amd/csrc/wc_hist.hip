@@ -21,52 +21,25 @@
 
 namespace wc {
 
-namespace {
-
-constexpr int kHistBins = 4096;
-constexpr int kHistShift = 19;
 constexpr int kHistThreads = 256;
-
-// Wave-aggregated LDS increment: the coefficients of a box crowd into a few
-// bins (the detail bands of smooth data), and same-address LDS atomics of one
-// wave serialize.  kPeel rounds each take the bin of the first pending
-// lane, count every lane with that bin by ballot and add the count with ONE
-// atomic; lanes still pending after that add their own.
-constexpr int kPeel = 1;
-
-__device__ __forceinline__ void hist_add(uint32_t* h, float v, bool valid) {
-    const uint32_t m = __float_as_uint(v) & 0x7fffffffu;
-    const uint32_t bin = m >> kHistShift;
-    bool pending = valid && m <= 0x7f800000u;  // NaN is not counted
-#pragma unroll
-    for (int r = 0; r < kPeel; ++r) {
-        const unsigned long long act = __ballot(pending);
-        if (!act) return;
-        const int leader = __ffsll((long long)act) - 1;
-        const uint32_t lb = __builtin_amdgcn_readlane(bin, leader);
-        const unsigned long long same = __ballot(pending && bin == lb);
-        if ((int)(threadIdx.x & 63) == leader) atomicAdd(h + lb, (uint32_t)__popcll(same));
-        pending = pending && bin != lb;
-    }
-    if (pending) atomicAdd(h + bin, 1u);
-}
-
-}  // namespace
 
 // Workgroup g folds flat tiles g, g + G, ... (kFlatTile coefficients of one
 // unit each, in the staged flat scratch at coef + coef_off) into its LDS bins,
 // then adds its nonzero bins to hist with 64-bit atomics (integer sums: the
-// result does not depend on their order).
+// result does not depend on their order).  skip_fast: only the units of the
+// generic transform (k_transform_hist has binned the fast units' coefficients
+// while it staged them).
 __global__ __launch_bounds__(kHistThreads) void k_hist(const UnitDev* __restrict__ units,
                                                      const FTile* __restrict__ ftiles, uint32_t nftiles,
                                                      const float* __restrict__ coef,
-                                                     unsigned long long* __restrict__ hist) {
+                                                     unsigned long long* __restrict__ hist, int skip_fast) {
     __shared__ uint32_t h[kHistBins];
     for (int i = threadIdx.x; i < kHistBins; i += kHistThreads) h[i] = 0u;
     __syncthreads();
     for (uint32_t t = blockIdx.x; t < nftiles; t += gridDim.x) {
         const FTile ft = ftiles[t];
         const UnitDev& U = units[ft.unit];
+        if (skip_fast && U.fast) continue;  // uniform
         const uint64_t start = (uint64_t)ft.index * kFlatTile;
         const uint32_t len = (uint32_t)min((uint64_t)kFlatTile, U.ncells - start);
         // coef_off is 16-B aligned and kFlatTile a multiple of 4: float4 loads
@@ -93,10 +66,10 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(const UnitDev* __restrict
 }
 
 hipError_t launch_hist(hipStream_t st, const UnitDev* units, const FTile* ftiles, uint32_t nftiles,
-                       const float* coef, uint32_t max_blocks, unsigned long long* hist) {
+                       const float* coef, uint32_t max_blocks, unsigned long long* hist, bool skip_fast) {
     if (nftiles == 0) return hipSuccess;
     const uint32_t g = nftiles < max_blocks ? nftiles : max_blocks;
-    k_hist<<<g, kHistThreads, 0, st>>>(units, ftiles, nftiles, coef, hist);
+    k_hist<<<g, kHistThreads, 0, st>>>(units, ftiles, nftiles, coef, hist, skip_fast ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -429,12 +429,13 @@ int ensure_scratch(wc_ctx* c) {
 }
 
 // Resident workgroups of a persistent kernel (which: 0 k_transform_fast_pf,
-// 1 k_inverse_rows) for an LDS size, cached per context (one device).
+// 1 k_inverse_rows, 2 k_transform_hist) for an LDS size, cached per context
+// (one device).
 uint32_t persistent_grid(wc_ctx* c, int which, size_t lds) {
     auto key = std::make_pair(which, lds);
     auto it = c->grids.find(key);
     if (it != c->grids.end()) return it->second;
-    const uint32_t g = which == 0 ? transform_pf_grid(lds) : inverse_rows_grid(lds);
+    const uint32_t g = which == 0 ? transform_pf_grid(lds) : which == 1 ? inverse_rows_grid(lds) : transform_hist_grid(lds);
     c->grids[key] = g;
     return g;
 }

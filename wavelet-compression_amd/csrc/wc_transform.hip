@@ -1,7 +1,9 @@
 // wc_transform.hip — K1: one-level 3-D Haar, cells -> flat coefficients.
 //   k_transform       generic tiles (any dims, odd tails)     src/compressor.cpp:85-185
 //   k_transform_fast  even dims, D % 8 == 0 (4 z-blocks per thread)
-// Both also reduce the unit's max-|c| key (src/compressor.cpp:212-215).
+//   k_transform_hist  the fast tiles with the global-threshold mode's
+//                     magnitude histogram folded in (wc_forward_stage)
+// All also reduce the unit's max-|c| key (src/compressor.cpp:212-215).
 // The tile bodies live in wc_xform.h.
 //
 // Numerics (bit-exact with the reference): the reference
@@ -196,6 +198,44 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast_pf(
     }
 }
 
+// The opt-in global-threshold mode's stage (wc_forward_stage with a
+// histogram) over the fast tiles: dense staging, unit keys, AND the
+// coefficient-magnitude histogram (wc_hist.hip's bins) folded into the store
+// of phase 2, where every coefficient is already in registers, so no kernel
+// re-reads the staged coefficients for it (4 B per coefficient saved).
+// Persistent (workgroup b: tiles b, b + G, ...): the workgroup's LDS bins
+// (16 KiB past the tile rows) add up its tiles and reach `hist` once, as one
+// 64-bit atomic per nonzero bin, instead of once per tile.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void k_transform_hist(
+    const T* __restrict__ cells, const UnitDev* __restrict__ units, const XTile* __restrict__ tiles,
+    uint32_t ntiles, uint32_t tile_floats, float* __restrict__ out, unsigned long long* __restrict__ unit_key,
+    unsigned long long* __restrict__ hist) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ unsigned long long s_key[kThreads / kWave];
+    uint32_t* __restrict__ h = reinterpret_cast<uint32_t*>(lds + tile_floats);
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kHistBins; i += kThreads) h[i] = 0u;  // ordered before any add by the barrier after p1
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const XTile td = tiles[t];
+        const UnitDev& U = units[td.unit];
+        xform_fast_p1<T>(cells + U.cell_off, U, td, lds, tid);
+        __syncthreads();
+        float* __restrict__ dst = out + U.coef_off;  // 128-B aligned: 16-B stores
+        const unsigned long long kmax = xform_fast_p2<true>(U, td, lds, tid, [&](int64_t f, float4 v) {
+            stage_store4(dst + f, v);
+            hist_add(h, v.x, true);
+            hist_add(h, v.y, true);
+            hist_add(h, v.z, true);
+            hist_add(h, v.w, true);
+        });
+        block_key_max(kmax, s_key, unit_key + td.unit);  // its barrier: the rows are free for the next tile
+    }
+    __syncthreads();
+    for (int i = tid; i < kHistBins; i += kThreads)
+        if (h[i]) atomicAdd(hist + i, (unsigned long long)h[i]);
+}
+
 // ---------------------------------------------------------------------------
 // Launch wrappers
 size_t transform_lds_bytes(int lbx, int lby, int lbz) {
@@ -239,6 +279,36 @@ uint32_t transform_pf_grid(size_t lds) {
         per_cu = 2;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
     return (uint32_t)per_cu * (uint32_t)ncu;
+}
+
+// Dynamic LDS of k_transform_hist: the tile rows, then the bins.
+size_t transform_hist_lds_bytes(size_t lds_fast) { return ((lds_fast + 15) & ~size_t(15)) + 4 * kHistBins; }
+
+uint32_t transform_hist_grid(size_t lds) {
+    int per_cu = 0, ncu = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_transform_hist<double>, kThreads, lds) !=
+            hipSuccess ||
+        per_cu < 1)
+        per_cu = 2;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+    return (uint32_t)per_cu * (uint32_t)ncu;
+}
+
+hipError_t launch_transform_hist(hipStream_t st, const void* cells, int dtype, const UnitDev* units,
+                                 const XTile* tiles, uint32_t ntiles, size_t lds_fast, float* out,
+                                 unsigned long long* keys, unsigned long long* hist, uint32_t grid) {
+    if (ntiles == 0) return hipSuccess;
+    const size_t lds = transform_hist_lds_bytes(lds_fast);
+    const uint32_t tf = (uint32_t)((lds - 4 * kHistBins) / sizeof(float));
+    const uint32_t g = std::min(ntiles, std::max(1u, grid));
+    if (dtype == 1)
+        k_transform_hist<double><<<g, kThreads, lds, st>>>((const double*)cells, units, tiles, ntiles, tf, out, keys,
+                                                           hist);
+    else
+        k_transform_hist<float><<<g, kThreads, lds, st>>>((const float*)cells, units, tiles, ntiles, tf, out, keys,
+                                                          hist);
+    return hipGetLastError();
 }
 
 hipError_t launch_transform_fast(hipStream_t st, const void* cells, int dtype, const UnitDev* units,
