@@ -19,28 +19,10 @@ __device__ __forceinline__ int lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0));
 }
 
-__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long w = __shfl_xor(v, o);
-        v = w > v ? w : v;
-    }
-    return v;
-}
-
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        uint32_t w = __shfl_xor(v, o);
-        v = w > v ? w : v;
-    }
     return v;
 }
 
@@ -50,16 +32,12 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // chain of six VALU ops instead of six LDS-crossbar bpermutes (__shfl_xor).
 // Lanes whose DPP source is out of range read 0, the identity of the unsigned
 // max and of the sum.
-#ifndef WC_DPP_RED
-#define WC_DPP_RED 1
-#endif
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
     return __builtin_amdgcn_update_dpp(0u, v, CTRL, ROW_MASK, 0xf, false);
 }
 
 __device__ __forceinline__ uint32_t wave_max_u32_u(uint32_t v) {
-#if WC_DPP_RED
     v = max(v, dpp_u32<0x111, 0xf>(v));
     v = max(v, dpp_u32<0x112, 0xf>(v));
     v = max(v, dpp_u32<0x114, 0xf>(v));
@@ -67,13 +45,9 @@ __device__ __forceinline__ uint32_t wave_max_u32_u(uint32_t v) {
     v = max(v, dpp_u32<0x142, 0xa>(v));
     v = max(v, dpp_u32<0x143, 0xc>(v));
     return __builtin_amdgcn_readlane(v, 63);
-#else
-    return wave_max_u32(v);
-#endif
 }
 
 __device__ __forceinline__ uint32_t wave_sum_u32_u(uint32_t v) {
-#if WC_DPP_RED
     v += dpp_u32<0x111, 0xf>(v);
     v += dpp_u32<0x112, 0xf>(v);
     v += dpp_u32<0x114, 0xf>(v);
@@ -81,24 +55,6 @@ __device__ __forceinline__ uint32_t wave_sum_u32_u(uint32_t v) {
     v += dpp_u32<0x142, 0xa>(v);
     v += dpp_u32<0x143, 0xc>(v);
     return __builtin_amdgcn_readlane(v, 63);
-#else
-    return wave_sum(v);
-#endif
-}
-
-// Exclusive max over the lanes below this one (0 for lane 0): the inclusive
-// DPP max scan, then wave_shr:1 (a GFX9 whole-wave DPP shift).
-#ifndef WC_DPP_SHIFT
-#define WC_DPP_SHIFT 1
-#endif
-__device__ __forceinline__ uint32_t wave_excl_max_u32(uint32_t v) {
-    v = max(v, dpp_u32<0x111, 0xf>(v));
-    v = max(v, dpp_u32<0x112, 0xf>(v));
-    v = max(v, dpp_u32<0x114, 0xf>(v));
-    v = max(v, dpp_u32<0x118, 0xf>(v));
-    v = max(v, dpp_u32<0x142, 0xa>(v));
-    v = max(v, dpp_u32<0x143, 0xc>(v));
-    return dpp_u32<0x138, 0xf>(v);  // wave_shr:1
 }
 
 __device__ __forceinline__ unsigned long long dpp_u64_max_step(unsigned long long v, uint32_t lo, uint32_t hi) {
@@ -107,7 +63,6 @@ __device__ __forceinline__ unsigned long long dpp_u64_max_step(unsigned long lon
 }
 
 __device__ __forceinline__ unsigned long long wave_max_u64_u(unsigned long long v) {
-#if WC_DPP_RED
 #define WC_MAX64_STEP(C, M) v = dpp_u64_max_step(v, dpp_u32<C, M>((uint32_t)v), dpp_u32<C, M>((uint32_t)(v >> 32)))
     WC_MAX64_STEP(0x111, 0xf);
     WC_MAX64_STEP(0x112, 0xf);
@@ -118,9 +73,6 @@ __device__ __forceinline__ unsigned long long wave_max_u64_u(unsigned long long 
 #undef WC_MAX64_STEP
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 63), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), 63);
     return ((unsigned long long)hi << 32) | lo;
-#else
-    return wave_max_u64(v);
-#endif
 }
 
 // Load the x-pair (x, x+1) of a row as fp32 (fp64 cells narrowed RNE,

@@ -8,19 +8,8 @@
 #ifndef WC_EMIT_SB
 #define WC_EMIT_SB 2  // 256-element blocks whose pairs share one copy-out (stage: 256 * WC_EMIT_SB pairs per wave)
 #endif
-#ifndef WC_EMIT_FULL
-#define WC_EMIT_FULL 1  // full emit tiles skip the per-element range checks
-#endif
-#ifndef WC_EMIT_RUNLATE
-#define WC_EMIT_RUNLATE 1  // pairs staged as (flat index, value); runs taken at the copy-out (no per-block scan)
-#endif
 #ifndef WC_EMIT_KEYPAR
 #define WC_EMIT_KEYPAR 1  // the unit key loads beside the flags (bit 0: 4-wave launch, bit 1: 8-wave: +11 VGPRs there)
-#endif
-#ifndef WC_EMIT_NTLOAD
-// staged coefficients read with nontemporal loads (their last use): emit -8 % at C2, -11 % at C3
-// (profiles/r05/experiments/gpu_nt.txt; nontemporal payload stores measured +7 %: not used)
-#define WC_EMIT_NTLOAD 1
 #endif
 
 namespace wc {
@@ -49,7 +38,7 @@ struct RowOut {
 // Emit the kept coefficients of one kEmitTile chunk held in q (thread (w, l)
 // owns elements w*2048 + it*256 + 4l + j; kb bit it*4 + j = kept) as (run,
 // value) pairs: ranks from per-column ballots, run = f - prev - 1 (taken at
-// the copy-out from the staged indices, WC_EMIT_RUNLATE).  rank /
+// the copy-out from the staged indices: no per-block scan).  rank /
 // prev: this wave's first pair index and the unit-relative flat index of the
 // last kept coefficient before this wave's elements (0xffffffff = none, so
 // that run = f).  32-bit arithmetic: flat indices are < 2^31.
@@ -67,11 +56,7 @@ template <bool kRows>
 __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, uint32_t start, int w, int l,
                                            uint32_t rank, uint32_t prev, uint2* __restrict__ pairs, uint2* stage,
                                            const RowOut& ro) {
-    static_assert(!kRows || WC_EMIT_RUNLATE, "the row-index output needs the late-run copy-out");
     uint32_t soff = 0;  // pairs staged since the last copy-out
-#if !WC_EMIT_RUNLATE
-    const unsigned long long lt = (1ull << l) - 1ull;
-#endif
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
         const uint32_t nib = (kb >> (it * 4)) & 0xfu;
@@ -85,7 +70,6 @@ __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, ui
             const uint32_t itot = (uint32_t)(__popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3));
             const uint32_t ebase = start + (uint32_t)(w * 2048 + it * 256 + l * 4);
             uint32_t r = soff + pre;
-#if WC_EMIT_RUNLATE
             // staged as (flat index, value); runs are taken at the copy-out
             if (nib) {
                 const float vv[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
@@ -93,34 +77,11 @@ __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, ui
                 for (int j = 0; j < 4; ++j)
                     if (nib & (1u << j)) stage[r++] = make_uint2(ebase + (uint32_t)j, __float_as_uint(vv[j]));
             }
-#else
-            const uint32_t lane_last = ebase + (nib ? 31u - (uint32_t)__clz(nib) : 0u);
-            const unsigned long long below = any & lt;
-            // last kept index of the nearest lower lane with a kept element:
-            // indices grow with the lane, so the exclusive max over the lanes
-            // below (lanes without one contribute 0)
-            const uint32_t from_lane = wave_excl_max_u32(nib ? lane_last : 0u);
-            uint32_t p = below ? from_lane : prev;
-            if (nib) {
-                const float vv[4] = {q[it].x, q[it].y, q[it].z, q[it].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    if (nib & (1u << j)) {
-                        const uint32_t f = ebase + (uint32_t)j;
-                        stage[r] = make_uint2(f - p - 1u, __float_as_uint(vv[j]));
-                        p = f;
-                        ++r;
-                    }
-                }
-            }
-            prev = __builtin_amdgcn_readlane(lane_last, 63 - __clzll(any));  // uniform source lane
-#endif
             soff += itot;
         }
         // copy-out every WC_EMIT_SB blocks of 256 elements (the stage holds their pairs)
         if (it % WC_EMIT_SB == WC_EMIT_SB - 1 && soff) {
             __builtin_amdgcn_wave_barrier();
-#if WC_EMIT_RUNLATE
             {
                 // run = f - (previous pair's f) - 1: the previous pair is lane
                 // l - 1's (a whole-wave DPP shift), for lane 0 the carry (the
@@ -145,9 +106,6 @@ __device__ __forceinline__ void emit_pairs(const float4 (&q)[8], uint32_t kb, ui
                 }
                 prev = __builtin_amdgcn_readlane(e.x, (soff - 1u) & 63u);  // the last pair's index
             }
-#else
-            for (uint32_t k = (uint32_t)l; k < soff; k += 64) pairs[rank + k] = stage[k];
-#endif
             __builtin_amdgcn_wave_barrier();
             rank += soff;
             soff = 0;
@@ -213,12 +171,10 @@ constexpr unsigned long long kMask31 = 0x7fffffffull;
 struct PlainTile {
     const float4* __restrict__ p;
     __device__ __forceinline__ float4 operator[](int i) const {
-        if constexpr (WC_EMIT_NTLOAD) {  // the staged coefficients' last use
-            const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + i));
-            return make_float4(x.x, x.y, x.z, x.w);
-        } else {
-            return p[i];
-        }
+        // the staged coefficients' last use: nontemporal (emit -8 % at C2, -11 % at C3,
+        // profiles/r05/experiments/gpu_nt.txt; nontemporal payload stores measured +7 %: not used)
+        const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + i));
+        return make_float4(x.x, x.y, x.z, x.w);
     }
 };
 struct PlainSrc {
@@ -292,16 +248,10 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
         // one flag byte per segment of TZ = 2^lbz coefficients (16 or 32)
         const int sh = (int)((U.mode >> 1) & 7u);  // lbz
         const uint8_t* fl = P.flags + U.flag_off + (((uint64_t)index * kTile) >> sh);
-#if WC_FLAG_PERM
         // this thread's 8 flags in 8 consecutive bytes (flag_pos): bytes 0 / 1
         const uint2 f8 = *reinterpret_cast<const uint2*>(fl + ((uint32_t)w << (11 - sh)) + ((((uint32_t)l << 2) >> sh) << 3));
         segf = (f8.x & 1u) | ((f8.x >> 7) & 2u) | ((f8.x >> 14) & 4u) | ((f8.x >> 21) & 8u) | ((f8.y & 1u) << 4) |
                ((f8.y >> 3) & 0x20u) | ((f8.y >> 10) & 0x40u) | ((f8.y >> 17) & 0x80u);
-#else
-        segf = 0;
-#pragma unroll
-        for (int it = 0; it < 8; ++it) segf |= (uint32_t)(fl[(w * 2048 + it * 256 + 4 * l) >> sh] != 0) << it;
-#endif
     }
     // the unit key: a finished earlier launch wrote it, one uniform load
     float tf = 0.0f;
@@ -318,7 +268,7 @@ __device__ __forceinline__ void emit_tile(const EmitParams& P, const Src& src, c
         if (!(tf >= 0.0f)) segf = 0xffu;
     float4 q[8];
     uint32_t kb;
-    if (WC_EMIT_FULL && len == kTile) {  // uniform: a full tile, no range checks
+    if (len == kTile) {  // uniform: a full tile, no range checks
 #pragma unroll
         for (int it = 0; it < 8; ++it)
             q[it] = ((segf >> it) & 1u) ? p4[w * 512 + it * 64 + l] : make_float4(0, 0, 0, 0);

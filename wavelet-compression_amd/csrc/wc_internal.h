@@ -143,11 +143,8 @@ struct EmitParams {
 };
 
 constexpr int kSegShift = 4;    // sparse staging: flag index space of 16 coefficients per byte (min segment)
-#ifndef WC_FLAG_PERM
-#define WC_FLAG_PERM 1
-#endif
 // Byte position of sparse-staging segment s (= flat index >> sh, sh = log2 of
-// the segment length, 4 or 5) in its unit's flag range.  WC_FLAG_PERM: within
+// the segment length, 4 or 5) in its unit's flag range: within
 // each 2048-coefficient block of a unit (one emit wave's share of a tile) the
 // 8 flags one emit thread reads (element groups it = 0..7: segment it * G + g,
 // G = 256 >> sh, g = its lane group) sit in 8 consecutive bytes, g * 8 + it:
@@ -155,25 +152,15 @@ constexpr int kSegShift = 4;    // sparse staging: flag index space of 16 coeffi
 // flag range (UnitDev::flag_off) is 8-B aligned and spans whole blocks, so
 // permuted positions never leave it.
 __host__ __device__ inline uint64_t flag_pos(uint64_t s, int sh) {
-#if WC_FLAG_PERM
     const int lb = 11 - sh, lg = 8 - sh;
     const uint64_t sw = s & ((1ull << lb) - 1);
     return (s & ~((1ull << lb) - 1)) | ((sw & ((1ull << lg) - 1)) << 3) | (sw >> lg);
-#else
-    (void)sh;
-    return s;
-#endif
 }
 // flag_pos on 32-bit segment indices (K1's S32 form: units of < 2^30 cells).
 __host__ __device__ inline uint32_t flag_pos32(uint32_t s, int sh) {
-#if WC_FLAG_PERM
     const int lb = 11 - sh, lg = 8 - sh;
     const uint32_t sw = s & ((1u << lb) - 1);
     return (s & ~((1u << lb) - 1)) | ((sw & ((1u << lg) - 1)) << 3) | (sw >> lg);
-#else
-    (void)sh;
-    return s;
-#endif
 }
 #ifndef WC_RIX_TILE
 #define WC_RIX_TILE 4096

@@ -76,16 +76,8 @@ __device__ __forceinline__ uint32_t wave_incl_sum32_sat(uint32_t v) {
 // the payload's pair tiles exit after the header.  The look-back granules are
 // epoch-tagged: no zeroing between calls.
 
-#ifndef WC_RIX_LDSV
-#define WC_RIX_LDSV 1  // park the inclusive sums in LDS across the look-back (16 KB per workgroup)
-#endif
 #ifndef WC_RIX_MINB
 #define WC_RIX_MINB 8  // waves per SIMD the register budget is sized for (4-wave blocks: 8 per CU, <= 64 VGPRs)
-#endif
-#ifndef WC_RIX_RUNS_NT
-// the row index's run loads nontemporal: K5 -12 % at C2, K6r after it +1 %, C5 even
-// (profiles/r05/experiments/gpu_nt.txt)
-#define WC_RIX_RUNS_NT 1
 #endif
 __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDev* __restrict__ units,
                                                      const FTile* __restrict__ tiles, uint32_t* __restrict__ ticket,
@@ -96,11 +88,9 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDe
                                                      int ordered, uint32_t epoch, uint32_t* __restrict__ npairs) {
     __shared__ uint32_t s_w[4];
     __shared__ uint32_t s_x[2];
-#if WC_RIX_LDSV
     // the waves' inclusive sums, parked across the look-back (round r of thread
-    // tid at [r][tid]: the row phase holds no 16-register array)
+    // tid at [r][tid]: the row phase holds no 16-register array; 16 KB per workgroup)
     __shared__ uint32_t s_v[kRixRounds5][kThreads];
-#endif
     const int tid = threadIdx.x, l = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const FTile ft = cst(tiles)[blockIdx.x];
@@ -127,7 +117,8 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDe
 #pragma unroll
         for (int r = 0; r < kRixRounds5; ++r) {
             const uint32_t k = kw + r * 64 + l;
-            v[r] = k < n ? (WC_RIX_RUNS_NT ? __builtin_nontemporal_load(runs + 2 * k) : runs[2 * k]) : 0u;
+            // nontemporal: K5 -12 % at C2, K6r after it +1 %, C5 even (profiles/r05/experiments/gpu_nt.txt)
+            v[r] = k < n ? __builtin_nontemporal_load(runs + 2 * k) : 0u;
         }
     }
     if (!hok && t == 0 && tid == 0) atomicOr(err, kErrHeader);
@@ -143,11 +134,7 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDe
         neg |= k < n && run < 0;
         const uint32_t x = k < n ? (run < 0 ? 1u : (uint32_t)run + 1u) : 0u;
         const uint32_t s = wave_incl_sum32_sat(x);
-#if WC_RIX_LDSV
         s_v[r][tid] = sat_add(wsum, s);
-#else
-        v[r] = sat_add(wsum, s);
-#endif
         wsum = sat_add(wsum, __builtin_amdgcn_readlane(s, 63));
     }
     if (neg) atomicOr(err, kErrNegativeRun);
@@ -199,19 +186,11 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINB) void k_rowindex(const UnitDe
 #pragma unroll
     for (int r = 0; r < kRixRounds5; ++r) {
         const uint32_t k = kw + r * 64 + l;
-#if WC_RIX_LDSV
         const uint32_t vr = s_v[r][tid];
-#else
-        const uint32_t vr = v[r];
-#endif
         const uint32_t phk = k < n ? min(sat_add(A, vr) - 1u, nc) : nc;
         const int32_t rhi = k <= n ? (int32_t)div_rows(phk, U.dmagic) : -1;
         // rhi of pair k - 1: lane l - 1, the carry in lane 0
-#if WC_DPP_SHIFT
         const int32_t from = __builtin_amdgcn_update_dpp(0, rhi, 0x138, 0xf, 0xf, false);  // wave_shr:1
-#else
-        const int32_t from = __builtin_amdgcn_ds_bpermute((l - 1) << 2, rhi);
-#endif
         const int32_t rlo = (l == 0 ? carry : from) + 1;
         const uint32_t cnt = (k <= n && rhi >= rlo) ? (uint32_t)(rhi - rlo + 1) : 0u;
         write_rows(ri, (uint32_t)rlo, cnt, k, phk, D, l);
@@ -598,14 +577,6 @@ __global__ __launch_bounds__(kThreads) void k_inverse_fast(const float* __restri
 #ifndef WC_RIX_ROUNDS
 #define WC_RIX_ROUNDS 16  // prefetch slots (one per range): 128 VGPRs with the x-quad synthesis, 4 waves per SIMD, no spills
 #endif
-#ifndef WC_RIX_F4
-#define WC_RIX_F4 1  // x-quad (16-B) stores where the output allows them
-#endif
-#ifndef WC_RIX_NT
-// x-quad output stores nontemporal where no RMSE pass re-reads them: K6r -9 % at C2, -6 % at C3
-// (profiles/r05/experiments/gpu_nt.txt; nontemporal pair loads measured slower: not used)
-#define WC_RIX_NT 1
-#endif
 constexpr int kRixRounds = WC_RIX_ROUNDS;
   // rounds of 64 pairs prefetched per wave
 
@@ -743,9 +714,6 @@ __device__ __forceinline__ void rix_prefetch(uint2 (&q)[NR], const uint2* __rest
     static_assert(NR <= 16, "rix_prefetch: extend WC_RIX_PF");
 }
 
-#ifndef WC_RIX_RMSE_INLINE
-#define WC_RIX_RMSE_INLINE 1  // fp64 originals: fused RMSE summed inside the x-quad synthesis (no re-read of the output)
-#endif
 #ifndef WC_RIX_RMSE_ROUNDS_LESS
 // prefetch slots given up by the inline fused-RMSE form (OT 1): 3 is the fewest
 // without spills; 9 measured 3 % faster at C3, 1 % at C2 (profiles/r05/
@@ -883,7 +851,8 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
             float* __restrict__ dst = out + T.cell_off;
             const int64_t sy = W, sz = (int64_t)W * H;
             const int64_t lo = (int64_t)(T.bx0 * 2);
-            f4 = WC_RIX_F4 && TX >= 2 && ((T.cell_off & 3) == 0) && ((W & 3) == 0);  // uniform (out: 16-B aligned)
+            // x-quad (16-B) stores where the output allows them (uniform: out 16-B aligned)
+            f4 = TX >= 2 && ((T.cell_off & 3) == 0) && ((W & 3) == 0);
             if (f4) {
                 // two x-blocks x two z-blocks per thread: 16-B x-quad stores
                 const int nq = (TX >> 1) * TYv * (hz >> 1);
@@ -892,10 +861,11 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
                     const int byl = rest % TYv, bq = rest / TYv;
                     const int bxl = 2 * bp, by = T.by0 + byl, bzb = 2 * bq;
                     if (T.bx0 + bxl >= hx) continue;
-                    // fused RMSE (WC_RIX_RMSE_INLINE): the original cells of z-block
+                    // fused RMSE (OT 1, fp64 originals: summed inside this synthesis, no
+                    // re-read of the output): the original cells of z-block
                     // pair qb = 0, issued before the LDS reads (qb = 1: after qb 0)
                     float og[2][2][2][4];  // [qb][dz][dy][4 x-cells], original cells narrowed to float
-                    if constexpr (OT == 1 && WC_RIX_RMSE_INLINE)
+                    if constexpr (OT == 1)
                         rix_load_orig<OT>(orig, T.cell_off + lo + 2 * bxl + sy * (2 * by) + sz * (2 * bzb), sy, sz, og[0]);
                     float c[2][2][2][2][2];  // [x-block][sz][sy][sx][z-block]
 #pragma unroll
@@ -931,7 +901,9 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
 #pragma unroll
                             for (int dy = 0; dy < 2; ++dy) {
                                 float* p = dst + lo + 2 * bxl + sy * (2 * by + dy) + sz * (2 * (bzb + qb) + dz);
-                                if constexpr (WC_RIX_NT && OT <= 1) {  // OT 2, 3 re-read the output from L2
+                                // nontemporal where no RMSE pass re-reads the output (OT 2, 3 re-read it
+                                // from L2): K6r -9 % at C2, -6 % at C3 (profiles/r05/experiments/gpu_nt.txt)
+                                if constexpr (OT <= 1) {
                                     const f32x4 x = {V[0][dz][dy][0], V[0][dz][dy][1], V[1][dz][dy][0],
                                                      V[1][dz][dy][1]};
                                     __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p));
@@ -940,7 +912,7 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
                                                                                 V[1][dz][dy][0], V[1][dz][dy][1]);
                                 }
                             }
-                        if constexpr (OT == 1 && WC_RIX_RMSE_INLINE) {
+                        if constexpr (OT == 1) {
                             if (qb == 0)  // the second z-block pair's originals, in flight during this one's sums
                                 rix_load_orig<OT>(orig, T.cell_off + lo + 2 * bxl + sy * (2 * by) + sz * (2 * (bzb + 1)),
                                                   sy, sz, og[1]);
@@ -1009,13 +981,13 @@ __global__ __launch_bounds__(kThreads, WC_RIX_MINW) void k_inverse_rows(const RT
             }
         }
         __syncthreads();
-        if constexpr (OT == 1 && WC_RIX_RMSE_INLINE) {
+        if constexpr (OT == 1) {
             if (f4) {  // uniform: the x-quad synthesis summed its own cells
                 const double acc = wave_sum(racc);
                 if (l == 0) part[4 * (uint64_t)T.nat + w] = acc;
             }
         }
-        if constexpr (OT != 0) if (!(OT == 1 && WC_RIX_RMSE_INLINE && f4)) {  // 4. calc_rmse_per_box over tile t's cells (src/calc-loss.cpp:12-43)
+        if constexpr (OT != 0) if (!(OT == 1 && f4)) {  // 4. calc_rmse_per_box over tile t's cells (src/calc-loss.cpp:12-43)
             const int TX = 1 << T.lbx, txv = min(TX, (T.W >> 1) - T.bx0), ny2 = 2 * T.tyv;
             const uint32_t nc = (uint32_t)(T.D * ny2) << T.lbx;
             const int64_t sy = T.W, sz = (int64_t)T.W * T.H;

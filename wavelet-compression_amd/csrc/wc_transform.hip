@@ -23,9 +23,6 @@ __device__ __forceinline__ uint64_t out_base(const UnitDev& U, int mode) {
 }
 
 // ---------------------------------------------------------------------------
-#ifndef WC_K1_S32
-#define WC_K1_S32 1  // the 32 x 1 x 32 tile shape specialised (wc_xform.h s32_ok)
-#endif
 
 // K1 kernels of the staged path: one tile per workgroup, coefficients written
 // to the flat scratch (plain stores: the next kernel reads them), the unit's
@@ -64,7 +61,7 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast(
     float* __restrict__ dst = out + obase;
     if constexpr (KEYS) {
         if (flags && U.sparse) {  // uniform; coef_off is 128-B aligned here
-            const bool s32 = WC_K1_S32 && s32_ok(U);  // uniform
+            const bool s32 = s32_ok(U);  // uniform: the 32 x 1 x 32 tile shape specialised
             uint32_t mag = s32 ? xform_fast_p1<T, false, true, true>(cells + U.cell_off, U, td, lds, threadIdx.x)
                                : xform_fast_p1<T, false, true>(cells + U.cell_off, U, td, lds, threadIdx.x);
             mag = wave_max_u32_u(mag);

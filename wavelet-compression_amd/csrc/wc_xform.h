@@ -18,10 +18,6 @@
 
 #include "wc_device.h"
 
-#ifndef WC_K1_NT
-#define WC_K1_NT false
-#endif
-
 namespace wc {
 
 __device__ __forceinline__ unsigned long long coef_key(float c, uint32_t f) {
@@ -201,7 +197,7 @@ __device__ __forceinline__ uint32_t xform_fast_p1(const T* __restrict__ src, con
             for (int zp = 0; zp < 4; ++zp)
 #pragma unroll
                 for (int dy = 0; dy < 2; ++dy)
-                    load_xpair<T, WC_K1_NT>(p0 + sz * (4 * h + zp) + sy * dy, true, vec, v[zp][dy][0], v[zp][dy][1]);
+                    load_xpair<T>(p0 + sz * (4 * h + zp) + sy * dy, true, vec, v[zp][dy][0], v[zp][dy][1]);
 #pragma unroll
             for (int qq = 0; qq < 2; ++qq) {
                 const int q = 2 * h + qq;
@@ -391,7 +387,7 @@ __device__ __forceinline__ double sparse_bound(uint32_t magkey, double keep) {
     return b >= 0.0 ? b : -1.0;
 }
 
-// Branch-free max key (WC_K1_BFKEY): with amax = the tile's largest |c| bits
+// Branch-free max key: with amax = the tile's largest |c| bits
 // and no NaN in the tile, only coefficients with |c| bits == amax can carry
 // the tile's max key, and among those coef_key orders by the low word alone
 // ((0x7fffffff - f) << 1 | sign: smallest flat index first).  So each
@@ -399,27 +395,11 @@ __device__ __forceinline__ double sparse_bound(uint32_t magkey, double keep) {
 // (`best`, 0 = none) instead of a branch around a 64-bit key; the key is
 // (amax << 32) | best.  A tile holding a NaN (amax > +inf's bits) takes the
 // per-coefficient coef_key pass instead (kKeyNaNFirst at flat index 0).
-#ifndef WC_K1_BFKEY
-#define WC_K1_BFKEY 1
-#endif
-#ifndef WC_K1_HITSKIP
-#define WC_K1_HITSKIP 1  // S32 phase 2: key work only in waves holding the tile max
-#endif
-#ifndef WC_K1_IDX32
-#define WC_K1_IDX32 1  // S32 phase 2: 32-bit flat indices with uniform per-row steps
-#endif
-#ifndef WC_K1_NT_STAGE
-// staged coefficients written with nontemporal stores: K1 -2 % at C2, -4 % at C5
-// (profiles/r05/experiments/gpu_nt.txt)
-#define WC_K1_NT_STAGE 1
-#endif
+// Staged coefficients are written with nontemporal stores (their next reader
+// is another kernel): K1 -2 % at C2, -4 % at C5 (profiles/r05/experiments/gpu_nt.txt).
 __device__ __forceinline__ void stage_store4(float* __restrict__ p, const float4& v) {
-    if constexpr (WC_K1_NT_STAGE) {
-        const f32x4 x = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p));
-    } else {
-        *reinterpret_cast<float4*>(p) = v;
-    }
+    const f32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p));
 }
 __device__ __forceinline__ uint32_t key_lo_max(uint32_t best, float c, uint32_t f, uint32_t amax) {
     const uint32_t bits = __float_as_uint(c);
@@ -439,7 +419,7 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse(const UnitDev
                                                                    const float* lds, int tid, double bound,
                                                                    uint32_t amax, uint8_t* __restrict__ flags,
                                                                    Store4 st) {
-    const bool bf = WC_K1_BFKEY && amax <= 0x7f800000u;  // uniform: no NaN in the tile
+    const bool bf = amax <= 0x7f800000u;  // uniform: no NaN in the tile
     uint32_t best = 0;
     const int H = U.ny, D = U.nz;
     const int hx = U.hx, hy = U.hy, hz = U.hz;
@@ -514,8 +494,7 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse_s32(const Uni
     const float bf = thresh_as_float(bound);
     const bool allkeys = amax > 0x7f800000u;  // a NaN in the tile: every key as in the generic form
     unsigned long long kmax = 0;
-    uint32_t best = 0;  // WC_K1_BFKEY running low word
-#if WC_K1_IDX32
+    uint32_t best = 0;  // running low word of the branch-free max key
     // 32-bit unit-relative indices (s32_ok: < 2^30 cells): row r0 + 16 it has
     // flat index fb + (it & 1) 16 H D + ssx hx H D + ssy hy D, uniform steps;
     // stores through the uniform bases with 32-bit offsets.
@@ -524,7 +503,6 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse_s32(const Uni
     const uint32_t dA = 16u * HD, dB = (uint32_t)hx * HD, dC = (uint32_t)hy * (uint32_t)D;
     uint8_t* __restrict__ fl = flags + U.flag_off;
     char* __restrict__ dstb = reinterpret_cast<char*>(dst);
-#endif
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
         const int row = r0 + 16 * it;  // row_of with lbx 5, lby 0: bxl, ssx, ssy
@@ -533,39 +511,17 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse_s32(const Uni
         const float m4 = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
         const bool cand = m4 > bf;
         const bool flag = ((__ballot(cand) >> g0) & 0xffull) != 0 || dense;
-#if WC_K1_IDX32
         const uint32_t f0 = fb + ((it & 1) ? dA : 0u) + (((it >> 1) & 1) ? dB : 0u) + ((it >> 2) ? dC : 0u);
         if (flag) stage_store4(reinterpret_cast<float*>(dstb + (f0 << 2)), v);
         if ((tid & 7) == 0) fl[flag_pos32(f0 >> lbz, lbz)] = flag ? 1 : 0;
-#else
-        const int bxl = row & 31, ssx = (row >> 5) & 1, ssy = row >> 6;
-        const int I = td.bx0 + bxl + ssx * hx, J = (int)td.by0 + ssy * hy;
-        const int64_t f = ((int64_t)I * H + J) * D + K;
-        if (flag) *reinterpret_cast<float4*>(dst + f) = v;
-        if ((tid & 7) == 0) flags[U.flag_off + flag_pos((uint64_t)f >> lbz, lbz)] = flag ? 1 : 0;
-        const uint32_t f0 = (uint32_t)f;
-#endif
         const float e[4] = {v.x, v.y, v.z, v.w};
-#if WC_K1_BFKEY
-        (void)allkeys;
         // only a wave with a lane holding the tile's largest |c| can raise the
         // key (no NaN here: allkeys tiles redo every key below)
-        if (!WC_K1_HITSKIP || __ballot(__float_as_uint(m4) == amax)) {
+        if (__ballot(__float_as_uint(m4) == amax)) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) best = key_lo_max(best, e[j], f0 + (uint32_t)j, amax);
         }
-#else
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t ab = __float_as_uint(e[j]) & 0x7fffffffu;
-            if (allkeys || ab == amax || (f0 + j == 0 && ab > 0x7f800000u)) {
-                const unsigned long long k = coef_key(e[j], f0 + (uint32_t)j);
-                kmax = k > kmax ? k : kmax;
-            }
-        }
-#endif
     }
-#if WC_K1_BFKEY
     if (!allkeys) return key_from_lo(amax, best);
     // a NaN in the tile (rare): every coefficient's key, as the generic form
 #pragma unroll
@@ -582,7 +538,6 @@ __device__ __forceinline__ unsigned long long xform_fast_p2_sparse_s32(const Uni
             kmax = k > kmax ? k : kmax;
         }
     }
-#endif
     return kmax;
 }
 
