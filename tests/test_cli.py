@@ -161,8 +161,9 @@ def test_estimate_matches_oracle(run, compressed, oracle):
 
 
 def test_multi_device_workers_write_identical_files(run, compressed, tmp_path):
-    """WCAMD_DEVICES spreads chunks (and -d timesteps) over one host thread +
-    context per listed device; "0,0" runs that path on a one-GPU box."""
+    """Chunks (and -d timesteps) spread over one host thread + context per
+    device: every visible device by default, WCAMD_DEVICES picks them ("0,0"
+    runs the multi-device path on a one-GPU box), WCAMD_DEVICE pins one."""
     import filecmp
     base, _ = run
     out = base / "comp_md"
@@ -174,12 +175,23 @@ def test_multi_device_workers_write_identical_files(run, compressed, tmp_path):
     for n in names:
         assert filecmp.cmp(compressed / n, out / n, shallow=False), n
     r1, r2 = base / "regen_md1", base / "regen_md2"
-    cli(f"compresseddir={compressed}/", f"out={r1}/", "-d")
+    cli(f"compresseddir={compressed}/", f"out={r1}/", "-d", env={"WCAMD_DEVICE": "0"})
     cli(f"compresseddir={out}/", f"out={r2}/", "-d", env={"WCAMD_DEVICES": "0,0"})
     for root, _, files in os.walk(r1):
         for f in files:
             a = Path(root) / f
             assert filecmp.cmp(a, r2 / a.relative_to(r1), shallow=False), a
+    # -estimate over two device workers (chunks of one box each, in any order):
+    # the same RMSE / adjusted loss / size lines as one device (the per-box
+    # RMSEs are averaged in iterator order whatever chunk finishes first)
+    args = (f"datadir={base}/data/", "minfile=plt00010", "maxfile=plt00012", "minlevel=0", "maxlevel=0",
+            "components=temp pressure", f"keep={KEEP}", f"compresseddir={base}/unused/", "-estimate")
+    want = re.findall(r"Predicted .*", cli(*args, env={"WCAMD_DEVICE": "0"}))
+    got = re.findall(r"Predicted .*", cli(*args, env={"WCAMD_CHUNK_CELLS": "20000", "WCAMD_DEVICES": "0,0",
+                                                     "WCAMD_THREADS": "4"}))
+    assert len(want) == 5 and got == want
+    # no device variable: every visible device (this box's one GPU), same lines
+    assert re.findall(r"Predicted .*", cli(*args, env={"WCAMD_CHUNK_CELLS": "20000"})) == want
 
 
 def test_fast_xz_preset_round_trip(run, compressed, tmp_path):

@@ -59,6 +59,18 @@ def place(boxes):
     return out
 
 
+def cli_devices() -> int:
+    """The GPUs the CLI spreads a run over (host/modes.cpp run_devices): every
+    visible device unless WCAMD_DEVICES / WCAMD_DEVICE pick them."""
+    v, one = os.environ.get("WCAMD_DEVICES", ""), os.environ.get("WCAMD_DEVICE", "")
+    if not v and one:
+        return 1
+    if v and v != "all":
+        return len([x for x in v.split(",") if x])
+    import torch  # counting devices does not initialise the GPU in this process
+    return torch.cuda.device_count()
+
+
 def digit_free_dir() -> Path:
     p = Path(tempfile.gettempdir()) / ("wcamd_etoe_" + "".join(random.choice(string.ascii_lowercase) for _ in range(8)))
     assert not any(ch.isdigit() for ch in str(p)), p  # format_files reads the digits of the WHOLE path
@@ -154,6 +166,7 @@ def main():
             "decompress_cells_per_s": ncells / t_d,
             "xz_bytes": xz_bytes, "compressed_fraction": xz_bytes / (ncells * 8),
             "xz_preset": 6, "fast_xz_presets": fast,
+            "gpu_devices": cli_devices(),
             "host_threads": int(os.environ.get("WCAMD_THREADS", os.environ.get("OMP_NUM_THREADS", os.cpu_count()))),
             "cpu_compress_cells_per_s": args.cpu_cells_per_s,
             "speedup_vs_cpu_compress": (ncells / t_c) / args.cpu_cells_per_s if args.cpu_cells_per_s else None,

@@ -19,6 +19,7 @@
 #include <filesystem>
 #include <fstream>
 #include <future>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <numeric>
@@ -49,22 +50,29 @@ std::string fmt_double(double v) {
     return std::string(b, r.ptr);
 }
 
-uint64_t chunk_cells() {
+// Cells per chunk: $WCAMD_CHUNK_CELLS, else 2^28 (2 GiB of fp64), cut to the
+// run's share of each device (down to 2^24 cells) so every device gets work.
+uint64_t chunk_cells(uint64_t total = 0, size_t ndev = 1) {
     if (const char* v = std::getenv("WCAMD_CHUNK_CELLS")) {
         const long long n = std::atoll(v);
         if (n > 0) return (uint64_t)n;
     }
-    return 1ull << 28;
+    const uint64_t share = ndev > 1 ? (total + ndev - 1) / ndev : total;
+    return std::clamp<uint64_t>(share, 1ull << 24, 1ull << 28);
 }
 
-// GPUs to spread a run over: $WCAMD_DEVICES = "all" or "0,2,5"; unset -> one
-// device ($WCAMD_DEVICE, default 0), as the reference runs on one process.
+// GPUs to spread a run over (units shard over the node's
+// GPUs): every visible device by default; $WCAMD_DEVICES = "all" or a list
+// "0,2,5" (a device may repeat: several host workers on one GPU) picks them;
+// $WCAMD_DEVICE alone pins the run to one device.
 std::vector<int> run_devices() {
     std::vector<int> d;
     const char* v = std::getenv("WCAMD_DEVICES");
-    if (!v || !*v) return {-1};  // -1: thread_ctx()'s default device
-    if (std::string(v) == "all") {
+    const char* one = std::getenv("WCAMD_DEVICE");
+    if ((!v || !*v) && one && *one) return {std::atoi(one)};
+    if (!v || !*v || std::string(v) == "all") {
         for (int i = 0; i < wc_device_count(); ++i) d.push_back(i);
+        if (d.empty()) return {-1};  // no device: thread_ctx() fails loudly on first use
     } else {
         std::string cur;
         for (const char* p = v;; ++p) {
@@ -81,9 +89,12 @@ std::vector<int> run_devices() {
     return d;
 }
 
-// Run worker(device, threads_per_device) on one host thread per device.
+// Run worker(threads_per_device) on one host thread per device, for `work`
+// items (chunks, timesteps): no more devices than items, so a small run keeps
+// the whole host pool for its xz stage.
 template <class F>
-void on_devices(const std::vector<int>& devs, F worker) {
+void on_devices(std::vector<int> devs, size_t work, F worker) {
+    devs.resize(std::max<size_t>(1, std::min(devs.size(), work)));
     const int tpd = std::max(1, host_threads() / (int)devs.size());
     if (devs.size() == 1) {
         if (devs[0] >= 0) set_thread_device(devs[0]);
@@ -257,14 +268,26 @@ void inverse_batch(const std::vector<std::string>& payloads, const std::vector<w
     check(ctx, wc_inverse_host(ctx, buf.data(), offs.data(), units.data(), (int)units.size(), out), "GPU decompress");
 }
 
+// The run's cells over all (t, lev, box) and selected components.
+uint64_t run_cells(const RunIndex& r, size_t nc) {
+    uint64_t total = 0;
+    for (const auto& t : r.fabs)
+        for (const auto& l : t)
+            for (const FabRef& f : l)
+                total += (uint64_t)(f.hi[0] - f.lo[0] + 1) * (f.hi[1] - f.lo[1] + 1) * (f.hi[2] - f.lo[2] + 1) * nc;
+    return total;
+}
+
 // Compress every unit of `r` into `dir` (file names joined as std::filesystem
-// paths, src/compressor.cpp:250-254).  `on_chunk` sees each chunk and its
-// payloads after its forward pass (round_trip: with every unit's RMSE).
+// paths, src/compressor.cpp:250-254), chunks spread over `devs`.  `on_chunk(i,
+// chunk, payloads)` sees chunk i (iterator order) after its forward pass
+// (round_trip: with every unit's RMSE), on the device's host thread: chunks
+// arrive in any order and concurrently, so it does its own locking.
 template <class OnChunk>
 void compress_run(const RunIndex& r, double keep, const std::filesystem::path& dir, OnChunk on_chunk,
                   const std::vector<int>& devs, bool round_trip = false) {
     const size_t nc = r.comp_idxs.size();
-    std::vector<Chunk> chunks = plan_chunks(r, nc, chunk_cells());
+    std::vector<Chunk> chunks = plan_chunks(r, nc, chunk_cells(run_cells(r, nc), devs.size()));
     auto jobs_of = [&](const Chunk& c, const Packed& p) {
         std::vector<XzJob> jobs;
         for (size_t i = 0; i < c.boxes.size(); ++i)
@@ -277,8 +300,7 @@ void compress_run(const RunIndex& r, double keep, const std::filesystem::path& d
         return jobs;
     };
     std::atomic<size_t> next{0};
-    std::mutex cb;
-    on_devices(devs, [&](int threads) {
+    on_devices(devs, chunks.size(), [&](int threads) {
         // per device: read + GPU pass of chunk i overlapped with the xz stage of chunk i-1
         std::future<void> xz_done;
         for (size_t i = next.fetch_add(1); i < chunks.size(); i = next.fetch_add(1)) {
@@ -289,10 +311,7 @@ void compress_run(const RunIndex& r, double keep, const std::filesystem::path& d
             if (xz_done.valid()) xz_done.get();
             xz_done = std::async(std::launch::async,
                                  [jobs = std::move(jobs), p, threads]() { xz_write_files(jobs, threads); });
-            {
-                std::lock_guard<std::mutex> g(cb);
-                on_chunk(c, *p);
-            }
+            on_chunk(i, c, *p);
             c.cells.clear();
             c.cells.shrink_to_fit();
         }
@@ -328,8 +347,8 @@ int compress(const Config& cfg) {
     write_amrexinfo(r.amrexinfo, cfg.compressed_dir, "amrexinfo.raw");
     log_info("Successfully processed data in " + fmt_double(since(t0)) + " seconds. Beginning compression...");
     const auto t1 = Clock::now();
-    compress_run(r, (double)cfg.keep, std::filesystem::path(cfg.compressed_dir), [](const Chunk&, const Packed&) {},
-                 run_devices());
+    compress_run(r, (double)cfg.keep, std::filesystem::path(cfg.compressed_dir),
+                 [](size_t, const Chunk&, const Packed&) {}, run_devices());
     log_info("Compression completed in " + fmt_double(since(t1)) + " seconds.");
     return 0;
 }
@@ -353,7 +372,7 @@ int decompress(const Config& cfg) {
     // One timestep at a time per device: decode its files on the pool, one GPU
     // inverse for all its units, then write its plotfile.
     std::atomic<int> next{0};
-    on_devices(run_devices(), [&](int threads) {
+    on_devices(run_devices(), (size_t)std::max(num_times, 0), [&](int threads) {
         for (int t = next.fetch_add(1); t < num_times; t = next.fetch_add(1)) {
             std::vector<std::string> paths;
             std::vector<wc_unit> units;
@@ -417,22 +436,45 @@ int estimate(Config& cfg) {
     // (wc_round_trip_host): the files are still written (their sizes are the
     // estimate), the RMSE comes from the same payload bytes they hold.
     // min/max over the narrowed values.
+    // Chunks run on every device; the per-box RMSEs are kept per chunk and
+    // averaged in iterator order (the reference's order, so the mean is the
+    // same double whatever the device count); min / max do not depend on order.
     std::vector<std::vector<double>> all_rmses(nc);
     std::vector<float> minv(nc, FLT_MAX), maxv(nc, FLT_MIN);  // src/preprocess.cpp:30-31 quirk
-    const std::vector<int> one_device = {run_devices()[0]};
-    compress_run(r, (double)cfg.keep, scratch.path(), [&](Chunk& c, const Packed& p) {
+    std::map<size_t, std::vector<double>> chunk_rmse;  // chunk -> its units' RMSEs
+    std::mutex mu;
+    compress_run(r, (double)cfg.keep, scratch.path(), [&](size_t ci, Chunk& c, const Packed& p) {
+        std::vector<float> lo(nc, FLT_MAX), hi(nc, FLT_MIN);
         for (size_t u = 0; u < c.units.size(); ++u) {
             const size_t k = u % nc;
             const uint64_t n = (uint64_t)c.units[u].nx * c.units[u].ny * c.units[u].nz;
             const double* s = c.cells.data() + c.units[u].cell_offset;
             for (uint64_t i = 0; i < n; ++i) {
                 const float v = (float)s[i];
-                if (v < minv[k]) minv[k] = v;
-                if (v > maxv[k]) maxv[k] = v;
+                if (v < lo[k]) lo[k] = v;
+                if (v > hi[k]) hi[k] = v;
             }
-            all_rmses[k].push_back(p.rmse[u]);
         }
-    }, one_device, /*round_trip=*/true);
+        std::lock_guard<std::mutex> g(mu);
+        for (size_t k = 0; k < nc; ++k) {
+            minv[k] = std::min(minv[k], lo[k]);
+            maxv[k] = std::max(maxv[k], hi[k]);
+        }
+        chunk_rmse[ci] = p.rmse;
+    }, run_devices(), /*round_trip=*/true);
+    for (const auto& [ci, rm] : chunk_rmse)
+        for (size_t u = 0; u < rm.size(); ++u) all_rmses[u % nc].push_back(rm[u]);
+    // The reference reads every file back (src/modes.cpp:250-265) and exits on
+    // one it cannot read; the RMSE here comes from the payloads in memory, so
+    // check the files the size estimate counts exist and are not empty.
+    for (int b = 0; b < r.box_counts[0][0]; ++b)
+        for (int comp : r.comp_idxs) {
+            const std::string f = (scratch.path() / unit_name(0, 0, comp, b)).string();
+            std::error_code ec;
+            const auto sz = std::filesystem::file_size(f, ec);
+            if (ec) fatal("Error getting file size: " + ec.message() + " " + f);
+            if (sz == 0) fatal("Failed to read file: " + f);
+        }
     log_info("Compression complete.");
     log_info("Decompression complete.");
     for (int c = 0; c < num_components && c < (int)nc; ++c) {
