@@ -52,8 +52,8 @@ bool xz_encode_try(const uint8_t* data, size_t size, std::string& out, const cha
 // set_write_behind(true); default off = the reference's behaviour, every file
 // written before compress() returns).  On: compress() queues each component's
 // payload and returns; host_threads() workers encode and write the files.
-// They are complete once flush_writes() returns, before decompress() reads, and
-// at normal process exit.  set_write_behind(false) flushes first.  An encoder
+// They are complete once flush_writes() returns, before decompress() reads one
+// (flush_writes(path): that file's pending writes only), and at normal process exit.  set_write_behind(false) flushes first.  An encoder
 // failure in a worker is reported (log + exit(EXIT_FAILURE), as compress()
 // would) by the next flush, or at exit.
 bool write_behind();
@@ -61,5 +61,6 @@ void set_write_behind(bool on);
 void write_behind_submit(std::string payload, std::string path);
 void note_write_behind_used();
 void flush_writes();
+void flush_writes(const std::string& path);
 
 }  // namespace wavelet_amd

@@ -99,7 +99,7 @@ Box3D inverse_wavelet_decompose(std::vector<float> flat, int x, int y, int z) {
 }
 
 Box3D decompress(std::string file_path, int /*time*/, int /*level*/, int /*component*/, int /*box_idx*/) {
-    flush_writes();  // a file compress() queued (write-behind, opt-in) is complete before it is read
+    flush_writes(file_path);  // this file, if compress() queued it (write-behind, opt-in), is complete first
     const std::string payload = xz_decompress(read_file(file_path));
     if (payload.size() < 20) fatal("Deserialization failed: payload shorter than its header");
     int32_t hdr[5];

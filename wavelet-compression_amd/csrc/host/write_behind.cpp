@@ -10,8 +10,11 @@
 // the caller's loop moves on to the next boxes.  Every file is complete, with
 // the bytes compress() would have written, by the time
 //   * flush_writes() returns (explicit),
-//   * decompress() reads (it flushes first: -estimate reads what -c wrote), or
-//   * the process exits normally (the queue's static destructor flushes).
+//   * decompress() reads it (it waits for that file's pending writes only:
+//     -estimate reads what -c wrote), or
+//   * the process exits normally (an atexit handler drains the queue; the
+//     queue itself is never destroyed, so a thread still blocked in submit()
+//     at exit never waits on a destroyed condition variable).
 // A file that cannot be opened is skipped, as in compress(); an encoder
 // failure (compress() would log and exit) is logged and exits the process from
 // the next flush, or at exit, once every other queued file is written (a
@@ -24,8 +27,10 @@
 #include <cstdlib>
 #include <deque>
 #include <fstream>
+#include <filesystem>
 #include <mutex>
 #include <thread>
+#include <unordered_map>
 
 #include "host_ctx.h"
 #include "wavelet_amd/xz_pool.h"
@@ -39,7 +44,16 @@ std::atomic<int> g_on{-1};  // -1: not chosen yet ($WCAMD_WRITE_BEHIND)
 struct Job {
     std::string payload;
     std::string path;
+    std::string key;  // path_key(path)
 };
+
+// A queued file's key: its absolute, lexically normal path (compress() joins
+// std::filesystem paths, the -d loop concatenates strings).
+std::string path_key(const std::string& p) {
+    std::error_code ec;
+    std::filesystem::path a = std::filesystem::absolute(p, ec);
+    return (ec ? std::filesystem::path(p) : a).lexically_normal().string();
+}
 
 class Writer {
 public:
@@ -48,20 +62,18 @@ public:
         const long v = mb ? std::atol(mb) : 0;
         limit_ = (uint64_t)(v > 0 ? v : 2048) << 20;
         const int n = std::max(1, host_threads());
-        for (int i = 0; i < n; ++i) workers_.emplace_back([this] { run(); });
+        // detached: the Writer lives until the process ends (writer())
+        for (int i = 0; i < n; ++i) std::thread([this] { run(); }).detach();
     }
-    ~Writer() {
+    // At exit (atexit handler): every queued file written; an encoder failure
+    // reported, failing the process as compress() would have.
+    void at_exit() {
         drain();
-        if (!error_.empty()) {  // at exit: report, and fail the process as compress() would have
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!error_.empty()) {
             std::fprintf(stderr, "[error] %s\n", error_.c_str());
             std::_Exit(EXIT_FAILURE);
         }
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-        }
-        work_.notify_all();
-        for (auto& t : workers_) t.join();
     }
     void submit(std::string payload, std::string path) {
         std::unique_lock<std::mutex> lk(mu_);
@@ -70,15 +82,23 @@ public:
         room_.wait(lk, [&] { return queued_ == 0 || queued_ + b <= limit_; });
         queued_ += b;
         ++pending_;
-        q_.push_back(Job{std::move(payload), std::move(path)});
+        std::string key = path_key(path);
+        ++paths_[key];
+        q_.push_back(Job{std::move(payload), std::move(path), std::move(key)});
         lk.unlock();
         work_.notify_one();
     }
-    void flush() {
-        drain();
+    // Every queued file (path empty), or only `path`'s pending writes.
+    void flush(const std::string* path = nullptr) {
         std::string e;
         {
-            std::lock_guard<std::mutex> lk(mu_);
+            std::unique_lock<std::mutex> lk(mu_);
+            if (path) {
+                const std::string key = path_key(*path);
+                done_.wait(lk, [&] { return paths_.find(key) == paths_.end(); });
+            } else {
+                done_.wait(lk, [&] { return pending_ == 0; });
+            }
             e = error_;
         }
         if (!e.empty()) fatal(e);
@@ -94,8 +114,7 @@ private:
             Job j;
             {
                 std::unique_lock<std::mutex> lk(mu_);
-                work_.wait(lk, [&] { return stop_ || !q_.empty(); });
-                if (q_.empty()) return;  // stop_ with nothing left
+                work_.wait(lk, [&] { return !q_.empty(); });
                 j = std::move(q_.front());
                 q_.pop_front();
             }
@@ -112,8 +131,11 @@ private:
                 std::lock_guard<std::mutex> lk(mu_);
                 if (err && error_.empty()) error_ = std::string(err) + ": " + j.path;
                 queued_ -= j.payload.size();
-                if (--pending_ == 0) done_.notify_all();
+                --pending_;
+                auto it = paths_.find(j.key);
+                if (it != paths_.end() && --it->second == 0) paths_.erase(it);
             }
+            done_.notify_all();  // a full flush or a one-file wait may be done
             room_.notify_all();
         }
     }
@@ -123,14 +145,20 @@ private:
     std::deque<Job> q_;
     uint64_t queued_ = 0, limit_ = 0;
     size_t pending_ = 0;  // queued + being written
+    std::unordered_map<std::string, size_t> paths_;  // path_key -> its queued + in-progress writes
     std::string error_;   // the first encoder failure
-    bool stop_ = false;
-    std::vector<std::thread> workers_;
 };
 
 Writer& writer() {
-    static Writer w;  // destroyed at exit: every queued file is written first
-    return w;
+    // never destroyed (its workers and condition variables outlive every
+    // caller); drained by an atexit handler registered after it is built, so
+    // it runs before the destructors of statics built earlier
+    static Writer* w = [] {
+        Writer* p = new Writer();
+        std::atexit([] { writer().at_exit(); });
+        return p;
+    }();
+    return *w;
 }
 
 }  // namespace
@@ -158,6 +186,10 @@ static std::atomic<bool> g_used{false};
 
 void flush_writes() {
     if (g_used.load(std::memory_order_acquire)) writer().flush();
+}
+
+void flush_writes(const std::string& path) {
+    if (g_used.load(std::memory_order_acquire)) writer().flush(&path);
 }
 
 void note_write_behind_used() { g_used.store(true, std::memory_order_release); }
