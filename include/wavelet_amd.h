@@ -28,8 +28,9 @@
  *   - Device buffers of cells, payloads, coefficients and reconstructions must
  *     be 16-byte aligned (hipMalloc and torch allocations are); offsets,
  *     kept counts, row indexes and RMSE outputs need their element alignment;
- *     original cells of the RMSE calls any element alignment.  Otherwise
- *     WC_ERR_INVALID.
+ *     both inputs of wc_rmse (the original cells and the reconstruction) and
+ *     the original cells of the fused calls, any element alignment (wc_rmse
+ *     only reads them).  Otherwise WC_ERR_INVALID.
  *   - One context per device per host thread.  The context owns its stream and
  *     its scratch memory; the caller owns every buffer it passes.
  *
@@ -257,7 +258,8 @@ int wc_inverse_flat(wc_ctx* ctx, const float* d_flat, const wc_unit* units, int 
 int wc_inverse_flat_host(wc_ctx* ctx, const float* flat, const wc_unit* units, int n, float* out);
 
 /* Per-unit RMSE between original cells (fp64 narrowed, or fp32) and fp32
- * reconstructions; d_rmse: n doubles (device). */
+ * reconstructions; d_rmse: n doubles (device).  d_orig and d_regen at any
+ * element alignment (vector loads where both bases allow them). */
 int wc_rmse(wc_ctx* ctx, const void* d_orig, int dtype, const float* d_regen,
             const wc_unit* units, int n, double* d_rmse);
 int wc_rmse_host(wc_ctx* ctx, const void* orig, int dtype, const float* regen,
@@ -282,7 +284,8 @@ int wc_inverse_rmse(wc_ctx* ctx, const uint8_t* d_payload, const uint64_t* d_off
  * payloads (the row index kernel of wc_inverse, a third of its time).
  *
  *   Row index layout (caller-owned device buffer, wc_rowindex_bytes): unit u
- *   owns W*H + 1 entries of 8 bytes, after the entries of units 0..u-1.  Entry
+ *   owns W*H + 1 entries of 8 bytes (none when it has no cells), after the
+ *   entries of units 0..u-1.  Entry
  *   r < W*H of flat row r = I*H + J (the D coefficients r*D .. r*D + D - 1 of
  *   the reference's flat order, src/compressor.cpp:178-181) is {uint32 k,
  *   uint32 p_k - r*D}: k the first pair whose flat position p_k is >= r*D;

@@ -72,6 +72,10 @@ def test_host_helpers(wc):
     assert L.wc_payload_bound(units, n) == 4 + sum(24 + 8 * c for c in (64 ** 3, 64, 105))
     assert units[1].cell_offset % 4 == 0 and units[2].cell_offset % 4 == 0
     assert L.wc_version().startswith(b"wavelet_amd")
+    # row index: W*H + 1 entries of 8 B per unit with cells, none for an empty unit
+    assert wc.capi.rowindex_bytes(units, n) == 8 * (64 * 64 + 1 + 8 * 4 + 1 + 3 * 5 + 1)
+    e_units, e_n, _ = wc.capi.make_units([(0, 4, 4), (2, 2, 8), (1024, 1024, 0)])
+    assert wc.capi.rowindex_bytes(e_units, e_n) == 8 * (2 * 2 + 1)
 
 
 def test_null_context_is_rejected(wc):

@@ -149,7 +149,8 @@ def payload_bound(units, n) -> int:
 
 
 def rowindex_bytes(units, n) -> int:
-    """Bytes of a batch's row index (wc_rowindex_bytes: W*H + 1 entries of 8 B per unit)."""
+    """Bytes of a batch's row index (wc_rowindex_bytes: W*H + 1 entries of 8 B per unit
+    with cells, none for an empty unit)."""
     return int(load_library().wc_rowindex_bytes(units, n))
 
 

@@ -137,7 +137,8 @@ uint64_t wc_cell_count(const wc_unit* units, int n) {
 
 uint64_t wc_rowindex_bytes(const wc_unit* units, int n) {
     uint64_t e = 0;
-    for (int i = 0; i < n; ++i) e += (uint64_t)units[i].nx * units[i].ny + 1;
+    for (int i = 0; i < n; ++i)  // W*H + 1 entries per unit with cells, none for an empty unit
+        if ((uint64_t)units[i].nx * units[i].ny * units[i].nz) e += (uint64_t)units[i].nx * units[i].ny + 1;
     return 8 * e;
 }
 

@@ -432,26 +432,15 @@ __device__ __forceinline__ void block_key_max(unsigned long long v, unsigned lon
 
 // Coefficient-magnitude histogram of the opt-in global-threshold mode
 // (wc_hist.hip, k_transform_hist): bin = fp32 bits of |c| >> kHistShift,
-// NaN not counted.  Wave-aggregated LDS increment: the coefficients of a tile
-// crowd into a few bins, and same-address LDS atomics of one wave serialize,
-// so one round takes the bin of the first pending lane, counts every lane
-// with that bin by ballot and adds the count with ONE atomic; lanes still
-// pending add their own.
+// NaN not counted.  One LDS atomic per coefficient: a wave-aggregated form
+// (the first pending lane's bin counted by ballot, one atomic for its lanes)
+// measured 1.6 ms slower in C4's K1 (profiles/r06/experiments/gpu_hist_split.txt).
 constexpr int kHistBins = 4096;
 constexpr int kHistShift = 19;
 
 __device__ __forceinline__ void hist_add(uint32_t* h, float v, bool valid) {
     const uint32_t m = __float_as_uint(v) & 0x7fffffffu;
-    const uint32_t bin = m >> kHistShift;
-    bool pending = valid && m <= 0x7f800000u;  // NaN is not counted
-    const unsigned long long act = __ballot(pending);
-    if (!act) return;
-    const int leader = __ffsll((long long)act) - 1;
-    const uint32_t lb = __builtin_amdgcn_readlane(bin, leader);
-    const unsigned long long same = __ballot(pending && bin == lb);
-    if ((int)(threadIdx.x & 63) == leader) atomicAdd(h + lb, (uint32_t)__popcll(same));
-    pending = pending && bin != lb;
-    if (pending) atomicAdd(h + bin, 1u);
+    if (valid && m <= 0x7f800000u) atomicAdd(h + (m >> kHistShift), 1u);  // NaN is not counted
 }
 
 }  // namespace wc

@@ -219,9 +219,10 @@ int get_plan(wc_ctx* c, const wc_unit* units, int n) {
         d.ntz = (d.nbz + (1 << d.lbz) - 1) >> d.lbz;
         d.pay_off = pay_cursor;  // slot of 20 + 8*ncells bytes + 4 pad: next slot stays == 4 (mod 8)
         pay_cursor += 24 + 8 * d.ncells;
-        // row index entries (include/wavelet_amd.h wc_rowindex_bytes): W*H + 1 per unit, every unit
+        // row index entries (include/wavelet_amd.h wc_rowindex_bytes): W*H + 1 per unit with
+        // cells, none for an empty one (which writes and reads no entry)
         d.row_off = P.rowinfo_entries;
-        P.rowinfo_entries += (uint64_t)u.nx * u.ny + 1;
+        if (d.ncells) P.rowinfo_entries += (uint64_t)u.nx * u.ny + 1;
         d.coef_off = (coef_cursor + 31) & ~uint64_t(31);  // 128 B: sparse-staging segments align
         coef_cursor = d.coef_off + d.ncells;
         if (d.ncells == 0) continue;
