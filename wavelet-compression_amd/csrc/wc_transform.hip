@@ -200,9 +200,12 @@ __global__ __launch_bounds__(kThreads) void k_transform_fast_pf(
 // coefficient-magnitude histogram (wc_hist.hip's bins) folded into the store
 // of phase 2, where every coefficient is already in registers, so no kernel
 // re-reads the staged coefficients for it (4 B per coefficient saved).
-// Persistent (workgroup b: tiles b, b + G, ...): the workgroup's LDS bins
-// (16 KiB past the tile rows) add up its tiles and reach `hist` once, as one
-// 64-bit atomic per nonzero bin, instead of once per tile.
+// Workgroup b takes tiles b, b + G, ... with G = tiles / kHistTilesPerWg (at
+// least the resident workgroups): its LDS bins (16 KiB past the tile rows) add
+// up its ~32 tiles and reach `hist` once, as one 64-bit atomic per nonzero
+// bin.  C4 K1: 8.38-8.43 ms at 32 tiles per workgroup, 8.44-8.46 at 16, 8.54-
+// 8.60 at 64, 8.82-8.93 with a resident (persistent) grid, 12.5 at one tile
+// per workgroup (the flush atomics) (profiles/r06/experiments/gpu_hist_tpw.txt).
 template <typename T>
 __global__ __launch_bounds__(kThreads) void k_transform_hist(
     const T* __restrict__ cells, const UnitDev* __restrict__ units, const XTile* __restrict__ tiles,
@@ -292,13 +295,16 @@ uint32_t transform_hist_grid(size_t lds) {
     return (uint32_t)per_cu * (uint32_t)ncu;
 }
 
+constexpr uint32_t kHistTilesPerWg = 32;
+
+// grid: the resident workgroups of k_transform_hist (transform_hist_grid).
 hipError_t launch_transform_hist(hipStream_t st, const void* cells, int dtype, const UnitDev* units,
                                  const XTile* tiles, uint32_t ntiles, size_t lds_fast, float* out,
                                  unsigned long long* keys, unsigned long long* hist, uint32_t grid) {
     if (ntiles == 0) return hipSuccess;
     const size_t lds = transform_hist_lds_bytes(lds_fast);
     const uint32_t tf = (uint32_t)((lds - 4 * kHistBins) / sizeof(float));
-    const uint32_t g = std::min(ntiles, std::max(1u, grid));
+    const uint32_t g = std::min(ntiles, std::max({1u, grid, (ntiles + kHistTilesPerWg - 1) / kHistTilesPerWg}));
     if (dtype == 1)
         k_transform_hist<double><<<g, kThreads, lds, st>>>((const double*)cells, units, tiles, ntiles, tf, out, keys,
                                                            hist);
