@@ -17,13 +17,13 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 OUT = ROOT / "gpurun_out"
-WORKLOADS = ("c2", "c3", "c4", "c5", "f32_64")
+WORKLOADS = ("c2", "c3", "c4", "c5", "f32_64", "c4_hist")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("log")
-    ap.add_argument("--round", default="r05")
+    ap.add_argument("--round", default="r06")
     a = ap.parse_args()
     dst = ROOT / "profiles" / a.round
     dst.mkdir(parents=True, exist_ok=True)
@@ -52,7 +52,9 @@ def main():
     log = Path(a.log).read_text().splitlines()
     rc = [i for i, s in enumerate(log) if s.startswith("== gputest rc=")]
     if rc:
-        body = [s for s in log[rc[0] + 1:] if not s.startswith("== ")]
+        full = OUT / "gputest.log"  # the suite's whole output (the call's log holds its tail)
+        body = (full.read_text().splitlines() if full.exists()
+                else [s for s in log[rc[0] + 1:] if not s.startswith("== ")])
         head = (f"# python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread (tools/gpu_profile.sh "
                 f"GPUTEST=1, kernel-source hash {pmc['kernel_sources_sha']}, commit {pmc['git']})")
         (dst / "gpu_tests.txt").write_text("\n".join([head] + body) + "\n")
