@@ -897,7 +897,7 @@ def plumbing_run(args, d: Dist):
                         "expected_total": sum(u.cells for u in bw.WORKLOADS[name]["units"]())}
     m = d.reduce({"seconds": 0.001 * (d.rank + 1), "boxes": 1})
     return {"metric": "plumbing (no kernels)", "value": None, "n_gpus": d.world, "ranks_seen": int(m["boxes"]),
-            "max_seconds": m["seconds"], "shards": shards}
+            "max_seconds": m["seconds"], "shards": shards, "dist_backend": d.backend()}
 
 
 def main():

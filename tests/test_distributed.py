@@ -190,6 +190,29 @@ def test_bench_spawns_ranks_and_merges_one_line(tmp_path):
         assert sh["rank0_span"][0] == 0 and 0 < sh["rank0_span"][1] < sh["units_total"], name
 
 
+def test_bench_force_dist_takes_the_process_group_path_at_world1(tmp_path):
+    """bench.py --force-dist at one rank: started through torch.distributed.run
+    (no WORLD_SIZE in the environment), the Dist process-group path with every
+    reduction a real collective (gloo here; RCCL on the GPU box,
+    test_gpu_rccl.py), one line naming the backend."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["WCAMD_NO_TORCH"] = "1"
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--force-dist", "--plumbing"], env=env,
+                       capture_output=True, text=True, timeout=300, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 1 and out["ranks_seen"] == 1 and out["dist_backend"] == "gloo"
+    for name, sh in out["shards"].items():
+        assert sh["cells_total"] == sh["expected_total"], name
+
+
 def test_bench_rank_failure_ends_the_job_fast(tmp_path):
     """One rank of `bench.py --gpus 2` raises before the first collective: the
     launcher exits non-zero well within the process-group timeout and leaves
