@@ -166,7 +166,8 @@ static void xz_pool_case() {
 // The write-behind queue of compress() (opt-in; the GPU test checks compress()
 // itself): payloads submitted from 4 threads through a 1 MiB bound (submit
 // waits for room), a path that cannot be opened (skipped, as compress() does),
-// a flush, and every file equal to the serial encoder's bytes.
+// a flush, and every file equal to the serial encoder's bytes; a one-file
+// flush (decompress()'s) while other files are queued.
 static void write_behind_case() {
     setenv("WCAMD_WRITE_BEHIND_MB", "1", 1);  // read when the queue starts (first submit)
     TempDir dir;
@@ -192,6 +193,20 @@ static void write_behind_case() {
         const std::string got((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
         REQUIRE(got == wavelet_amd::xz_compress(payloads[i]));
     }
+    // flush_writes(path) (what decompress() calls): that file complete, named
+    // another way (a "." component), while others may still be queued
+    const std::string big(20 + 8 * 200000, '\3');
+    for (int i = 0; i < 8; ++i)
+        wavelet_amd::write_behind_submit(big, (dir.path() / ("b" + std::to_string(i) + ".xz")).string());
+    wavelet_amd::write_behind_submit(payloads[1], (dir.path() / "one.xz").string());
+    wavelet_amd::flush_writes((dir.path() / "." / "one.xz").string());
+    {
+        std::ifstream f(dir.path() / "one.xz", std::ios::binary);
+        const std::string got((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        REQUIRE(got == wavelet_amd::xz_compress(payloads[1]));
+    }
+    wavelet_amd::flush_writes();
+    for (int i = 0; i < 8; ++i) REQUIRE(fs::file_size(dir.path() / ("b" + std::to_string(i) + ".xz")) > 0);
 }
 
 // The optional faster xz preset: preset parsing, the

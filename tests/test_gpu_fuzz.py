@@ -1,0 +1,133 @@
+"""Seeded random batches through every device entry point, against the CPU oracle.
+
+The other GPU tests pin chosen shapes, the bench workloads at full size and
+the special boxes one by one; this one mixes them the way a caller's batch
+would: random dims (odd and even, thin and cubic, sizes that land on the
+specialised, fast, generic and sparse-staging paths), random cell offsets
+(aligned and not), random fields per unit (the smooth SURVEY field, wide-range
+Gaussians, constants of either sign, all-zero, subnormals, NaN / inf
+sprinkled in), one random float32 keep per batch (the reference's Config::keep,
+src/argparse.h:13), fp64 and fp32 cells.  Per batch:
+
+  * wc_forward: every payload = oracle compress() minus xz
+    (src/compressor.cpp:192-248);
+  * wc_forward_rows + wc_inverse_rows with the fused RMSE: the same payloads;
+    every reconstruction = oracle decompress() (src/decompressor.cpp:238-255)
+    bit for bit; every RMSE = calc_rmse_per_box (src/calc-loss.cpp:12-43)
+    within 1e-12 relative (NaN where the oracle's is NaN);
+  * wc_inverse from the payloads alone: the same reconstructions.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SIZES = (1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 15, 16, 17, 24, 31, 32, 33, 40, 48, 63, 64)
+
+
+def _dims(rng, n):
+    out = []
+    for _ in range(n):
+        if rng.random() < 0.1:  # a few large, specialised-shape boxes
+            out.append(tuple(int(x) for x in rng.choice([64, 96, 128], size=3)))
+        else:
+            out.append(tuple(int(x) for x in rng.choice(SIZES, size=3)))
+    return out
+
+
+def _field(rng, O, i, dims):
+    W, H, D = dims
+    kind = rng.integers(0, 8)
+    if kind <= 2:  # the SURVEY §8(d) field
+        return O.synth_box_f64(O.unit_seed(99, 1, i, int(kind)), (W * i % 997, 7 * i, 3 * i), W, H, D)
+    if kind == 3:  # wide-range Gaussian, mixed sign
+        return rng.standard_normal((D, H, W)) * 10.0 ** rng.uniform(-30, 30)
+    if kind == 4:  # a constant of either sign (sign quirk: a negative max keeps everything)
+        return np.full((D, H, W), rng.choice([-1.0, 1.0]) * rng.uniform(0.1, 1e3))
+    if kind == 5:  # all zero
+        return np.zeros((D, H, W))
+    if kind == 6:  # subnormal-scale values (fp32 denormals survive: no FTZ)
+        return rng.standard_normal((D, H, W)) * 1e-41
+    b = rng.standard_normal((D, H, W)) * 100.0  # specials sprinkled in
+    flat = b.reshape(-1)
+    for v in (np.nan, np.inf, -np.inf, 0.0, -0.0):
+        if flat.size and rng.random() < 0.5:
+            flat[rng.integers(0, flat.size)] = v
+    return b
+
+
+def _batch(O, seed):
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(20, 120))
+    dims = _dims(rng, n)
+    boxes = [_field(rng, O, i, d) for i, d in enumerate(dims)]
+    dtype = np.float64 if seed % 2 == 0 else np.float32
+    # cell offsets: packed with random gaps, every third unit at an odd element offset
+    offs, cur = [], 0
+    for i, (W, H, D) in enumerate(dims):
+        cur += int(rng.integers(0, 9))
+        if i % 3 == 0 and cur % 2 == 0:
+            cur += 1
+        offs.append(cur)
+        cur += W * H * D
+    keep = float(np.float32(rng.choice([rng.uniform(0.5, 0.99999), 0.999, 0.0, 1.0, 1.5])))
+    return boxes, dims, offs, cur, dtype, keep
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_batch_all_entry_points(wc, ctx, oracle, seed):
+    import torch
+    boxes, dims, offs, extent, dtype, keep = _batch(oracle, seed)
+    units, n, ext = wc.capi.make_units(dims, offsets=offs)
+    assert ext == extent
+    host = np.zeros(max(extent, 1), dtype)
+    for o, b in zip(offs, boxes):
+        host[o:o + b.size] = b.ravel().astype(dtype)
+    code = wc.capi.WC_F64 if dtype == np.float64 else wc.capi.WC_F32
+    dev = torch.device("cuda", 0)
+    cells = torch.from_numpy(host).to(dev)
+    cap = wc.capi.payload_bound(units, n)
+    rb = wc.capi.rowindex_bytes(units, n)
+
+    def bufs():
+        return (torch.zeros(cap, dtype=torch.uint8, device=dev), torch.zeros(n + 1, dtype=torch.int64, device=dev),
+                torch.zeros(n, dtype=torch.int32, device=dev))
+
+    pay, po, kept = bufs()
+    pay2, po2, kept2 = bufs()
+    rows = torch.zeros(max(rb // 8, 1), dtype=torch.int64, device=dev)
+    out = torch.full((max(extent, 1),), float("nan"), dtype=torch.float32, device=dev)
+    out2 = torch.full((max(extent, 1),), float("nan"), dtype=torch.float32, device=dev)
+    rmse = torch.full((n,), -1.0, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    ctx.forward(cells.data_ptr(), code, units, n, keep, pay.data_ptr(), cap, po.data_ptr(), kept.data_ptr())
+    ctx.forward_rows(cells.data_ptr(), code, units, n, keep, pay2.data_ptr(), cap, po2.data_ptr(), kept2.data_ptr(),
+                     rows.data_ptr(), rb)
+    ctx.inverse_rows(pay2.data_ptr(), po2.data_ptr(), units, n, rows.data_ptr(), out.data_ptr(), cells.data_ptr(),
+                     code, rmse.data_ptr())
+    ctx.inverse(pay.data_ptr(), po.data_ptr(), units, n, out2.data_ptr())
+    ctx.synchronize()
+    P, O_, K = pay.cpu().numpy(), po.cpu().numpy(), kept.cpu().numpy()
+    assert np.array_equal(O_, po2.cpu().numpy()) and np.array_equal(K, kept2.cpu().numpy())
+    P2 = pay2.cpu().numpy()
+    R, R2, E = out.cpu().numpy(), out2.cpu().numpy(), rmse.cpu().numpy()
+    for i, b in enumerate(boxes):
+        b32 = oracle.narrow(b) if dtype == np.float64 else b.astype(np.float32)
+        want, wk = oracle.compress_payload(b32, keep)
+        a = int(O_[i])
+        got = P[a:a + 20 + 8 * int(K[i])].tobytes()
+        assert got == want and int(K[i]) == wk, (seed, i, dims[i], keep)
+        assert P2[a:a + len(want)].tobytes() == want, (seed, i, "forward_rows")
+        if b.size == 0:
+            continue
+        back = oracle.decompress_payload(want).ravel()
+        o = offs[i]
+        assert R[o:o + b.size].tobytes() == back.tobytes(), (seed, i, dims[i], "inverse_rows")
+        assert R2[o:o + b.size].tobytes() == back.tobytes(), (seed, i, dims[i], "inverse")
+        ref = oracle.rmse(b32, back.reshape(b32.shape))
+        if np.isnan(ref):
+            assert np.isnan(E[i]), (seed, i, E[i])
+        elif np.isinf(ref):
+            assert E[i] == ref, (seed, i, E[i], ref)
+        else:
+            assert abs(E[i] - ref) <= 1e-12 * abs(ref), (seed, i, dims[i], E[i], ref)
