@@ -96,6 +96,12 @@ public:
             if (path) {
                 const std::string key = path_key(*path);
                 done_.wait(lk, [&] { return paths_.find(key) == paths_.end(); });
+                // a file queued under another spelling (e.g. relative to a working
+                // directory that has changed since) is not found by its key: if the
+                // file is not there yet, drain everything
+                std::error_code ec;
+                if (pending_ != 0 && !std::filesystem::exists(*path, ec))
+                    done_.wait(lk, [&] { return pending_ == 0; });
             } else {
                 done_.wait(lk, [&] { return pending_ == 0; });
             }
