@@ -93,6 +93,7 @@ public:
         std::string e;
         {
             std::unique_lock<std::mutex> lk(mu_);
+            ++waiters_;
             if (path) {
                 const std::string key = path_key(*path);
                 done_.wait(lk, [&] { return paths_.find(key) == paths_.end(); });
@@ -105,6 +106,7 @@ public:
             } else {
                 done_.wait(lk, [&] { return pending_ == 0; });
             }
+            --waiters_;
             e = error_;
         }
         if (!e.empty()) fatal(e);
@@ -113,7 +115,9 @@ public:
 private:
     void drain() {
         std::unique_lock<std::mutex> lk(mu_);
+        ++waiters_;
         done_.wait(lk, [&] { return pending_ == 0; });
+        --waiters_;
     }
     void run() {
         for (;;) {
@@ -133,6 +137,7 @@ private:
                         f.write(xz.data(), (std::streamsize)xz.size());
                 }
             }
+            bool wake;
             {
                 std::lock_guard<std::mutex> lk(mu_);
                 if (err && error_.empty()) error_ = std::string(err) + ": " + j.path;
@@ -140,8 +145,9 @@ private:
                 --pending_;
                 auto it = paths_.find(j.key);
                 if (it != paths_.end() && --it->second == 0) paths_.erase(it);
+                wake = waiters_ != 0;
             }
-            done_.notify_all();  // a full flush or a one-file wait may be done
+            if (wake) done_.notify_all();  // a full flush or a one-file wait may be done
             room_.notify_all();
         }
     }
@@ -152,6 +158,7 @@ private:
     uint64_t queued_ = 0, limit_ = 0;
     size_t pending_ = 0;  // queued + being written
     std::unordered_map<std::string, size_t> paths_;  // path_key -> its queued + in-progress writes
+    size_t waiters_ = 0;  // threads in flush() / drain()
     std::string error_;   // the first encoder failure
 };
 
