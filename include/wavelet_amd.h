@@ -217,7 +217,8 @@ int wc_round_trip_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit*
  *   wc_forward_stage: transform a batch into the context's coefficient scratch
  *     (the first half of wc_forward) and, when d_hist is not null, ADD the
  *     batch's magnitude histogram to d_hist (WC_HIST_BINS uint64 on the device;
- *     bin = fp32 bits of |c| >> WC_HIST_SHIFT, NaN not counted).
+ *     bin = fp32 bits of |c| >> WC_HIST_SHIFT, NaN not counted).  The bins are
+ *     counted as the transform stages the coefficients (no second pass over them).
  *   (caller: all-reduce d_hist over ranks, e.g. RCCL sum of 4096 uint64)
  *   wc_hist_threshold: host-only; the fp32 threshold that keeps every
  *     coefficient whose bin is >= the highest bin b at which the count of
@@ -326,7 +327,8 @@ int wc_decompose_host(wc_ctx* ctx, const void* cells, int dtype, const wc_unit* 
 #define WC_STAGE_DECODE 2     /* K5  rle_decode */
 #define WC_STAGE_INVERSE 3    /* K6  inverse transform */
 #define WC_STAGE_RMSE 4       /* K7  */
-#define WC_STAGE_HIST 5       /* coefficient-magnitude histogram (wc_forward_stage with d_hist) */
+#define WC_STAGE_HIST 5       /* histogram pass of generic units (wc_forward_stage with d_hist; the fast
+                                 units' bins are counted inside the transform stage) */
 #define WC_STAGE_PAIRS 6      /* header check + pair counts of wc_inverse_rows with a caller row index */
 #define WC_NUM_STAGES 7
 int wc_profile_enable(wc_ctx* ctx, int on);
