@@ -131,3 +131,42 @@ def test_random_batch_all_entry_points(wc, ctx, oracle, seed):
             assert E[i] == ref, (seed, i, E[i], ref)
         else:
             assert abs(E[i] - ref) <= 1e-12 * abs(ref), (seed, i, dims[i], E[i], ref)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_batch_global_threshold_mode(wc, ctx, oracle, seed):
+    """The opt-in global-threshold mode on the same random batches: the
+    histogram (counted inside K1 for the fast units, by k_hist for the generic
+    ones) equals the oracle's bins, and the payloads at the thresholds of three
+    quantiles equal the reference's mask + RLE + serialize at that threshold."""
+    import torch
+    boxes, dims, offs, extent, dtype, _ = _batch(oracle, seed + 10)
+    units, n, _ = wc.capi.make_units(dims, offsets=offs)
+    host = np.zeros(max(extent, 1), dtype)
+    for o, b in zip(offs, boxes):
+        host[o:o + b.size] = b.ravel().astype(dtype)
+    code = wc.capi.WC_F64 if dtype == np.float64 else wc.capi.WC_F32
+    dev = torch.device("cuda", 0)
+    cells = torch.from_numpy(host).to(dev)
+    cap = wc.capi.payload_bound(units, n)
+    hist = torch.zeros(wc.capi.HIST_BINS, dtype=torch.int64, device=dev)
+    pay = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    po = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    kept = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    ctx.forward_stage(cells.data_ptr(), code, units, n, hist.data_ptr())
+    ctx.synchronize()
+    h = hist.cpu().numpy().view(np.uint64)
+    b32 = [oracle.narrow(b) if dtype == np.float64 else b.astype(np.float32) for b in boxes]
+    with np.errstate(all="ignore"):
+        want = sum(oracle.magnitude_hist(oracle.wavelet_decompose(b)) for b in b32)
+    assert np.array_equal(h, want), seed
+    for q in (0.3, 0.9, 0.999):
+        t, r = wc.capi.hist_threshold(h, q)
+        ctx.forward_emit(units, n, 0.0, t, pay.data_ptr(), cap, po.data_ptr(), kept.data_ptr())
+        ctx.synchronize()
+        P, O_, K = pay.cpu().numpy(), po.cpu().numpy(), kept.cpu().numpy()
+        assert int(K.astype(np.int64).sum()) == r, (seed, q)
+        for i, b in enumerate(b32):
+            a = int(O_[i])
+            assert P[a:a + 20 + 8 * int(K[i])].tobytes() == oracle.compress_payload_thresh(b, t), (seed, q, i, dims[i])
