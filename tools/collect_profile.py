@@ -48,6 +48,8 @@ def main():
                      "same call: oracle transform+threshold+RLE+serialize + xz preset 6), per box of this layout's "
                      "mean size")}
         d["speedup_vs_cpu_single_thread"] = d["compress_cells_per_s"] / per
+        if "write_behind" in d:
+            d["write_behind"]["speedup_vs_cpu_single_thread"] = d["write_behind"]["compress_cells_per_s"] / per
         (dst / "dropin.json").write_text(json.dumps(d, indent=1))
     log = Path(a.log).read_text().splitlines()
     rc = [i for i, s in enumerate(log) if s.startswith("== gputest rc=")]

@@ -78,6 +78,8 @@ __device__ __forceinline__ unsigned long long wave_max_u64_u(unsigned long long 
 // Load the x-pair (x, x+1) of a row as fp32 (fp64 cells narrowed RNE,
 // src/preprocess.cpp:78).  `vec`: both elements in one aligned vector load.
 // NT: non-temporal (streaming) vector load: the cells are read exactly once.
+// Every K1 form loads its cells this way (round 6, profiles/r06/experiments/
+// gpu_nt_cells.txt: C2 forward -6 %, K1 -12 % with the emit after it +6 %).
 using f64x2 = double __attribute__((ext_vector_type(2)));
 using f32x2 = float __attribute__((ext_vector_type(2)));
 using f32x4 = float __attribute__((ext_vector_type(4)));

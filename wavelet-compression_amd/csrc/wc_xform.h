@@ -74,7 +74,7 @@ __device__ __forceinline__ void xform_generic_p1(const T* __restrict__ src, cons
             for (int dy = 0; dy < 2; ++dy) {
                 if ((dz == 0 || pz) && (dy == 0 || py)) {
                     const T* p = src + 2 * (int64_t)bx + sy * (2 * by + dy) + sz * (2 * bz + dz);
-                    load_xpair<T>(p, px, vec, v[dz][dy][0], v[dz][dy][1]);
+                    load_xpair<T, true>(p, px, vec, v[dz][dy][0], v[dz][dy][1]);
                 } else {
                     v[dz][dy][0] = 0.0f;
                     v[dz][dy][1] = 0.0f;
@@ -197,7 +197,7 @@ __device__ __forceinline__ uint32_t xform_fast_p1(const T* __restrict__ src, con
             for (int zp = 0; zp < 4; ++zp)
 #pragma unroll
                 for (int dy = 0; dy < 2; ++dy)
-                    load_xpair<T>(p0 + sz * (4 * h + zp) + sy * dy, true, vec, v[zp][dy][0], v[zp][dy][1]);
+                    load_xpair<T, true>(p0 + sz * (4 * h + zp) + sy * dy, true, vec, v[zp][dy][0], v[zp][dy][1]);
 #pragma unroll
             for (int qq = 0; qq < 2; ++qq) {
                 const int q = 2 * h + qq;
@@ -273,7 +273,7 @@ __device__ __forceinline__ bool fast_load(const T* __restrict__ src, const UnitD
 #pragma unroll
     for (int zp = 0; zp < 8; ++zp)
 #pragma unroll
-        for (int dy = 0; dy < 2; ++dy) load_xpair<T>(p0 + sz * zp + sy * dy, true, vec, c.v[zp][dy][0], c.v[zp][dy][1]);
+        for (int dy = 0; dy < 2; ++dy) load_xpair<T, true>(p0 + sz * zp + sy * dy, true, vec, c.v[zp][dy][0], c.v[zp][dy][1]);
     return true;
 }
 
