@@ -230,9 +230,23 @@ int main(int argc, char** argv) {
     uint64_t* d_hist = nullptr;
     std::vector<uint64_t> h_hist(WC_HIST_BINS);
     if (hist_q >= 0.0) CK(hipMalloc(&d_hist, 8 * WC_HIST_BINS));
+    // WCB_SPLIT=us (diagnostic): the reference rule as wc_forward_stage + wc_synchronize + an idle
+    // gap of `us` microseconds on the host + wc_forward_emit (stage + emit == wc_forward): does
+    // the emit's time depend on how long ago K1 finished?
+    const char* split_env = std::getenv("WCB_SPLIT");
+    const int split_us = split_env ? std::atoi(split_env) : -1;
     auto fwd = [&]() {
         int rc = WC_OK;
-        if (hist_q >= 0.0) {
+        if (split_us >= 0 && hist_q < 0.0) {
+            if ((rc = wc_forward_stage(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, nullptr)) == WC_OK &&
+                (rc = wc_synchronize(ctx)) == WC_OK) {
+                const auto t0 = std::chrono::steady_clock::now();
+                while (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() <
+                       split_us) {
+                }
+                rc = wc_forward_emit(ctx, units.data(), boxes, keep, nullptr, payload, cap, offsets, kept);
+            }
+        } else if (hist_q >= 0.0) {
             float t = 0.0f;
             CK(hipMemset(d_hist, 0, 8 * WC_HIST_BINS));
             if ((rc = wc_forward_stage(ctx, cells, f64 ? WC_F64 : WC_F32, units.data(), boxes, d_hist)) == WC_OK &&
