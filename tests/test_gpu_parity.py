@@ -988,6 +988,45 @@ def test_s32_shape_special_values(wc, ctx, oracle):
                 assert int(kept[i]) == wk
 
 
+def test_32xHx32_shape_special_values(wc, ctx, oracle):
+    """The 16 x 4 x 16-block transform tiles of 32 x H x 32 boxes (H % 8 == 0: the
+    32^3 units of C3 / C4; 16-coefficient sparse segments; a specialised body for
+    them was measured and not kept, profiles/r06/experiments/gpu_s16.txt) on the
+    same quirks as the S32 test above: NaN at flat index 0 and later, +/-inf,
+    +M / -M ties in one block and across tiles, -0.0, constant fields, denormals,
+    smooth noise of either sign — fp32 and fp64, keep 0.5, 0.999f, 1.0, 1.5."""
+    def box(shape, fill, edits=()):
+        b = np.full(shape, fill, np.float32)
+        for idx, v in edits:
+            b[idx] = v
+        return b
+    s, c, t = (32, 8, 32), (32, 32, 32), (32, 24, 32)  # (D, H, W)
+    rng = np.random.default_rng(16)
+    noise = (rng.standard_normal(c) * 0.05 + 300.0).astype(np.float32)
+    boxes = [
+        box(s, 2.0, [((0, 0, 0), np.nan)]),
+        box(c, 2.0, [((20, 29, 17), np.nan)]),
+        box(s, 1.0, [((5, 3, 7), np.inf)]),
+        box(t, 1.0, [((30, 21, 30), -np.inf)]),
+        box(c, 0.0, [((9, 2, 20), 8.0), ((9, 2, 21), -8.0)]),
+        box(c, 0.0, [((3, 1, 2), -8.0), ((30, 30, 31), 8.0)]),
+        box(c, 0.0, [((30, 30, 31), -8.0), ((3, 1, 2), 8.0)]),
+        box(s, 0.0, [((7, 5, 9), np.float32(-0.0)), ((8, 5, 9), np.float32(-0.0))]),
+        box(t, 3.0),
+        box(c, np.float32(1e-40), [((30, 8, 30), np.float32(3e-39))]),
+        noise,
+        -noise,
+        noise[:, :8, :] * np.float32(0.5),
+    ]
+    for keep in (0.5, KEEPS[1], 1.0, 1.5):
+        for dtype in (np.float32, np.float64):
+            got, kept = gpu_payloads(wc, ctx, [b.astype(dtype) for b in boxes], keep, dtype=dtype)
+            for i, b in enumerate(boxes):
+                want, wk = oracle.compress_payload(b, keep)
+                assert got[i] == want, (keep, dtype.__name__, i)
+                assert int(kept[i]) == wk
+
+
 @pytest.mark.parametrize("seed", [101, 202])
 def test_random_shapes_round_trip(wc, ctx, oracle, seed):
     """Seeded random batches over every tile class the planner picks (odd and even
