@@ -14,15 +14,27 @@ src/argparse.h:13), fp64 and fp32 cells.  Per batch:
   * wc_forward_rows + wc_inverse_rows with the fused RMSE: the same payloads;
     every reconstruction = oracle decompress() (src/decompressor.cpp:238-255)
     bit for bit; every RMSE = calc_rmse_per_box (src/calc-loss.cpp:12-43)
-    within 1e-12 relative (NaN where the oracle's is NaN);
+    within max(1e-12, (n + 4) 2^-53) relative for a box of n cells (NaN where
+    the oracle's is NaN).  Both sides add the same n exact double terms (a
+    float difference squared in double is exact); only the order differs (the
+    reference sums in z, y, x order, the GPU per tile then tiles in order), so
+    each sum is within (n - 1) 2^-53 of the exact one and the square root halves
+    that; the 1e-12 floor holds for the smooth fields, and the wide-range
+    Gaussian fields (ten to the +-30) reach ~1e-12 on 10^5-10^6-cell boxes
+    (seed 56 of a 300-seed soak: 1.02e-12 on a 128 x 64 x 96 box);
   * wc_inverse from the payloads alone: the same reconstructions.
 """
+import os
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 SIZES = (1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 15, 16, 17, 24, 31, 32, 33, 40, 48, 63, 64)
+# WC_FUZZ_SEEDS=N: N seeds per test instead of the suite's 6 / 4 (a longer soak; seeds >= the
+# defaults draw batches the default suite does not)
+_N = int(os.environ.get("WC_FUZZ_SEEDS", "0"))
 
 
 def _dims(rng, n):
@@ -74,7 +86,7 @@ def _batch(O, seed):
     return boxes, dims, offs, cur, dtype, keep
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(_N or 6))
 def test_random_batch_all_entry_points(wc, ctx, oracle, seed):
     import torch
     boxes, dims, offs, extent, dtype, keep = _batch(oracle, seed)
@@ -130,10 +142,11 @@ def test_random_batch_all_entry_points(wc, ctx, oracle, seed):
         elif np.isinf(ref):
             assert E[i] == ref, (seed, i, E[i], ref)
         else:
-            assert abs(E[i] - ref) <= 1e-12 * abs(ref), (seed, i, dims[i], E[i], ref)
+            tol = max(1e-12, (b.size + 4) * 2.0 ** -53)
+            assert abs(E[i] - ref) <= tol * abs(ref), (seed, i, dims[i], E[i], ref)
 
 
-@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("seed", range(_N or 4))
 def test_random_batch_global_threshold_mode(wc, ctx, oracle, seed):
     """The opt-in global-threshold mode on the same random batches: the
     histogram (counted inside K1 for the fast units, by k_hist for the generic
