@@ -88,8 +88,43 @@ def _batch(O, seed):
 
 @pytest.mark.parametrize("seed", range(_N or 6))
 def test_random_batch_all_entry_points(wc, ctx, oracle, seed):
+    _check_all_entry_points(wc, ctx, oracle, seed, seed)
+
+
+# Library options every path must produce the same bytes under (include/wavelet_amd.h
+# wc_set_option): dense staging, the ticket look-back, the worst dispatch order, a wait bound
+# of one poll (every look-back wait derives its predecessor), both of those, the dense-decode
+# inverse.
+_OPTION_SETS = {
+    "dense_staging": (("WC_OPT_SPARSE", 0),),
+    "tickets": (("WC_OPT_TICKETS", 1),),
+    "reversed_tiles": (("WC_OPT_REVERSE_TILES", 1),),
+    "spin_limit_1": (("WC_OPT_SPIN_LIMIT", 1),),
+    "reversed_spin_1": (("WC_OPT_REVERSE_TILES", 1), ("WC_OPT_SPIN_LIMIT", 1)),
+    "dense_inverse": (("WC_OPT_INVERSE_ROWS", 0),),
+}
+
+
+@pytest.mark.parametrize("seed", range(_N or 2))
+@pytest.mark.parametrize("opts", sorted(_OPTION_SETS))
+def test_random_batch_option_paths(wc, ctx, oracle, seed, opts):
+    """The random batches above through every entry point with each option set of
+    _OPTION_SETS: payloads, reconstructions and RMSEs as with the defaults (the
+    oracle's), the options restored afterwards."""
+    keys = [(getattr(wc.capi, name), v) for name, v in _OPTION_SETS[opts]]
+    before = [(k, ctx.get_option(k)) for k, _ in keys]
+    for k, v in keys:
+        ctx.set_option(k, v)
+    try:
+        _check_all_entry_points(wc, ctx, oracle, 20 + seed, (opts, seed))
+    finally:
+        for k, v in before:
+            ctx.set_option(k, v)
+
+
+def _check_all_entry_points(wc, ctx, oracle, batch_seed, seed):
     import torch
-    boxes, dims, offs, extent, dtype, keep = _batch(oracle, seed)
+    boxes, dims, offs, extent, dtype, keep = _batch(oracle, batch_seed)
     units, n, ext = wc.capi.make_units(dims, offsets=offs)
     assert ext == extent
     host = np.zeros(max(extent, 1), dtype)
