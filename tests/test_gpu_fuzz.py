@@ -218,3 +218,47 @@ def test_random_batch_global_threshold_mode(wc, ctx, oracle, seed):
         for i, b in enumerate(b32):
             a = int(O_[i])
             assert P[a:a + 20 + 8 * int(K[i])].tobytes() == oracle.compress_payload_thresh(b, t), (seed, q, i, dims[i])
+
+
+@pytest.mark.parametrize("seed", range(_N or 3))
+def test_random_batch_host_entry_points(wc, ctx, oracle, seed):
+    """The random batches through the host-buffer entry points (PCIe-inclusive;
+    include/wavelet_amd.h wc_forward_host, wc_forward_host_units,
+    wc_round_trip_host, wc_inverse_host) with a random pipelined unit-run size
+    (WC_OPT_HOST_CHUNK: one run, or runs of 2^14 .. 2^25 cells): densely packed
+    payloads equal to the oracle's compress() minus xz, reconstructions equal to
+    its decompress(), RMSEs within the summation-order bound."""
+    boxes, dims, offs, extent, dtype, keep = _batch(oracle, 40 + seed)
+    units, n, ext = wc.capi.make_units(dims, offsets=offs)
+    host = np.zeros(max(extent, 1), dtype)
+    for o, b in zip(offs, boxes):
+        host[o:o + b.size] = b.ravel().astype(dtype)
+    chunk = int(np.random.default_rng(seed).choice([0, 1 << 14, 1 << 18, 1 << 21, 1 << 25]))
+    before = ctx.get_option(wc.capi.WC_OPT_HOST_CHUNK)
+    ctx.set_option(wc.capi.WC_OPT_HOST_CHUNK, chunk)
+    try:
+        pay, po, kept = ctx.forward_host(host, units, n, keep)
+        pay_u, po_u, kept_u = ctx.forward_host_units([host[o:o + b.size] for o, b in zip(offs, boxes)], units, n,
+                                                     keep)
+        pay_r, po_r, kept_r, rmse = ctx.round_trip_host(host, units, n, keep)
+        regen = ctx.inverse_host(pay, po, units, n, extent)
+    finally:
+        ctx.set_option(wc.capi.WC_OPT_HOST_CHUNK, before)
+    for i, b in enumerate(boxes):
+        b32 = oracle.narrow(b) if dtype == np.float64 else b.astype(np.float32)
+        want, wk = oracle.compress_payload(b32, keep)
+        for tag, (p, o, k) in (("forward_host", (pay, po, kept)), ("forward_host_units", (pay_u, po_u, kept_u)),
+                               ("round_trip_host", (pay_r, po_r, kept_r))):
+            assert wc.capi.unit_payload(p, o, k, i) == want and int(k[i]) == wk, (seed, chunk, i, dims[i], tag)
+        if b.size == 0:
+            continue
+        back = oracle.decompress_payload(want).ravel()
+        assert regen[offs[i]:offs[i] + b.size].tobytes() == back.tobytes(), (seed, chunk, i, dims[i], "inverse_host")
+        ref = oracle.rmse(b32, back.reshape(b32.shape))
+        if np.isnan(ref):
+            assert np.isnan(rmse[i]), (seed, i, rmse[i])
+        elif np.isinf(ref):
+            assert rmse[i] == ref, (seed, i, rmse[i], ref)
+        else:
+            tol = max(1e-12, (b.size + 4) * 2.0 ** -53)
+            assert abs(rmse[i] - ref) <= tol * abs(ref), (seed, chunk, i, dims[i], rmse[i], ref)
