@@ -1,0 +1,157 @@
+// test_mirror_fuzz.cpp — seeded random boxes through the C++ mirror of the
+// reference API (include/wavelet_amd/*.h -> libwavelet_amd_host.so -> GPU),
+// checked against the CPU oracle (oracle/wc_oracle.c, linked into this test
+// binary only: test infrastructure).
+//
+// Per seed: a multiBox3D of 1-4 components with random dims (odd and even,
+// thin and cubic, up to 64 per axis), random fields per component (smooth,
+// wide-range Gaussian, constants of either sign, zeros, subnormals, NaN / inf
+// sprinkled in), a random float32 keep (src/argparse.h:13), random
+// (time, level, box, component index) file names.  Then:
+//   * compress() (src/compressor.cpp:192-297): every returned CompressedWavelet
+//     (shape, coeff_shape, (run, value) pairs bit for bit) = the oracle's
+//     transform + threshold + RLE of that component, and its .xz file exists
+//     under the reference's name (:250-254);
+//   * decompress() of each file (src/decompressor.cpp:238-255) = the oracle's
+//     rle_decode + inverse_wavelet_decompose, bit for bit;
+//   * calc_rmse_per_box (src/calc-loss.cpp:12-43) of the decoded boxes = the
+//     oracle's within (n + 4) 2^-53 relative (the mirror's RMSE runs on the
+//     GPU: the same exact double terms summed in another order);
+//   * compress() leaves its input boxes unchanged (the reference clones them,
+//     src/compressor.cpp:206).
+// usage: test_mirror_fuzz [seeds=20] [first_seed=0]
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <filesystem>
+#include <random>
+#include <string>
+#include <unistd.h>
+#include <vector>
+
+#include "../../oracle/wc_oracle.h"
+#include "wavelet_amd/calc-loss.h"
+#include "wavelet_amd/compressor.h"
+#include "wavelet_amd/decompressor.h"
+
+static int g_checks = 0;
+#define REQUIRE(cond, ...)                                                              \
+    do {                                                                                \
+        ++g_checks;                                                                     \
+        if (!(cond)) {                                                                  \
+            std::fprintf(stderr, "FAILED %s:%d: %s | ", __FILE__, __LINE__, #cond);     \
+            std::fprintf(stderr, __VA_ARGS__);                                          \
+            std::fprintf(stderr, "\n");                                                 \
+            std::exit(1);                                                               \
+        }                                                                               \
+    } while (0)
+
+static const int kSizes[] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 15, 16, 17, 24, 31, 32, 33, 40, 48, 63, 64};
+
+static Box3D make_field(std::mt19937_64& g, int W, int H, int D) {
+    Box3D b(W, H, D, 0.0f);
+    std::uniform_real_distribution<double> u(0.0, 1.0);
+    std::normal_distribution<double> n(0.0, 1.0);
+    const int kind = (int)(g() % 7);
+    const double scale = std::pow(10.0, -30.0 + 60.0 * u(g));
+    const double cst = (g() & 1 ? 1.0 : -1.0) * (0.1 + 1000.0 * u(g));
+    const double ph = 6.28 * u(g);
+    b.iterate([&](float& v, int x, int y, int z) {
+        switch (kind) {
+            case 0: v = (float)(300.0 + 50.0 * std::sin(0.1 * x + ph) * std::cos(0.07 * y) + 0.01 * z + 0.05 * n(g)); break;
+            case 1: v = (float)(n(g) * scale); break;
+            case 2: v = (float)cst; break;
+            case 3: v = 0.0f; break;
+            case 4: v = (float)(n(g) * 1e-41); break;
+            default: v = (float)(n(g) * 100.0); break;
+        }
+    });
+    if (kind >= 5) {  // specials sprinkled in
+        const float sp[] = {NAN, INFINITY, -INFINITY, 0.0f, -0.0f};
+        for (float s : sp)
+            if (g() & 1) b.set(g() % W, g() % H, g() % D, s);
+    }
+    return b;
+}
+
+static void check_seed(int seed, const std::filesystem::path& dir) {
+    std::mt19937_64 g(0x5eed0000ull + (uint64_t)seed);
+    const int W = kSizes[g() % 21], H = kSizes[g() % 21], D = kSizes[g() % 21];
+    const int ncomp = 1 + (int)(g() % 4);
+    multiBox3D mb;
+    std::vector<int> comps;
+    for (int c = 0; c < ncomp; ++c) {
+        mb.push_back(make_field(g, W, H, D));
+        comps.push_back((int)(g() % 40));
+        for (int k = 0; k < c; ++k)  // distinct names: one file per component
+            if (comps[k] == comps[c]) comps[c] += 40;
+    }
+    const float keeps[] = {0.5f, 0.99f, 0.999f, 0.9999f, 0.0f, 1.0f, 1.5f};
+    const float keepf = (g() & 3) ? keeps[g() % 7] : (float)std::uniform_real_distribution<double>(0.5, 1.0)(g);
+    const double keep = (double)keepf;
+    const int t = (int)(g() % 10), lev = (int)(g() % 4), box = (int)(g() % 1000);
+    std::vector<Box3D> inputs;
+    for (auto& b : mb) inputs.push_back(b.clone());
+
+    const auto cws = compress(mb, comps, keep, t, lev, box, dir.string());
+    REQUIRE((int)cws.size() == ncomp, "seed %d", seed);
+    const int64_t n = (int64_t)W * H * D;
+    std::vector<uint8_t> want(wco_serialized_size(n));
+    std::vector<float> flat(n), back(n);
+    multiBox3D decoded, originals;
+    for (int c = 0; c < ncomp; ++c) {
+        REQUIRE(std::memcmp(mb[c].data(), inputs[c].data(), sizeof(float) * (size_t)W * H * D) == 0,
+                "seed %d comp %d: compress() changed its input", seed, c);
+        int64_t kept = 0;
+        const size_t len = wco_compress_payload(inputs[c].data(), W, H, D, keep, want.data(), &kept);
+        const CompressedWavelet& cw = cws[c];
+        REQUIRE((cw.shape == std::vector<int>{W, H, D}) && (cw.coeff_shape == std::vector<int>{(int)n}),
+                "seed %d comp %d", seed, c);
+        REQUIRE((int64_t)cw.rle_encoded.size() == kept, "seed %d comp %d dims %dx%dx%d keep %.9g: %zu vs %lld pairs",
+                seed, c, W, H, D, keep, cw.rle_encoded.size(), (long long)kept);
+        for (int64_t k = 0; k < kept; ++k) {
+            int32_t run;
+            float val;
+            std::memcpy(&run, want.data() + 20 + 8 * k, 4);
+            std::memcpy(&val, want.data() + 24 + 8 * k, 4);
+            REQUIRE(cw.rle_encoded[k].first == run && std::memcmp(&cw.rle_encoded[k].second, &val, 4) == 0,
+                    "seed %d comp %d pair %lld", seed, c, (long long)k);
+        }
+        const std::string name = "compressed-wavelet-" + std::to_string(t) + "-" + std::to_string(lev) + "-" +
+                                 std::to_string(comps[c]) + "-" + std::to_string(box) + ".xz";
+        REQUIRE(std::filesystem::exists(dir / name), "seed %d: %s", seed, name.c_str());
+        Box3D r = decompress((dir / name).string(), t, lev, comps[c], box);
+        REQUIRE(r.width() == (size_t)W && r.height() == (size_t)H && r.depth() == (size_t)D, "seed %d", seed);
+        REQUIRE(wco_payload_to_flat(want.data(), len, flat.data(), n) == 0, "seed %d", seed);
+        wco_inverse_wavelet_decompose(flat.data(), W, H, D, back.data());
+        REQUIRE(std::memcmp(r.data(), back.data(), sizeof(float) * n) == 0, "seed %d comp %d dims %dx%dx%d", seed, c,
+                W, H, D);
+        decoded.push_back(std::move(r));
+        originals.push_back(inputs[c].clone());
+    }
+    const std::vector<double> rm = calc_rmse_per_box(decoded, originals, ncomp);
+    for (int c = 0; c < ncomp; ++c) {
+        const double ref = wco_rmse(decoded[c].data(), originals[c].data(), W, H, D);
+        const double tol = std::max(1e-12, (double)(n + 4) * std::ldexp(1.0, -53));
+        const bool ok = std::isnan(ref) ? std::isnan(rm[c])
+                        : std::isinf(ref) ? rm[c] == ref
+                                          : std::fabs(rm[c] - ref) <= tol * std::fabs(ref);
+        REQUIRE(ok, "seed %d comp %d rmse %.17g vs %.17g", seed, c, rm[c], ref);
+    }
+}
+
+int main(int argc, char** argv) {
+    const int seeds = argc > 1 ? std::atoi(argv[1]) : 20;
+    const int first = argc > 2 ? std::atoi(argv[2]) : 0;
+    char tmpl[] = "/tmp/wavelet_amd_mirror_fuzz.XXXXXX";
+    const char* p = mkdtemp(tmpl);
+    REQUIRE(p != nullptr, "mkdtemp");
+    const std::filesystem::path dir(p);
+    for (int s = first; s < first + seeds; ++s) check_seed(s, dir);
+    std::filesystem::remove_all(dir);
+    std::printf("%d seeds, %d checks passed\n", seeds, g_checks);
+    return 0;
+}

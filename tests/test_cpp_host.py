@@ -42,3 +42,20 @@ def test_reference_unit_tests_against_cpp_mirror():
     r = subprocess.run([str(TEST_BIN)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "7 cases" in r.stdout
+
+
+@pytest.mark.gpu
+def test_random_boxes_through_cpp_mirror():
+    """tests/cpp/test_mirror_fuzz.cpp: seeded random multiBox3Ds (1-4 components,
+    random dims up to 64 per axis, fields with NaN / inf / subnormals, random
+    float32 keeps) through the C++ mirror's compress() / decompress() /
+    calc_rmse_per_box against the CPU oracle compiled into that test binary:
+    the returned pairs and the decoded boxes bit for bit, the files under the
+    reference's names, the RMSE within the summation-order bound.
+    WC_MIRROR_FUZZ_SEEDS overrides the 24 seeds (a longer soak)."""
+    import os
+    seeds = os.environ.get("WC_MIRROR_FUZZ_SEEDS", "24")
+    r = subprocess.run([str(ROOT / "tools" / "bin" / "test_mirror_fuzz"), seeds], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert f"{seeds} seeds" in r.stdout
