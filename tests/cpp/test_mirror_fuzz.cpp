@@ -13,7 +13,8 @@
 //     transform + threshold + RLE of that component, and its .xz file exists
 //     under the reference's name (:250-254);
 //   * decompress() of each file (src/decompressor.cpp:238-255) = the oracle's
-//     rle_decode + inverse_wavelet_decompose, bit for bit;
+//     rle_decode + inverse_wavelet_decompose, bit for bit (a NaN matches any
+//     NaN: IEEE 754 does not specify a NaN result's sign or payload);
 //   * calc_rmse_per_box (src/calc-loss.cpp:12-43) of the decoded boxes = the
 //     oracle's within (n + 4) 2^-53 relative (the mirror's RMSE runs on the
 //     GPU: the same exact double terms summed in another order);
@@ -127,8 +128,25 @@ static void check_seed(int seed, const std::filesystem::path& dir) {
         REQUIRE(r.width() == (size_t)W && r.height() == (size_t)H && r.depth() == (size_t)D, "seed %d", seed);
         REQUIRE(wco_payload_to_flat(want.data(), len, flat.data(), n) == 0, "seed %d", seed);
         wco_inverse_wavelet_decompose(flat.data(), W, H, D, back.data());
-        REQUIRE(std::memcmp(r.data(), back.data(), sizeof(float) * n) == 0, "seed %d comp %d dims %dx%dx%d", seed, c,
-                W, H, D);
+        // bit for bit, except that a NaN matches any NaN: IEEE 754 leaves the sign and payload
+        // of a NaN result unspecified and the reference's own depend on its compiler (operand
+        // order of its double additions; DESIGN.md "Numerics")
+        auto same = [](float x, float y) { return (std::isnan(x) && std::isnan(y)) || std::memcmp(&x, &y, 4) == 0; };
+        int64_t bad = 0, first = -1;
+        for (int64_t i = 0; i < n; ++i)
+            if (!same(r.data()[i], back.data()[i])) {
+                if (first < 0) first = i;
+                ++bad;
+            }
+        if (bad) {
+            uint32_t gb, ob;
+            std::memcpy(&gb, r.data() + first, 4);
+            std::memcpy(&ob, back.data() + first, 4);
+            REQUIRE(false, "seed %d comp %d dims %dx%dx%d keep %.9g kept %lld: %lld cells differ, first (x %lld, y %lld, "
+                    "z %lld): got %08x (%.9g) want %08x (%.9g)", seed, c, W, H, D, keep, (long long)kept,
+                    (long long)bad, (long long)(first % W), (long long)(first / W % H), (long long)(first / W / H),
+                    gb, r.data()[first], ob, back.data()[first]);
+        }
         decoded.push_back(std::move(r));
         originals.push_back(inputs[c].clone());
     }
