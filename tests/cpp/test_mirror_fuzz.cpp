@@ -4,7 +4,7 @@
 // binary only: test infrastructure).
 //
 // Per seed: a multiBox3D of 1-4 components with random dims (odd and even,
-// thin and cubic, up to 64 per axis), random fields per component (smooth,
+// thin and cubic, up to 64 per axis; WC_MIRROR_FUZZ_LARGE=1: one seed in ten 64-128), random fields per component (smooth,
 // wide-range Gaussian, constants of either sign, zeros, subnormals, NaN / inf
 // sprinkled in), a random float32 keep (src/argparse.h:13), random
 // (time, level, box, component index) file names.  Then:
@@ -20,7 +20,8 @@
 //     GPU: the same exact double terms summed in another order);
 //   * compress() leaves its input boxes unchanged (the reference clones them,
 //     src/compressor.cpp:206).
-// usage: test_mirror_fuzz [seeds=20] [first_seed=0]
+// usage: test_mirror_fuzz [seeds=20] [first_seed=0]   (WCAMD_XZ_PRESET=0 speeds a long soak: the
+// checks hold at any preset)
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -80,7 +81,13 @@ static Box3D make_field(std::mt19937_64& g, int W, int H, int D) {
 
 static void check_seed(int seed, const std::filesystem::path& dir) {
     std::mt19937_64 g(0x5eed0000ull + (uint64_t)seed);
-    const int W = kSizes[g() % 21], H = kSizes[g() % 21], D = kSizes[g() % 21];
+    // WC_MIRROR_FUZZ_LARGE=1: one seed in ten draws from the large shapes (the specialised and
+    // big-unit paths); off, the draws are those of the default suite
+    static const bool large_on = std::getenv("WC_MIRROR_FUZZ_LARGE") != nullptr;
+    const int kLarge[] = {64, 96, 128};
+    const bool large = large_on && g() % 10 == 0;
+    const int W = large ? kLarge[g() % 3] : kSizes[g() % 21], H = large ? kLarge[g() % 3] : kSizes[g() % 21],
+              D = large ? kLarge[g() % 3] : kSizes[g() % 21];
     const int ncomp = 1 + (int)(g() % 4);
     multiBox3D mb;
     std::vector<int> comps;
@@ -168,7 +175,13 @@ int main(int argc, char** argv) {
     const char* p = mkdtemp(tmpl);
     REQUIRE(p != nullptr, "mkdtemp");
     const std::filesystem::path dir(p);
-    for (int s = first; s < first + seeds; ++s) check_seed(s, dir);
+    for (int s = first; s < first + seeds; ++s) {
+        check_seed(s, dir);
+        if ((s - first + 1) % 100 == 0) {  // progress for long soaks
+            std::printf("%d seeds done\n", s - first + 1);
+            std::fflush(stdout);
+        }
+    }
     std::filesystem::remove_all(dir);
     std::printf("%d seeds, %d checks passed\n", seeds, g_checks);
     return 0;
